@@ -1,0 +1,193 @@
+#!/usr/bin/env python3
+"""DSGD throughput bench: SGD rating updates/s at rank 128 on the Netflix-shaped synthetic.
+
+One step = one DSGD epoch (numBlocks supersteps, DSGDforMF.scala:341-344) over the training
+split, fast f32 mode, factors and rating blocks resident in HBM before timing starts.
+
+    python bench.py [--gpus N --steps K --warmup W] [--config NFLX|ML20M|...] [--mode fast|det]
+
+N > 1 is launched by torch.distributed.run (one process per GPU).  Each rank owns
+numBlocks/N user blocks; item blocks rotate between ranks over RCCL inside libmfhip
+(mf_create_rank).  torch.distributed (gloo) carries only the control plane: the RCCL
+unique id, the barriers around the timed region and the max/sum reductions.
+
+Prints ONE JSON line on rank 0 with the contract fields plus "roofline" (dominant kernel,
+HIP-event timed over the timed region) and "cpu_baseline" (oracle/ C restatement of the
+reference, rank 0 at N=1 only, on a bounded sample of the same workload).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "large-scale-recommendation_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=9)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="NFLX")
+    ap.add_argument("--mode", default="fast", choices=["fast", "det"])
+    ap.add_argument("--scale", type=float, default=1.0, help="shrink the synthetic (tests only)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-supersteps", type=int, default=-1, help="oracle sample size (default: 1 epoch)")
+    ap.add_argument("--fast-waves", type=int, default=0)
+    ap.add_argument("--traffic-json", default=None, help="rocprof PMC summary to fill roofline.traffic")
+    ap.add_argument("--no-profile", action="store_true", help="time without per-launch HIP events")
+    return ap.parse_args()
+
+
+class Dist:
+    """Control plane over torch.distributed (gloo); a no-op at world size 1."""
+
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", str(self.rank)))
+        self.dist = None
+        if self.world > 1:
+            import torch.distributed as dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def bcast_bytes(self, b: bytes | None) -> bytes:
+        if not self.dist:
+            return b
+        obj = [b]
+        self.dist.broadcast_object_list(obj, src=0)
+        return obj[0]
+
+    def reduce(self, x: float, op: str) -> float:
+        if not self.dist:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX if op == "max" else self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def cpu_baseline(tu, ti, tr, k, nb, supersteps):
+    """Oracle C restatement (f64, exact reference order), one thread per block of a stratum."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import coracle  # checker / baseline only
+    cores = min(nb, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), os.cpu_count() or 1)
+    m = coracle.dsgd_fit(tu, ti, tr, k=k, iterations=10, n_blocks=nb, seed=0, threads=cores,
+                         max_supersteps=supersteps)
+    v = m.updates / m.sweep_seconds if m.sweep_seconds > 0 else 0.0
+    m.close()
+    return {"value": v, "unit": "updates/s", "cores": cores, "kind": "port",
+            "sample": f"{supersteps} superstep(s) of the training split ({m.updates} f64 updates, k={k}, "
+                      f"n={nb}), oracle/mf_oracle.c, one thread per active block",
+            "seconds": m.sweep_seconds}
+
+
+def main():
+    a = parse()
+    D = Dist()
+    import numpy as np
+    import mfhip
+    from mfhip import _lib as L
+    from mfhip import synth
+
+    nu, ni, nr, k, nb = synth.CONFIGS[a.config]
+    t0 = time.time()
+    data = synth.generate(max(1, int(nu * a.scale)), max(1, int(ni * a.scale)), max(1, int(nr * a.scale)))
+    (tu, ti, tr), (eu, ei, er) = data.split()
+    t_gen = time.time() - t0
+
+    p = L.default_params()
+    p.num_factors, p.num_blocks, p.seed, p.has_seed = k, nb, 0, 1
+    p.iterations = a.warmup + a.steps
+    p.mode = L.MODE_FAST_F32 if a.mode == "fast" else L.MODE_DETERMINISTIC_F64
+    p.fast_waves = a.fast_waves
+    if D.world > 1:
+        uid = D.bcast_bytes(mfhip.Context.unique_id() if D.rank == 0 else None)
+        ctx = mfhip.Context(p, rank=(D.local_rank, D.world, D.rank, uid))
+    else:
+        ctx = mfhip.Context(p)
+    t0 = time.time()
+    ctx.prepare(tu, ti, tr)
+    ctx.sync()
+    t_prep = time.time() - t0
+
+    ctx.run(a.warmup * nb)
+    ctx.sync()
+    ctx.reset_stats()
+    ctx.set_profiling(not a.no_profile)
+    import torch
+    have_torch_gpu = torch.cuda.is_available()
+    D.barrier()
+    if have_torch_gpu:
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ctx.run(a.steps * nb)
+    ctx.sync()
+    if have_torch_gpu:
+        torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    D.barrier()
+    st = ctx.stats()
+    elapsed = D.reduce(t1 - t0, "max")
+    updates = D.reduce(float(st["updates"]), "sum")
+    kernel_ms = D.reduce(st["kernel_ms"], "max")
+    launches = st["kernel_launches"]
+    alg_bytes_local = st["algorithmic_bytes"]
+    rmse, matched = ctx.rmse(eu, ei, er)
+
+    value = updates / elapsed
+    bpu = 16 * k + 20 if a.mode == "fast" else 32 * k + 24
+    roof = None
+    if st["kernel_ms"] > 0:
+        achieved = alg_bytes_local / (st["kernel_ms"] / 1e3) / 1e9  # GB/s, this rank's dominant kernel
+        traffic = None
+        if a.traffic_json and os.path.exists(a.traffic_json):
+            traffic = json.load(open(a.traffic_json)).get("bytes_per_launch")
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "kernel": "k_fast_substep" if a.mode == "fast" else "k_level",
+                "bytes_per_update": bpu, "avg_launch_us": round(st["kernel_ms"] * 1e3 / max(launches, 1), 2),
+                "launches": launches}
+
+    cpu = None
+    if D.rank == 0 and D.world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(tu, ti, tr, k, nb, a.cpu_supersteps if a.cpu_supersteps > 0 else nb)
+
+    if D.rank == 0:
+        out = {
+            "metric": "SGD rating updates/sec (node) at rank 128; RMSE after 10 epochs",
+            "value": round(value, 1), "unit": "updates/s", "n_gpus": D.world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(elapsed * 1e3 / max(a.steps, 1), 3),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": "f32" if a.mode == "fast" else "f64", "data": "synthetic (SURVEY.md 8d generator, seeds 42/1234/7)",
+            "config": {"workload": f"{a.config}-shaped DSGD {'fast' if a.mode == 'fast' else 'deterministic'}",
+                       "users": int(nu * a.scale), "items": int(ni * a.scale), "ratings": int(nr * a.scale),
+                       "train_ratings": int(len(tr)), "rank": k, "num_blocks": nb, "lambda": 1.0, "lr": 0.001,
+                       "lr_method": "Default", "groups": st["groups"], "parallelism": f"dsgd-ring{D.world}"},
+            "rmse": round(rmse, 6), "rmse_epochs": a.warmup + a.steps, "rmse_matched": matched,
+            "roofline": roof, "cpu_baseline": cpu,
+            "setup_s": {"generate": round(t_gen, 2), "prepare": round(t_prep, 2)},
+        }
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    D.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,139 @@
+// common.hpp -- status/error plumbing, device buffers and a small host thread pool.
+#pragma once
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdlib>
+#include <functional>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "mfhip.h"
+
+namespace mfhip {
+
+// Every API entry point catches this and converts it to a status + mf_last_error().
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+[[noreturn]] inline void fail(int code, const std::string& msg) { throw Error(code, msg); }
+
+#define MF_HIP(call)                                                                        \
+  do {                                                                                      \
+    hipError_t _e = (call);                                                                 \
+    if (_e != hipSuccess)                                                                   \
+      ::mfhip::fail(MF_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(_e) + " at " + \
+                                    __FILE__ + ":" + std::to_string(__LINE__));             \
+  } while (0)
+
+#define MF_REQUIRE(cond, msg) \
+  do {                        \
+    if (!(cond)) ::mfhip::fail(MF_ERR_INVALID, (msg)); \
+  } while (0)
+
+// Owning device allocation on the current device.
+class DevBuf {
+ public:
+  DevBuf() = default;
+  ~DevBuf() { release(); }
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  DevBuf(DevBuf&& o) noexcept : p_(o.p_), bytes_(o.bytes_) { o.p_ = nullptr; o.bytes_ = 0; }
+  DevBuf& operator=(DevBuf&& o) noexcept {
+    if (this != &o) { release(); p_ = o.p_; bytes_ = o.bytes_; o.p_ = nullptr; o.bytes_ = 0; }
+    return *this;
+  }
+  void alloc(size_t bytes) {
+    if (bytes <= bytes_ && p_) return;
+    release();
+    if (bytes == 0) return;
+    MF_HIP(hipMalloc(&p_, bytes));
+    bytes_ = bytes;
+  }
+  void release() {
+    if (p_) (void)hipFree(p_);
+    p_ = nullptr;
+    bytes_ = 0;
+  }
+  template <typename T> T* as() const { return static_cast<T*>(p_); }
+  void* get() const { return p_; }
+  size_t bytes() const { return bytes_; }
+
+ private:
+  void* p_ = nullptr;
+  size_t bytes_ = 0;
+};
+
+// Pinned host staging buffer.
+class PinnedBuf {
+ public:
+  PinnedBuf() = default;
+  ~PinnedBuf() { if (p_) (void)hipHostFree(p_); }
+  PinnedBuf(const PinnedBuf&) = delete;
+  PinnedBuf& operator=(const PinnedBuf&) = delete;
+  void alloc(size_t bytes) {
+    if (bytes <= bytes_ && p_) return;
+    if (p_) (void)hipHostFree(p_);
+    p_ = nullptr;
+    bytes_ = 0;
+    if (bytes == 0) return;
+    MF_HIP(hipHostMalloc(&p_, bytes, hipHostMallocDefault));
+    bytes_ = bytes;
+  }
+  template <typename T> T* as() const { return static_cast<T*>(p_); }
+  size_t bytes() const { return bytes_; }
+
+ private:
+  void* p_ = nullptr;
+  size_t bytes_ = 0;
+};
+
+// Host worker count: OMP_NUM_THREADS / MFHIP_THREADS if set (the GPU box exports 16),
+// else hardware_concurrency, capped at 32.
+inline int host_threads() {
+  for (const char* v : {"MFHIP_THREADS", "OMP_NUM_THREADS"}) {
+    if (const char* s = std::getenv(v)) {
+      int t = std::atoi(s);
+      if (t > 0) return std::min(t, 64);
+    }
+  }
+  unsigned hc = std::thread::hardware_concurrency();
+  return static_cast<int>(std::max(1u, std::min(hc, 32u)));
+}
+
+// parallel_for over [0, n) in contiguous chunks; fn(begin, end, worker).
+inline void parallel_for(int64_t n, const std::function<void(int64_t, int64_t, int)>& fn,
+                         int max_workers = 0, int64_t min_chunk = 1 << 14) {
+  if (n <= 0) return;
+  int w = max_workers > 0 ? max_workers : host_threads();
+  w = static_cast<int>(std::min<int64_t>(w, (n + min_chunk - 1) / min_chunk));
+  if (w <= 1) { fn(0, n, 0); return; }
+  std::vector<std::thread> th;
+  th.reserve(w);
+  const int64_t chunk = (n + w - 1) / w;
+  for (int t = 0; t < w; ++t) {
+    int64_t b = t * chunk, e = std::min(n, b + chunk);
+    if (b >= e) break;
+    th.emplace_back(fn, b, e, t);
+  }
+  for (auto& x : th) x.join();
+}
+
+// parallel over independent tasks 0..n-1 (dynamic: task t -> worker t % w).
+inline void parallel_tasks(int64_t n, const std::function<void(int64_t)>& fn, int max_workers = 0) {
+  if (n <= 0) return;
+  int w = max_workers > 0 ? max_workers : host_threads();
+  w = static_cast<int>(std::min<int64_t>(w, n));
+  if (w <= 1) { for (int64_t t = 0; t < n; ++t) fn(t); return; }
+  std::vector<std::thread> th;
+  for (int t = 0; t < w; ++t)
+    th.emplace_back([&, t] { for (int64_t x = t; x < n; x += w) fn(x); });
+  for (auto& x : th) x.join();
+}
+
+}  // namespace mfhip

@@ -1,0 +1,42 @@
+// kernels.hpp -- host-side launch wrappers of the HIP kernels (kernels_det.hip, kernels_fast.hip,
+// kernels_eval.hip).  All launches are asynchronous on the given stream.
+#pragma once
+#include <hip/hip_runtime_api.h>
+
+#include <cstdint>
+
+#include "plan.hpp"
+
+namespace mfhip {
+
+// Update arithmetic of one replayed rating.
+enum class Arith : int {
+  kDsgd = 0,     // DSGDforMF.updateLocalFactors body (:405-413), regularised
+  kSgdNext = 1,  // SGDUpdater.nextFactors (core/FactorUpdater.scala:37-45)
+};
+
+// Deterministic replay of one dependency level: one wave per entry, sequential dot.
+// T = double (bit-exact) or float (fast-mode online).  eta = learning rate of the superstep
+// (kDsgd) or SGDUpdater's learningRate (kSgdNext).
+void launch_level(hipStream_t st, const DetEntry* entries, int64_t n, void* U, void* I,
+                  const void* regU, const void* regI, int k, double eta, Arith arith, bool f64);
+
+// Fast-mode sweep, one rotation sub-step t for nblk rating blocks of one superstep.
+struct FastBlk {
+  int64_t rec_base;   // first record of the rating block
+  int64_t cell_base;  // its G*G+1 cell offsets in the cell table
+};
+void launch_fast_substep(hipStream_t st, const FastBlk* blks, int nblk, int G, int t,
+                         const FastRec* recs, const int32_t* cell_off, float* U, float* I,
+                         const float* regI, int k, float eta);
+
+// Gather-dot over resolved pairs (row -1 = unknown id).  out[j] = p.q summed left to right in
+// f64 (predictRating's ddot).  When r != nullptr every workgroup writes partials[3*wg + c]:
+//   c=0: sum (r - p.q)^2, c=1: matched count, c=2: sum mult*((r-p.q)^2 + lambda*(p.p + q.q)).
+// The grid has predict_grid(n) workgroups; the host adds the partials in a fixed order.
+int predict_grid(int64_t n);
+void launch_predict(hipStream_t st, const int32_t* urow, const int32_t* irow, int64_t n,
+                    const void* U, const void* I, int k, bool f64, double* out, const double* r,
+                    const int32_t* mult, double lambda, double* partials);
+
+}  // namespace mfhip

@@ -1,0 +1,196 @@
+// kernels_det.hip -- bit-exact f64 kernels.  Compiled with -ffp-contract=off: every a*b+c
+// stays two rounded operations, as on the JVM.
+//
+//  k_level    one dependency level of a replayed sequential order (DSGDforMF.scala:395-414
+//             or SGDUpdater.nextFactors, core/FactorUpdater.scala:37-45).  One wave per
+//             rating; a level never holds two ratings that share a row, so the updates of a
+//             level commute and the level-by-level replay equals the sequential loop.
+//  k_predict  predictRating / RMSE / empiricalRisk gathers (MatrixFactorization.scala:133-274).
+//
+// Roofline: both are HBM/L2 row gathers (B_f64(k) = 32k+24 bytes per update); the dot
+// product is summed left to right (netlib F2jBLAS.ddot order) with v_readlane broadcasts,
+// a k-long dependent f64 add chain per wave, so the deterministic path is latency-bound by
+// design; the fast path (kernels_fast.hip) is the throughput path.
+#include <hip/hip_runtime.h>
+
+#include "kernels.hpp"
+
+namespace mfhip {
+namespace {
+
+__device__ __forceinline__ double readlane(double v, int l) {
+  const unsigned long long b = static_cast<unsigned long long>(__double_as_longlong(v));
+  const unsigned lo = static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(b & 0xffffffffu), l));
+  const unsigned hi = static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(b >> 32), l));
+  return __longlong_as_double(static_cast<long long>((static_cast<unsigned long long>(hi) << 32) | lo));
+}
+__device__ __forceinline__ float readlane(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+// Sequential dot over f = 0..k-1 where lane l holds element l + 64c in prod[c]:
+// acc = ((0 + x0) + x1) + ... exactly as F2jBLAS.ddot / Scala's foldLeft sum.
+template <typename T, int KPL>
+__device__ __forceinline__ T seq_dot(const T (&prod)[KPL], int k) {
+  T acc = T(0);
+#pragma unroll
+  for (int c = 0; c < KPL; ++c) {
+    const int lim = min(64, k - 64 * c);
+    for (int l = 0; l < lim; ++l) acc = acc + readlane(prod[c], l);
+  }
+  return acc;
+}
+
+template <typename T, int KPL, int ARITH>
+__global__ __launch_bounds__(256) void k_level(const DetEntry* __restrict__ ent, int64_t n,
+                                               T* __restrict__ U, T* __restrict__ I,
+                                               const T* __restrict__ regU, const T* __restrict__ regI,
+                                               int k, T eta) {
+  const int lane = threadIdx.x & 63;
+  const int64_t j = static_cast<int64_t>(blockIdx.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (j >= n) return;
+  const uint32_t ur = ent[j].u, ir = ent[j].i;
+  const T r = static_cast<T>(ent[j].r);
+  T* p = U + static_cast<size_t>(ur) * k;
+  T* q = I + static_cast<size_t>(ir) * k;
+  T pv[KPL], qv[KPL], pr[KPL];
+#pragma unroll
+  for (int c = 0; c < KPL; ++c) {
+    const int f = lane + 64 * c;
+    pv[c] = f < k ? p[f] : T(0);
+    qv[c] = f < k ? q[f] : T(0);
+    pr[c] = pv[c] * qv[c];
+  }
+  const T e = r - seq_dot<T, KPL>(pr, k);
+  if constexpr (ARITH == static_cast<int>(Arith::kDsgd)) {
+    const T ru = regU[ur], ri = regI[ir];  // lambda / omega, as `lambda / omegai * p` (:408)
+#pragma unroll
+    for (int c = 0; c < KPL; ++c) {
+      const int f = lane + 64 * c;
+      if (f < k) {
+        p[f] = pv[c] - eta * (ru * pv[c] - e * qv[c]);
+        q[f] = qv[c] - eta * (ri * qv[c] - e * pv[c]);
+      }
+    }
+  } else {
+    const T le = eta * e;  // learningRate * e * i == (learningRate * e) * i
+#pragma unroll
+    for (int c = 0; c < KPL; ++c) {
+      const int f = lane + 64 * c;
+      if (f < k) {
+        p[f] = pv[c] + le * qv[c];
+        q[f] = qv[c] + le * pv[c];
+      }
+    }
+  }
+}
+
+template <typename T, int KPL>
+__global__ __launch_bounds__(256) void k_predict(const int32_t* __restrict__ urow,
+                                                 const int32_t* __restrict__ irow, int64_t n,
+                                                 const T* __restrict__ U, const T* __restrict__ I,
+                                                 int k, double* __restrict__ out,
+                                                 const double* __restrict__ r,
+                                                 const int32_t* __restrict__ mult, double lambda,
+                                                 double* __restrict__ partials) {
+  __shared__ double red[4][3];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t nwaves = static_cast<int64_t>(gridDim.x) * 4;
+  double sse = 0.0, cnt = 0.0, risk = 0.0;
+  for (int64_t j = static_cast<int64_t>(blockIdx.x) * 4 + wave; j < n; j += nwaves) {
+    const int32_t ur = urow[j], ir = irow[j];
+    if (ur < 0 || ir < 0) {
+      if (out && lane == 0) out[j] = 0.0;
+      continue;
+    }
+    const T* p = U + static_cast<size_t>(ur) * k;
+    const T* q = I + static_cast<size_t>(ir) * k;
+    double pq[KPL], pp[KPL], qq[KPL];
+#pragma unroll
+    for (int c = 0; c < KPL; ++c) {
+      const int f = lane + 64 * c;
+      const double a = f < k ? static_cast<double>(p[f]) : 0.0;
+      const double b = f < k ? static_cast<double>(q[f]) : 0.0;
+      pq[c] = a * b;
+      pp[c] = a * a;
+      qq[c] = b * b;
+    }
+    const double pred = seq_dot<double, KPL>(pq, k);
+    if (out && lane == 0) out[j] = pred;
+    if (r) {
+      const double d = r[j] - pred;
+      sse += d * d;
+      cnt += 1.0;
+      if (mult) {
+        const double term = d * d + lambda * (seq_dot<double, KPL>(pp, k) + seq_dot<double, KPL>(qq, k));
+        for (int m = 0; m < mult[j]; ++m) risk += term;
+      }
+    }
+  }
+  if (!partials) return;
+  if (lane == 0) { red[wave][0] = sse; red[wave][1] = cnt; red[wave][2] = risk; }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    const double s = ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+    partials[static_cast<size_t>(blockIdx.x) * 3 + threadIdx.x] = s;
+  }
+}
+
+template <typename T, int ARITH>
+void level_dispatch(hipStream_t st, const DetEntry* e, int64_t n, void* U, void* I, const void* rU,
+                    const void* rI, int k, double eta) {
+  const dim3 grid(static_cast<unsigned>((n + 3) / 4)), block(256);
+  T* u = static_cast<T*>(U);
+  T* i = static_cast<T*>(I);
+  const T* ru = static_cast<const T*>(rU);
+  const T* ri = static_cast<const T*>(rI);
+  const T et = static_cast<T>(eta);
+  if (k <= 64) hipLaunchKernelGGL((k_level<T, 1, ARITH>), grid, block, 0, st, e, n, u, i, ru, ri, k, et);
+  else if (k <= 128) hipLaunchKernelGGL((k_level<T, 2, ARITH>), grid, block, 0, st, e, n, u, i, ru, ri, k, et);
+  else if (k <= 256) hipLaunchKernelGGL((k_level<T, 4, ARITH>), grid, block, 0, st, e, n, u, i, ru, ri, k, et);
+  else hipLaunchKernelGGL((k_level<T, 8, ARITH>), grid, block, 0, st, e, n, u, i, ru, ri, k, et);
+}
+
+template <typename T>
+void predict_dispatch(hipStream_t st, const int32_t* ur, const int32_t* ir, int64_t n, const void* U,
+                      const void* I, int k, double* out, const double* r, const int32_t* mult,
+                      double lambda, double* partials, int grid_blocks) {
+  const dim3 grid(static_cast<unsigned>(grid_blocks)), block(256);
+  const T* u = static_cast<const T*>(U);
+  const T* i = static_cast<const T*>(I);
+  if (k <= 64) hipLaunchKernelGGL((k_predict<T, 1>), grid, block, 0, st, ur, ir, n, u, i, k, out, r, mult, lambda, partials);
+  else if (k <= 128) hipLaunchKernelGGL((k_predict<T, 2>), grid, block, 0, st, ur, ir, n, u, i, k, out, r, mult, lambda, partials);
+  else if (k <= 256) hipLaunchKernelGGL((k_predict<T, 4>), grid, block, 0, st, ur, ir, n, u, i, k, out, r, mult, lambda, partials);
+  else hipLaunchKernelGGL((k_predict<T, 8>), grid, block, 0, st, ur, ir, n, u, i, k, out, r, mult, lambda, partials);
+}
+
+}  // namespace
+
+void launch_level(hipStream_t st, const DetEntry* entries, int64_t n, void* U, void* I,
+                  const void* regU, const void* regI, int k, double eta, Arith arith, bool f64) {
+  if (n <= 0) return;
+  if (f64) {
+    if (arith == Arith::kDsgd) level_dispatch<double, 0>(st, entries, n, U, I, regU, regI, k, eta);
+    else level_dispatch<double, 1>(st, entries, n, U, I, regU, regI, k, eta);
+  } else {
+    if (arith == Arith::kDsgd) level_dispatch<float, 0>(st, entries, n, U, I, regU, regI, k, eta);
+    else level_dispatch<float, 1>(st, entries, n, U, I, regU, regI, k, eta);
+  }
+}
+
+int predict_grid(int64_t n) {
+  const int64_t g = (n + 3) / 4;
+  return static_cast<int>(g < 1 ? 1 : (g > 4096 ? 4096 : g));
+}
+
+void launch_predict(hipStream_t st, const int32_t* urow, const int32_t* irow, int64_t n,
+                    const void* U, const void* I, int k, bool f64, double* out, const double* r,
+                    const int32_t* mult, double lambda, double* partials) {
+  if (n <= 0) return;
+  const int g = predict_grid(n);
+  if (f64) predict_dispatch<double>(st, urow, irow, n, U, I, k, out, r, mult, lambda, partials, g);
+  else predict_dispatch<float>(st, urow, irow, n, U, I, k, out, r, mult, lambda, partials, g);
+}
+
+}  // namespace mfhip

@@ -1,0 +1,1273 @@
+// mfhip.cpp -- C ABI of libmfhip.so (include/mfhip.h): context, shards, DSGD driver,
+// online micro-batches, evaluation and the item-block ring between GPUs.
+//
+// Execution model:
+//  * A context owns G shards.  Shard g owns user blocks [g*c, (g+1)*c), c = numBlocks / G, and
+//    the rating blocks of those rows, resident in HBM for the whole fit.
+//  * Superstep s (1-based, DSGDforMF.scala:341-344, :476) runs rating blocks (p, (p+s-1) mod n)
+//    for the shard's p on the shard's stream; afterwards the shard hands item block
+//    (g*c + s - 1) mod n to shard g-1 and receives ((g+1)*c + s - 1) mod n from shard g+1 --
+//    the nextRatingBlock rotation (:611-619).  In-process shards use peer copies; one process
+//    per GPU (mf_create_rank) uses RCCL send/recv over xGMI.
+//  * Every shard keeps full-size factor slabs with the global row numbering, so a block moves
+//    by copying its row range; only the rows a shard currently owns are current.
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <numeric>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "common.hpp"
+#include "jvm_random.hpp"
+#include "kernels.hpp"
+#include "plan.hpp"
+
+namespace mfhip {
+
+thread_local std::string g_last_error;
+
+struct DeviceGuard {
+  int prev = 0;
+  explicit DeviceGuard(int dev) {
+    (void)hipGetDevice(&prev);
+    MF_HIP(hipSetDevice(dev));
+  }
+  ~DeviceGuard() { (void)hipSetDevice(prev); }
+};
+
+#define MF_NCCL(call)                                                                     \
+  do {                                                                                    \
+    ncclResult_t _r = (call);                                                             \
+    if (_r != ncclSuccess) ::mfhip::fail(MF_ERR_COMM, std::string(#call) + ": " + ncclGetErrorString(_r)); \
+  } while (0)
+
+struct Shard {
+  int device = 0;
+  int index = 0;  // global shard index (== rank in rank mode)
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;  // ring hand-off ordering between in-process shards
+  DevBuf uf, itf, regu, regi;
+  int64_t cap_u = 0, cap_i = 0;
+  // deterministic mode staging
+  DevBuf det_dev;
+  PinnedBuf det_pin;
+  // fast mode
+  DevBuf fast_recs, fast_cells, fast_blks;
+  // evaluation scratch
+  DevBuf ev_u, ev_i, ev_r, ev_mult, ev_out, ev_part;
+  // profiling
+  std::vector<hipEvent_t> ev;
+  size_t ev_used = 0;
+  int64_t ev_launches = 0;
+};
+
+}  // namespace mfhip
+
+struct mf_ctx {
+  mf_params P{};
+  bool f64 = true;
+  size_t es = 8;  // bytes per factor element
+  int G = 1;      // global shard count
+  bool rank_mode = false;
+  ncclComm_t comm = nullptr;
+  std::vector<mfhip::Shard> shards;  // local shards
+  mfhip::SideLayout U, I;
+  bool have_model = false;
+  bool prepared = false;
+  int32_t nb = 1;
+  int32_t c = 1;  // user blocks per shard
+  int64_t superstep_done = 0;
+  std::vector<int> item_loc;  // item block -> shard holding it
+  mfhip::RatingBlocks rb;     // deterministic mode keeps the rating blocks on the host
+  int32_t G_fast = 0;
+  std::vector<int64_t> fast_rb_size;  // per rating block (fast mode)
+  mf_stats stats{};
+  bool profiling = false;
+  std::vector<int32_t> rows_by_id_u, rows_by_id_i;  // ascending-id row permutations
+  bool order_dirty = true;
+};
+
+namespace mfhip {
+namespace {
+
+constexpr int kSideU = MF_SIDE_USER;
+
+void set_error(const std::string& m) { g_last_error = m; }
+
+template <typename F>
+int guarded(F&& f) {
+  try {
+    f();
+    return MF_OK;
+  } catch (const Error& e) {
+    set_error(e.what());
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    set_error("host allocation failed");
+    return MF_ERR_CAPACITY;
+  } catch (const std::exception& e) {
+    set_error(e.what());
+    return MF_ERR_INVALID;
+  }
+}
+
+double bytes_per_update(const mf_ctx* ctx) {
+  const double k = ctx->P.num_factors;
+  return ctx->f64 ? 32.0 * k + 24.0 : 16.0 * k + 20.0;
+}
+
+SideLayout& side_of(mf_ctx* ctx, int side) { return side == kSideU ? ctx->U : ctx->I; }
+
+void validate_params(const mf_params* p) {
+  MF_REQUIRE(p, "params is null");
+  MF_REQUIRE(p->num_factors >= 1 && p->num_factors <= 512, "num_factors must be in [1, 512]");
+  MF_REQUIRE(p->iterations >= 0, "iterations must be >= 0");
+  MF_REQUIRE(p->num_blocks >= 1, "num_blocks must be >= 1");
+  MF_REQUIRE(p->mode == MF_MODE_DETERMINISTIC_F64 || p->mode == MF_MODE_FAST_F32, "unknown mode");
+  MF_REQUIRE(p->lr_method >= MF_LR_DEFAULT && p->lr_method <= MF_LR_XU, "unknown lr_method");
+}
+
+void init_shard(Shard& s, int device, int index) {
+  s.device = device;
+  s.index = index;
+  DeviceGuard g(device);
+  MF_HIP(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+  MF_HIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+}
+
+void destroy_shard(Shard& s) {
+  if (!s.stream) return;
+  (void)hipSetDevice(s.device);
+  (void)hipStreamSynchronize(s.stream);
+  for (auto e : s.ev) (void)hipEventDestroy(e);
+  s.ev.clear();
+  (void)hipEventDestroy(s.done);
+  (void)hipStreamDestroy(s.stream);
+  s.stream = nullptr;
+}
+
+// Grow a factor slab (and its regularisation column) to hold `rows`, keeping the contents.
+void ensure_rows(mf_ctx* ctx, Shard& s, int side, int64_t rows) {
+  int64_t& cap = side == kSideU ? s.cap_u : s.cap_i;
+  if (rows <= cap) return;
+  DeviceGuard g(s.device);
+  const int64_t ncap = std::max<int64_t>({rows, cap * 2, 1024});
+  const size_t k = static_cast<size_t>(ctx->P.num_factors);
+  DevBuf f, rg;
+  f.alloc(static_cast<size_t>(ncap) * k * ctx->es);
+  rg.alloc(static_cast<size_t>(ncap) * ctx->es);
+  MF_HIP(hipMemsetAsync(rg.get(), 0, static_cast<size_t>(ncap) * ctx->es, s.stream));
+  DevBuf& of = side == kSideU ? s.uf : s.itf;
+  DevBuf& og = side == kSideU ? s.regu : s.regi;
+  if (cap > 0) {
+    MF_HIP(hipMemcpyAsync(f.get(), of.get(), static_cast<size_t>(cap) * k * ctx->es, hipMemcpyDeviceToDevice, s.stream));
+    MF_HIP(hipMemcpyAsync(rg.get(), og.get(), static_cast<size_t>(cap) * ctx->es, hipMemcpyDeviceToDevice, s.stream));
+  }
+  MF_HIP(hipStreamSynchronize(s.stream));
+  of = std::move(f);
+  og = std::move(rg);
+  cap = ncap;
+}
+
+// Host f64 rows -> device slab rows [row0, row0+n) in the context's precision.
+void upload_rows(mf_ctx* ctx, Shard& s, int side, int64_t row0, const double* src, int64_t n) {
+  if (n <= 0) return;
+  DeviceGuard g(s.device);
+  const size_t k = static_cast<size_t>(ctx->P.num_factors);
+  DevBuf& slab = side == kSideU ? s.uf : s.itf;
+  char* dst = slab.as<char>() + static_cast<size_t>(row0) * k * ctx->es;
+  if (ctx->f64) {
+    MF_HIP(hipMemcpy(dst, src, static_cast<size_t>(n) * k * 8, hipMemcpyHostToDevice));
+  } else {
+    std::vector<float> tmp(static_cast<size_t>(n) * k);
+    parallel_for(static_cast<int64_t>(tmp.size()), [&](int64_t b, int64_t e, int) {
+      for (int64_t x = b; x < e; ++x) tmp[x] = static_cast<float>(src[x]);
+    });
+    MF_HIP(hipMemcpy(dst, tmp.data(), tmp.size() * 4, hipMemcpyHostToDevice));
+  }
+}
+
+void upload_regs(mf_ctx* ctx, Shard& s, int side, int64_t row0, const double* src, int64_t n) {
+  if (n <= 0) return;
+  DeviceGuard g(s.device);
+  DevBuf& reg = side == kSideU ? s.regu : s.regi;
+  char* dst = reg.as<char>() + static_cast<size_t>(row0) * ctx->es;
+  if (ctx->f64) {
+    MF_HIP(hipMemcpy(dst, src, static_cast<size_t>(n) * 8, hipMemcpyHostToDevice));
+  } else {
+    std::vector<float> tmp(n);
+    for (int64_t x = 0; x < n; ++x) tmp[x] = static_cast<float>(src[x]);
+    MF_HIP(hipMemcpy(dst, tmp.data(), static_cast<size_t>(n) * 4, hipMemcpyHostToDevice));
+  }
+}
+
+// Device slab rows [row0, row0+n) -> host f64.
+void download_rows(mf_ctx* ctx, Shard& s, int side, int64_t row0, int64_t n, double* out) {
+  if (n <= 0) return;
+  DeviceGuard g(s.device);
+  const size_t k = static_cast<size_t>(ctx->P.num_factors);
+  DevBuf& slab = side == kSideU ? s.uf : s.itf;
+  const char* src = slab.as<char>() + static_cast<size_t>(row0) * k * ctx->es;
+  MF_HIP(hipStreamSynchronize(s.stream));
+  if (ctx->f64) {
+    MF_HIP(hipMemcpy(out, src, static_cast<size_t>(n) * k * 8, hipMemcpyDeviceToHost));
+  } else {
+    std::vector<float> tmp(static_cast<size_t>(n) * k);
+    MF_HIP(hipMemcpy(tmp.data(), src, tmp.size() * 4, hipMemcpyDeviceToHost));
+    for (size_t x = 0; x < tmp.size(); ++x) out[x] = static_cast<double>(tmp[x]);
+  }
+}
+
+// Initial factors: k x nextDouble of new Random(id ^ seed) (DSGDforMF.scala:548-549), or of
+// new Random(id) for PseudoRandomFactorInitializer (core/FactorInitializer.scala:23-27).
+void init_vectors(const int32_t* ids, int64_t n, int k, bool xor_seed, int64_t seed, std::vector<double>& out) {
+  out.resize(static_cast<size_t>(n) * k);
+  parallel_for(n, [&](int64_t b, int64_t e, int) {
+    for (int64_t x = b; x < e; ++x) {
+      JavaRandom rng(xor_seed ? (static_cast<int64_t>(ids[x]) ^ seed) : static_cast<int64_t>(ids[x]));
+      double* v = out.data() + static_cast<size_t>(x) * k;
+      for (int f = 0; f < k; ++f) v[f] = rng.nextDouble();
+    }
+  }, 0, 1024);
+}
+
+// ---------------------------------------------------------------------------------------
+// profiling: a pair of HIP events around every sweep-kernel launch on the shard's stream.
+struct LaunchTimer {
+  Shard& s;
+  bool on;
+  size_t slot = 0;
+  LaunchTimer(Shard& sh, bool enabled) : s(sh), on(enabled) {
+    if (!on) return;
+    if (s.ev_used + 2 > s.ev.size()) {
+      for (int x = 0; x < 512; ++x) {
+        hipEvent_t e;
+        MF_HIP(hipEventCreate(&e));
+        s.ev.push_back(e);
+      }
+    }
+    slot = s.ev_used;
+    s.ev_used += 2;
+    MF_HIP(hipEventRecord(s.ev[slot], s.stream));
+  }
+  ~LaunchTimer() {
+    if (on) {
+      (void)hipEventRecord(s.ev[slot + 1], s.stream);
+      s.ev_launches++;
+    }
+  }
+};
+
+void collect_profile(mf_ctx* ctx) {
+  for (auto& s : ctx->shards) {
+    if (s.ev_used == 0) continue;
+    DeviceGuard g(s.device);
+    MF_HIP(hipStreamSynchronize(s.stream));
+    double ms = 0.0;
+    for (size_t x = 0; x + 1 < s.ev_used; x += 2) {
+      float t = 0.f;
+      MF_HIP(hipEventElapsedTime(&t, s.ev[x], s.ev[x + 1]));
+      ms += t;
+    }
+    ctx->stats.kernel_ms += ms;
+    s.ev_used = 0;
+  }
+}
+
+void sync_all(mf_ctx* ctx) {
+  for (auto& s : ctx->shards) {
+    DeviceGuard g(s.device);
+    MF_HIP(hipStreamSynchronize(s.stream));
+  }
+  collect_profile(ctx);
+}
+
+// ---------------------------------------------------------------------------------------
+// Model construction for a fit.
+void build_model(mf_ctx* ctx, const int32_t* u, const int32_t* i, int64_t n) {
+  const bool seeded = ctx->P.has_seed != 0;
+  build_side(ctx->U, u, n, ctx->nb, ctx->P.seed, seeded);
+  build_side(ctx->I, i, n, ctx->nb, ctx->P.seed, seeded);
+  const int k = ctx->P.num_factors;
+  for (int side = 0; side < 2; ++side) {
+    SideLayout& S = side == kSideU ? ctx->U : ctx->I;
+    std::vector<double> vec, reg(S.rows());
+    int64_t seed = ctx->P.seed;
+    if (!seeded) {
+      std::random_device rd;
+      seed = (static_cast<int64_t>(rd()) << 32) ^ rd();
+    }
+    init_vectors(S.row_id.data(), S.rows(), k, true, seed, vec);
+    for (int64_t x = 0; x < S.rows(); ++x) reg[x] = ctx->P.lambda / static_cast<double>(S.omega[x]);
+    for (auto& s : ctx->shards) {
+      ensure_rows(ctx, s, side, std::max<int64_t>(S.rows(), 1));
+      upload_rows(ctx, s, side, 0, vec.data(), S.rows());
+      upload_regs(ctx, s, side, 0, reg.data(), S.rows());
+    }
+  }
+  ctx->have_model = true;
+  ctx->order_dirty = true;
+}
+
+void ensure_order(mf_ctx* ctx) {
+  if (!ctx->order_dirty) return;
+  for (int side = 0; side < 2; ++side) {
+    SideLayout& S = side_of(ctx, side);
+    auto& ord = side == kSideU ? ctx->rows_by_id_u : ctx->rows_by_id_i;
+    ord.resize(S.rows());
+    std::iota(ord.begin(), ord.end(), 0);
+    std::sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) { return S.row_id[a] < S.row_id[b]; });
+  }
+  ctx->order_dirty = false;
+}
+
+int shard_of_user_block(const mf_ctx* ctx, int32_t p) { return p / ctx->c; }
+
+Shard* local_shard(mf_ctx* ctx, int global) {
+  for (auto& s : ctx->shards)
+    if (s.index == global) return &s;
+  return nullptr;
+}
+
+// ---------------------------------------------------------------------------------------
+// One superstep on one shard.
+void det_superstep(mf_ctx* ctx, Shard& s, int64_t superstep, int32_t iteration, double eta) {
+  const int32_t n = ctx->nb;
+  std::vector<std::vector<int32_t>> orders;
+  std::vector<OrderedSeq> seqs;
+  std::vector<int64_t> rbids;
+  for (int32_t j = 0; j < ctx->c; ++j) {
+    const int32_t p = s.index * ctx->c + j;
+    const int32_t q = static_cast<int32_t>((p + superstep - 1) % n);
+    const int64_t b = static_cast<int64_t>(p) * n + q;  // toRatingBlockId (:597-601)
+    if (ctx->rb.size(b) > 0) rbids.push_back(b);
+  }
+  orders.resize(rbids.size());
+  parallel_tasks(static_cast<int64_t>(rbids.size()), [&](int64_t x) {
+    const int64_t b = rbids[x];
+    const int64_t len = ctx->rb.size(b);
+    orders[x].resize(len);
+    if (ctx->P.has_seed) {
+      JavaRandom rng(static_cast<int64_t>(iteration ^ static_cast<int32_t>(b)) ^ ctx->P.seed);  // :392
+      scala_shuffle(rng, orders[x].data(), len);                                                // :393
+    } else {
+      std::random_device rd;
+      JavaRandom rng((static_cast<int64_t>(rd()) << 32) ^ rd());
+      scala_shuffle(rng, orders[x].data(), len);
+    }
+  });
+  for (size_t x = 0; x < rbids.size(); ++x) {
+    const int64_t b = rbids[x];
+    const int32_t p = static_cast<int32_t>(b / n), q = static_cast<int32_t>(b % n);
+    const int64_t st = ctx->rb.start[b];
+    OrderedSeq sq;
+    sq.u = ctx->rb.urow.data() + st;
+    sq.i = ctx->rb.irow.data() + st;
+    sq.r = ctx->rb.r.data() + st;
+    sq.order = orders[x].data();
+    sq.len = ctx->rb.size(b);
+    sq.u_lo = static_cast<uint32_t>(ctx->U.block_start[p]);
+    sq.u_hi = static_cast<uint32_t>(ctx->U.block_start[p + 1]);
+    sq.i_lo = static_cast<uint32_t>(ctx->I.block_start[q]);
+    sq.i_hi = static_cast<uint32_t>(ctx->I.block_start[q + 1]);
+    seqs.push_back(sq);
+  }
+  if (seqs.empty()) return;
+  LevelPlan lp;
+  build_level_plan(seqs, lp);
+  DeviceGuard g(s.device);
+  const size_t bytes = lp.entries.size() * sizeof(DetEntry);
+  MF_HIP(hipStreamSynchronize(s.stream));  // the pinned staging buffer is reused
+  s.det_pin.alloc(bytes);
+  s.det_dev.alloc(bytes);
+  std::memcpy(s.det_pin.as<void>(), lp.entries.data(), bytes);
+  MF_HIP(hipMemcpyAsync(s.det_dev.get(), s.det_pin.as<void>(), bytes, hipMemcpyHostToDevice, s.stream));
+  const DetEntry* dev = s.det_dev.as<DetEntry>();
+  for (int64_t l = 0; l < lp.levels(); ++l) {
+    const int64_t b0 = lp.level_start[l], cnt = lp.level_start[l + 1] - b0;
+    LaunchTimer t(s, ctx->profiling);
+    launch_level(s.stream, dev + b0, cnt, s.uf.get(), s.itf.get(), s.regu.get(), s.regi.get(),
+                 ctx->P.num_factors, eta, Arith::kDsgd, true);
+  }
+  MF_HIP(hipGetLastError());
+  ctx->stats.levels += lp.levels();
+  ctx->stats.updates += static_cast<int64_t>(lp.entries.size());
+  ctx->stats.kernel_launches += lp.levels();
+}
+
+void fast_superstep(mf_ctx* ctx, Shard& s, int64_t superstep, double eta) {
+  const int32_t n = ctx->nb;
+  const int64_t smod = (superstep - 1) % n;
+  DeviceGuard g(s.device);
+  const FastBlk* blks = s.fast_blks.as<FastBlk>() + smod * ctx->c;
+  int64_t ups = 0;
+  for (int32_t j = 0; j < ctx->c; ++j) {
+    const int32_t p = s.index * ctx->c + j;
+    const int32_t q = static_cast<int32_t>((p + superstep - 1) % n);
+    ups += ctx->fast_rb_size[static_cast<int64_t>(p) * n + q];
+  }
+  if (ups == 0) return;
+  for (int32_t t = 0; t < ctx->G_fast; ++t) {
+    LaunchTimer tm(s, ctx->profiling);
+    launch_fast_substep(s.stream, blks, ctx->c, ctx->G_fast, t, s.fast_recs.as<FastRec>(),
+                        s.fast_cells.as<int32_t>(), s.uf.as<float>(), s.itf.as<float>(),
+                        s.regi.as<float>(), ctx->P.num_factors, static_cast<float>(eta));
+  }
+  MF_HIP(hipGetLastError());
+  ctx->stats.kernel_launches += ctx->G_fast;
+  ctx->stats.updates += ups;
+}
+
+// nextRatingBlock rotation (:611-619) across shards after superstep s.
+void ring_shift(mf_ctx* ctx, int64_t superstep) {
+  if (ctx->G <= 1) return;
+  const int32_t n = ctx->nb;
+  const size_t k = static_cast<size_t>(ctx->P.num_factors);
+  auto rows_of = [&](int32_t blk, int64_t& r0, int64_t& cnt) {
+    r0 = ctx->I.block_start[blk];
+    cnt = ctx->I.block_start[blk + 1] - r0;
+  };
+  if (ctx->rank_mode) {
+    Shard& s = ctx->shards[0];
+    DeviceGuard g(s.device);
+    const int gi = s.index;
+    const int32_t out_blk = static_cast<int32_t>((static_cast<int64_t>(gi) * ctx->c + superstep - 1) % n);
+    const int32_t in_blk = static_cast<int32_t>((static_cast<int64_t>((gi + 1) % ctx->G) * ctx->c + superstep - 1) % n);
+    int64_t o0, oc, i0, ic;
+    rows_of(out_blk, o0, oc);
+    rows_of(in_blk, i0, ic);
+    char* base = s.itf.as<char>();
+    MF_NCCL(ncclGroupStart());
+    if (oc > 0)
+      MF_NCCL(ncclSend(base + o0 * k * ctx->es, oc * k, ctx->f64 ? ncclFloat64 : ncclFloat32,
+                       (gi + ctx->G - 1) % ctx->G, ctx->comm, s.stream));
+    if (ic > 0)
+      MF_NCCL(ncclRecv(base + i0 * k * ctx->es, ic * k, ctx->f64 ? ncclFloat64 : ncclFloat32,
+                       (gi + 1) % ctx->G, ctx->comm, s.stream));
+    MF_NCCL(ncclGroupEnd());
+  } else {
+    // in-process shards: peer copy on the sender's stream, receiver waits on an event
+    for (auto& src : ctx->shards) {
+      DeviceGuard g(src.device);
+      MF_HIP(hipEventRecord(src.done, src.stream));
+    }
+    for (auto& src : ctx->shards) {
+      Shard& dst = *local_shard(ctx, (src.index + ctx->G - 1) % ctx->G);
+      const int32_t blk = static_cast<int32_t>((static_cast<int64_t>(src.index) * ctx->c + superstep - 1) % n);
+      int64_t r0, cnt;
+      rows_of(blk, r0, cnt);
+      if (cnt == 0) continue;
+      DeviceGuard g(src.device);
+      MF_HIP(hipStreamWaitEvent(src.stream, dst.done, 0));  // dst finished superstep s
+      const size_t off = static_cast<size_t>(r0) * k * ctx->es, bytes = static_cast<size_t>(cnt) * k * ctx->es;
+      MF_HIP(hipMemcpyPeerAsync(dst.itf.as<char>() + off, dst.device, src.itf.as<char>() + off, src.device,
+                                bytes, src.stream));
+    }
+    for (auto& src : ctx->shards) {
+      DeviceGuard g(src.device);
+      MF_HIP(hipEventRecord(src.done, src.stream));
+    }
+    for (auto& dst : ctx->shards) {
+      Shard& src = *local_shard(ctx, (dst.index + 1) % ctx->G);
+      DeviceGuard g(dst.device);
+      MF_HIP(hipStreamWaitEvent(dst.stream, src.done, 0));
+    }
+  }
+  for (int32_t g = 0; g < ctx->G; ++g) {
+    const int32_t blk = static_cast<int32_t>((static_cast<int64_t>(g) * ctx->c + superstep - 1) % n);
+    ctx->item_loc[blk] = (g + ctx->G - 1) % ctx->G;
+  }
+}
+
+void run_supersteps(mf_ctx* ctx, int64_t count) {
+  MF_REQUIRE(ctx->prepared, "mf_dsgd_run before mf_dsgd_prepare");
+  for (int64_t x = 0; x < count; ++x) {
+    const int64_t s = ctx->superstep_done + 1;
+    const int32_t iteration = static_cast<int32_t>(s / ctx->nb);  // getSuperstepNumber / numBlocks (:476)
+    const double eta = learning_rate(ctx->P.lr_method, ctx->P.learning_rate, iteration + 1, ctx->P.lambda,
+                                     ctx->P.lr_arg);  // :383-386
+    for (auto& sh : ctx->shards) {
+      if (ctx->f64) det_superstep(ctx, sh, s, iteration, eta);
+      else fast_superstep(ctx, sh, s, eta);
+    }
+    ring_shift(ctx, s);
+    ctx->superstep_done = s;
+    ctx->stats.supersteps++;
+  }
+  ctx->stats.algorithmic_bytes = static_cast<double>(ctx->stats.updates) * bytes_per_update(ctx);
+}
+
+void reset_item_loc(mf_ctx* ctx) {
+  ctx->item_loc.assign(ctx->nb, 0);
+  for (int32_t q = 0; q < ctx->nb; ++q) ctx->item_loc[q] = q / ctx->c;
+  for (int64_t s = 1; s <= ctx->superstep_done; ++s)
+    if (ctx->G > 1)
+      for (int32_t g = 0; g < ctx->G; ++g) {
+        const int32_t blk = static_cast<int32_t>((static_cast<int64_t>(g) * ctx->c + s - 1) % ctx->nb);
+        ctx->item_loc[blk] = (g + ctx->G - 1) % ctx->G;
+      }
+}
+
+void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, int64_t n) {
+  MF_REQUIRE(n >= 0, "negative rating count");
+  MF_REQUIRE(n == 0 || (u && i && r), "null rating arrays");
+  sync_all(ctx);
+  ctx->nb = std::max(1, ctx->P.num_blocks);
+  MF_REQUIRE(ctx->nb % ctx->G == 0, "num_blocks must be a multiple of the device count");
+  ctx->c = ctx->nb / ctx->G;
+  build_model(ctx, u, i, n);
+  int32_t lo = 0, hi = ctx->nb;
+  if (ctx->rank_mode) { lo = ctx->shards[0].index * ctx->c; hi = lo + ctx->c; }
+  build_rating_blocks(ctx->rb, ctx->U, ctx->I, u, i, r, n, lo, hi, ctx->f64 && ctx->P.has_seed);
+  const int64_t nb2 = static_cast<int64_t>(ctx->nb) * ctx->nb;
+  if (!ctx->f64) {
+    const int64_t local = ctx->rb.start[nb2];
+    const int64_t blocks_local = static_cast<int64_t>(hi - lo) * ctx->nb;
+    ctx->G_fast = choose_groups(local / std::max<int64_t>(blocks_local, 1), ctx->c, ctx->P.fast_waves);
+    FastPlan fp;
+    build_fast_plan(fp, ctx->rb, ctx->U, ctx->I, ctx->G_fast, ctx->P.lambda,
+                    static_cast<uint64_t>(ctx->P.seed) * 0x9E3779B97F4A7C15ULL + 1);
+    ctx->fast_rb_size.assign(nb2, 0);
+    for (int64_t b = 0; b < nb2; ++b) ctx->fast_rb_size[b] = ctx->rb.size(b);
+    ctx->stats.groups = ctx->G_fast;
+    for (auto& s : ctx->shards) {
+      DeviceGuard g(s.device);
+      s.fast_recs.alloc(std::max<size_t>(fp.recs.size(), 1) * sizeof(FastRec));
+      s.fast_cells.alloc(std::max<size_t>(fp.cell_off.size(), 1) * sizeof(int32_t));
+      if (!fp.recs.empty())
+        MF_HIP(hipMemcpy(s.fast_recs.get(), fp.recs.data(), fp.recs.size() * sizeof(FastRec), hipMemcpyHostToDevice));
+      if (!fp.cell_off.empty())
+        MF_HIP(hipMemcpy(s.fast_cells.get(), fp.cell_off.data(), fp.cell_off.size() * sizeof(int32_t),
+                         hipMemcpyHostToDevice));
+      std::vector<FastBlk> blks(static_cast<size_t>(ctx->nb) * ctx->c);
+      for (int32_t sm = 0; sm < ctx->nb; ++sm)
+        for (int32_t j = 0; j < ctx->c; ++j) {
+          const int32_t p = s.index * ctx->c + j;
+          const int32_t q = (p + sm) % ctx->nb;
+          const int64_t b = static_cast<int64_t>(p) * ctx->nb + q;
+          blks[static_cast<size_t>(sm) * ctx->c + j] = FastBlk{fp.rec_base[b], fp.cell_base[b] < 0 ? 0 : fp.cell_base[b]};
+        }
+      s.fast_blks.alloc(blks.size() * sizeof(FastBlk));
+      MF_HIP(hipMemcpy(s.fast_blks.get(), blks.data(), blks.size() * sizeof(FastBlk), hipMemcpyHostToDevice));
+    }
+    ctx->rb = RatingBlocks();  // the device holds the schedule; free the host copy
+    ctx->rb.n_blocks = ctx->nb;
+  }
+  ctx->superstep_done = 0;
+  reset_item_loc(ctx);
+  ctx->prepared = true;
+}
+
+// Make every row current on shard `dst` (users from their owners, items from their holders).
+void consolidate(mf_ctx* ctx, Shard& dst) {
+  if (ctx->G <= 1 || ctx->rank_mode || !ctx->prepared) return;
+  const size_t k = static_cast<size_t>(ctx->P.num_factors);
+  sync_all(ctx);
+  for (int32_t b = 0; b < ctx->nb; ++b) {
+    for (int side = 0; side < 2; ++side) {
+      const SideLayout& S = side_of(ctx, side);
+      const int owner = side == kSideU ? shard_of_user_block(ctx, b) : ctx->item_loc[b];
+      if (owner == dst.index) continue;
+      Shard& src = *local_shard(ctx, owner);
+      const int64_t r0 = S.block_start[b], cnt = S.block_start[b + 1] - r0;
+      if (cnt == 0) continue;
+      const size_t off = static_cast<size_t>(r0) * k * ctx->es, bytes = static_cast<size_t>(cnt) * k * ctx->es;
+      DevBuf& sb = side == kSideU ? src.uf : src.itf;
+      DevBuf& db = side == kSideU ? dst.uf : dst.itf;
+      DeviceGuard g(dst.device);
+      MF_HIP(hipMemcpyPeerAsync(db.as<char>() + off, dst.device, sb.as<char>() + off, src.device, bytes, dst.stream));
+    }
+  }
+  DeviceGuard g(dst.device);
+  MF_HIP(hipStreamSynchronize(dst.stream));
+}
+
+// Rank mode: broadcast each item block from its holder so every rank has all items.
+void allgather_items(mf_ctx* ctx) {
+  if (!ctx->rank_mode || ctx->G <= 1) return;
+  Shard& s = ctx->shards[0];
+  DeviceGuard g(s.device);
+  const size_t k = static_cast<size_t>(ctx->P.num_factors);
+  MF_NCCL(ncclGroupStart());
+  for (int32_t b = 0; b < ctx->nb; ++b) {
+    const int64_t r0 = ctx->I.block_start[b], cnt = ctx->I.block_start[b + 1] - r0;
+    if (cnt == 0) continue;
+    char* p = s.itf.as<char>() + static_cast<size_t>(r0) * k * ctx->es;
+    MF_NCCL(ncclBroadcast(p, p, cnt * k, ctx->f64 ? ncclFloat64 : ncclFloat32, ctx->item_loc[b], ctx->comm, s.stream));
+  }
+  MF_NCCL(ncclGroupEnd());
+  MF_HIP(hipStreamSynchronize(s.stream));
+  // item_loc keeps tracking the ring (all ranks simulate it identically); copies made here
+  // are read-only snapshots for evaluation.
+}
+
+// Evaluation: resolve ids on the host, gather-dot on the device.
+struct EvalOut {
+  double sse = 0, cnt = 0, risk = 0;
+};
+
+EvalOut evaluate(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, int64_t n,
+                 const int32_t* mult, double lambda, double* pred_out, uint8_t* found_out) {
+  MF_REQUIRE(ctx->have_model, "The MatrixFactorization model has not been fitted to data. "
+                              "Prior to predicting values, it has to be trained on data.");
+  MF_REQUIRE(n >= 0, "negative count");
+  EvalOut res;
+  if (n == 0) return res;
+  Shard& s = ctx->shards[0];
+  if (ctx->rank_mode) allgather_items(ctx);
+  else consolidate(ctx, s);
+  std::vector<uint32_t> ur, ir;
+  lookup_rows(ctx->U, u, n, ur);
+  lookup_rows(ctx->I, i, n, ir);
+  std::vector<int32_t> urow(n), irow(n);
+  const int me = s.index;
+  for (int64_t j = 0; j < n; ++j) {
+    int32_t a = static_cast<int32_t>(ur[j]), b = static_cast<int32_t>(ir[j]);
+    if (ctx->rank_mode && a >= 0 && ctx->U.row_block[a] / ctx->c != me) a = -1;  // not my user
+    urow[j] = a;
+    irow[j] = b;
+  }
+  DeviceGuard g(s.device);
+  MF_HIP(hipStreamSynchronize(s.stream));
+  s.ev_u.alloc(n * 4);
+  s.ev_i.alloc(n * 4);
+  MF_HIP(hipMemcpy(s.ev_u.get(), urow.data(), n * 4, hipMemcpyHostToDevice));
+  MF_HIP(hipMemcpy(s.ev_i.get(), irow.data(), n * 4, hipMemcpyHostToDevice));
+  double* dout = nullptr;
+  if (pred_out) { s.ev_out.alloc(n * 8); dout = s.ev_out.as<double>(); }
+  const double* dr = nullptr;
+  const int32_t* dm = nullptr;
+  double* dpart = nullptr;
+  const int grid = predict_grid(n);
+  if (r) {
+    s.ev_r.alloc(n * 8);
+    MF_HIP(hipMemcpy(s.ev_r.get(), r, n * 8, hipMemcpyHostToDevice));
+    dr = s.ev_r.as<double>();
+    s.ev_part.alloc(static_cast<size_t>(grid) * 3 * 8);
+    dpart = s.ev_part.as<double>();
+    if (mult) {
+      s.ev_mult.alloc(n * 4);
+      MF_HIP(hipMemcpy(s.ev_mult.get(), mult, n * 4, hipMemcpyHostToDevice));
+      dm = s.ev_mult.as<int32_t>();
+    }
+  }
+  launch_predict(s.stream, s.ev_u.as<int32_t>(), s.ev_i.as<int32_t>(), n, s.uf.get(), s.itf.get(),
+                 ctx->P.num_factors, ctx->f64, dout, dr, dm, lambda, dpart);
+  MF_HIP(hipGetLastError());
+  MF_HIP(hipStreamSynchronize(s.stream));
+  if (pred_out) {
+    MF_HIP(hipMemcpy(pred_out, dout, n * 8, hipMemcpyDeviceToHost));
+    for (int64_t j = 0; j < n; ++j) found_out[j] = (urow[j] >= 0 && irow[j] >= 0) ? 1 : 0;
+  }
+  if (r) {
+    std::vector<double> part(static_cast<size_t>(grid) * 3);
+    MF_HIP(hipMemcpy(part.data(), dpart, part.size() * 8, hipMemcpyDeviceToHost));
+    for (int w = 0; w < grid; ++w) {
+      res.sse += part[3 * w];
+      res.cnt += part[3 * w + 1];
+      res.risk += part[3 * w + 2];
+    }
+  }
+  if (ctx->rank_mode && ctx->G > 1) {
+    // combine per-rank results: predictions (owner rank writes, others contribute 0), sums
+    DevBuf red;
+    const int64_t m = 3 + (pred_out ? 2 * n : 0);
+    std::vector<double> h(m, 0.0);
+    h[0] = res.sse; h[1] = res.cnt; h[2] = res.risk;
+    if (pred_out)
+      for (int64_t j = 0; j < n; ++j) { h[3 + j] = found_out[j] ? pred_out[j] : 0.0; h[3 + n + j] = found_out[j]; }
+    red.alloc(m * 8);
+    MF_HIP(hipMemcpy(red.get(), h.data(), m * 8, hipMemcpyHostToDevice));
+    MF_NCCL(ncclAllReduce(red.get(), red.get(), m, ncclFloat64, ncclSum, ctx->comm, s.stream));
+    MF_HIP(hipStreamSynchronize(s.stream));
+    MF_HIP(hipMemcpy(h.data(), red.get(), m * 8, hipMemcpyDeviceToHost));
+    res.sse = h[0]; res.cnt = h[1]; res.risk = h[2];
+    if (pred_out)
+      for (int64_t j = 0; j < n; ++j) { pred_out[j] = h[3 + j]; found_out[j] = h[3 + n + j] > 0.5 ? 1 : 0; }
+  }
+  return res;
+}
+
+// ---------------------------------------------------------------------------------------
+// Online micro-batches (single shard).
+int32_t online_row(mf_ctx* ctx, SideLayout& S, int32_t id, std::vector<int32_t>& fresh) {
+  const int32_t row = S.index.find(id);
+  if (row >= 0) return row;
+  const int32_t nr = static_cast<int32_t>(S.rows());
+  S.index.insert(id, nr);
+  S.row_id.push_back(id);
+  S.omega.push_back(0);
+  S.row_block.push_back(-1);
+  fresh.push_back(id);
+  ctx->order_dirty = true;
+  return nr;
+}
+
+void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, int64_t n, int flavour,
+                   int num_partitions, int64_t* tu, int64_t* ti) {
+  MF_REQUIRE(ctx->shards.size() == 1 && !ctx->rank_mode, "online updates run on a single-device context");
+  MF_REQUIRE(flavour >= MF_ONLINE_NEXT_FACTORS && flavour <= MF_ONLINE_SPARK_SWEEP, "unknown online flavour");
+  MF_REQUIRE(n >= 0 && (n == 0 || (u && i && r)), "bad rating arrays");
+  Shard& s = ctx->shards[0];
+  if (!ctx->have_model) {
+    ctx->U = SideLayout();
+    ctx->I = SideLayout();
+    ctx->have_model = true;
+  }
+  const int k = ctx->P.num_factors;
+  std::vector<int32_t> fu, fi;
+  std::vector<uint32_t> ur(n), ir(n);
+  const int64_t u0 = ctx->U.rows(), i0 = ctx->I.rows();
+  std::vector<uint8_t> seen_u, seen_i;
+  int64_t cu = 0, ci = 0;
+  for (int64_t j = 0; j < n; ++j) {
+    ur[j] = static_cast<uint32_t>(online_row(ctx, ctx->U, u[j], fu));
+    ir[j] = static_cast<uint32_t>(online_row(ctx, ctx->I, i[j], fi));
+  }
+  // touched-row counts (UpdateSeparatedHashMap.updates, OfflineSpark.scala:33-67)
+  seen_u.assign(ctx->U.rows(), 0);
+  seen_i.assign(ctx->I.rows(), 0);
+  for (int64_t j = 0; j < n; ++j) {
+    if (!seen_u[ur[j]]) { seen_u[ur[j]] = 1; ++cu; }
+    if (!seen_i[ir[j]]) { seen_i[ir[j]] = 1; ++ci; }
+  }
+  if (tu) *tu = cu;
+  if (ti) *ti = ci;
+  // first-touch initialisation of unseen ids
+  const bool xor_seed = ctx->P.online_init == MF_INIT_SEEDED;
+  for (int side = 0; side < 2; ++side) {
+    const std::vector<int32_t>& fresh = side == kSideU ? fu : fi;
+    const int64_t row0 = side == kSideU ? u0 : i0;
+    const SideLayout& S = side_of(ctx, side);
+    ensure_rows(ctx, s, side, std::max<int64_t>(S.rows(), 1));
+    if (fresh.empty()) continue;
+    std::vector<double> vec;
+    init_vectors(fresh.data(), static_cast<int64_t>(fresh.size()), k, xor_seed, ctx->P.seed, vec);
+    upload_rows(ctx, s, side, row0, vec.data(), static_cast<int64_t>(fresh.size()));
+  }
+  if (n == 0) return;
+  // sequential order of the flavour
+  std::vector<int32_t> order(n);
+  std::iota(order.begin(), order.end(), 0);
+  if (flavour == MF_ONLINE_SPARK_SWEEP) {
+    // OfflineSpark.scala:135-147,163-203: user partition id % P, item rating block abs(i) % P;
+    // sub-epoch s (1-based) pairs partition p with item block (p - (s-1)) mod P; each cell in
+    // insertion order.  One iteration per micro-batch (OnlineSpark.scala:191-194).
+    MF_REQUIRE(num_partitions >= 1, "num_partitions must be >= 1 for MF_ONLINE_SPARK_SWEEP");
+    const int P = num_partitions;
+    std::vector<std::vector<int32_t>> cells(static_cast<size_t>(P) * P);
+    for (int64_t j = 0; j < n; ++j) {
+      MF_REQUIRE(u[j] >= 0 && i[j] != INT32_MIN, "Spark sweep needs non-negative user ids");
+      const int up = u[j] % P, ib = std::abs(i[j]) % P;
+      cells[static_cast<size_t>(up) * P + ib].push_back(static_cast<int32_t>(j));
+    }
+    order.clear();
+    for (int sub = 1; sub <= P; ++sub)
+      for (int p = 0; p < P; ++p) {
+        const int q = ((p - (sub - 1)) % P + P) % P;
+        const auto& c = cells[static_cast<size_t>(p) * P + q];
+        order.insert(order.end(), c.begin(), c.end());
+      }
+  }
+  std::vector<double> rr(r, r + n);
+  OrderedSeq sq;
+  sq.u = ur.data();
+  sq.i = ir.data();
+  sq.r = rr.data();
+  sq.order = order.data();
+  sq.len = n;
+  sq.u_lo = 0;
+  sq.u_hi = static_cast<uint32_t>(ctx->U.rows());
+  sq.i_lo = 0;
+  sq.i_hi = static_cast<uint32_t>(ctx->I.rows());
+  LevelPlan lp;
+  build_level_plan({sq}, lp);
+  DeviceGuard g(s.device);
+  const size_t bytes = lp.entries.size() * sizeof(DetEntry);
+  MF_HIP(hipStreamSynchronize(s.stream));
+  s.det_pin.alloc(bytes);
+  s.det_dev.alloc(bytes);
+  std::memcpy(s.det_pin.as<void>(), lp.entries.data(), bytes);
+  MF_HIP(hipMemcpyAsync(s.det_dev.get(), s.det_pin.as<void>(), bytes, hipMemcpyHostToDevice, s.stream));
+  for (int64_t l = 0; l < lp.levels(); ++l) {
+    const int64_t b0 = lp.level_start[l], cnt = lp.level_start[l + 1] - b0;
+    LaunchTimer t(s, ctx->profiling);
+    launch_level(s.stream, s.det_dev.as<DetEntry>() + b0, cnt, s.uf.get(), s.itf.get(), s.regu.get(),
+                 s.regi.get(), k, ctx->P.online_learning_rate, Arith::kSgdNext, ctx->f64);
+  }
+  MF_HIP(hipGetLastError());
+  MF_HIP(hipStreamSynchronize(s.stream));
+  ctx->stats.levels += lp.levels();
+  ctx->stats.kernel_launches += lp.levels();
+  ctx->stats.updates += n;
+}
+
+mf_ctx* new_ctx(const mf_params* p) {
+  validate_params(p);
+  auto* ctx = new mf_ctx();
+  ctx->P = *p;
+  ctx->f64 = p->mode == MF_MODE_DETERMINISTIC_F64;
+  ctx->es = ctx->f64 ? 8 : 4;
+  return ctx;
+}
+
+}  // namespace
+}  // namespace mfhip
+
+using namespace mfhip;
+
+extern "C" {
+
+void mf_params_init(mf_params* p) {
+  if (!p) return;
+  std::memset(p, 0, sizeof(*p));
+  p->num_factors = 10;        // MatrixFactorization.scala:201-203
+  p->iterations = 10;         // :209-211
+  p->lambda = 1.0;            // :205-207
+  p->learning_rate = 0.001;   // DSGDforMF.scala:163-165
+  p->lr_method = MF_LR_DEFAULT;  // :167-169
+  p->lr_arg = 0.0;
+  p->num_blocks = 1;          // Blocks None -> getOrElse(1) (:270)
+  p->seed = 0;                // Seed Some(0L) (:217-219)
+  p->has_seed = 1;
+  p->mode = MF_MODE_DETERMINISTIC_F64;
+  p->online_learning_rate = 0.01;  // SparkExample.scala:33 SGDUpdater(0.01)
+  p->online_init = MF_INIT_PSEUDO_RANDOM;
+  p->fast_waves = 0;
+}
+
+const char* mf_last_error(void) { return g_last_error.c_str(); }
+const char* mf_version(void) { return "mfhip 0.1.0 (gfx950)"; }
+
+int mf_device_count(int* n) {
+  return guarded([&] {
+    MF_REQUIRE(n, "null");
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    *n = (e == hipSuccess) ? c : 0;
+  });
+}
+
+int mf_create(const mf_params* p, const int* device_ids, int n_devices, mf_ctx** out) {
+  return guarded([&] {
+    MF_REQUIRE(out, "out is null");
+    *out = nullptr;
+    MF_REQUIRE(n_devices >= 1, "n_devices must be >= 1");
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count < 1)
+      fail(MF_ERR_NO_DEVICE, "no HIP device available (libmfhip has no CPU fallback)");
+    std::unique_ptr<mf_ctx> ctx(new_ctx(p));
+    ctx->G = n_devices;
+    { std::vector<Shard> tmp(n_devices); ctx->shards.swap(tmp); }
+    for (int d = 0; d < n_devices; ++d) {
+      const int dev = device_ids ? device_ids[d] : d % count;  // shards may share a device
+      MF_REQUIRE(dev >= 0 && dev < count, "device id out of range");
+      init_shard(ctx->shards[d], dev, d);
+    }
+    // enable peer access between distinct devices (ignore "already enabled")
+    for (auto& a : ctx->shards)
+      for (auto& b : ctx->shards)
+        if (a.device != b.device) {
+          int ok = 0;
+          (void)hipDeviceCanAccessPeer(&ok, a.device, b.device);
+          if (ok) {
+            DeviceGuard g(a.device);
+            (void)hipDeviceEnablePeerAccess(b.device, 0);
+            (void)hipGetLastError();
+          }
+        }
+    *out = ctx.release();
+  });
+}
+
+int mf_comm_unique_id(uint8_t uid_out[MF_UID_BYTES]) {
+  return guarded([&] {
+    MF_REQUIRE(uid_out, "null");
+    static_assert(sizeof(ncclUniqueId) <= MF_UID_BYTES, "uid size");
+    ncclUniqueId id;
+    MF_NCCL(ncclGetUniqueId(&id));
+    std::memset(uid_out, 0, MF_UID_BYTES);
+    std::memcpy(uid_out, &id, sizeof(id));
+  });
+}
+
+int mf_create_rank(const mf_params* p, int device_id, int nranks, int rank, const uint8_t uid[MF_UID_BYTES],
+                   mf_ctx** out) {
+  return guarded([&] {
+    MF_REQUIRE(out && uid, "null argument");
+    *out = nullptr;
+    MF_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank / nranks");
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count < 1)
+      fail(MF_ERR_NO_DEVICE, "no HIP device available (libmfhip has no CPU fallback)");
+    MF_REQUIRE(device_id >= 0 && device_id < count, "device id out of range");
+    std::unique_ptr<mf_ctx> ctx(new_ctx(p));
+    ctx->G = nranks;
+    ctx->rank_mode = true;
+    { std::vector<Shard> tmp(1); ctx->shards.swap(tmp); }
+    init_shard(ctx->shards[0], device_id, rank);
+    if (nranks > 1) {
+      DeviceGuard g(device_id);
+      ncclUniqueId id;
+      std::memcpy(&id, uid, sizeof(id));
+      MF_NCCL(ncclCommInitRank(&ctx->comm, nranks, id, rank));
+    }
+    *out = ctx.release();
+  });
+}
+
+int mf_destroy(mf_ctx* ctx) {
+  return guarded([&] {
+    if (!ctx) return;
+    for (auto& s : ctx->shards) destroy_shard(s);
+    if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+    delete ctx;
+  });
+}
+
+int mf_dsgd_prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, int64_t n) {
+  return guarded([&] {
+    MF_REQUIRE(ctx, "null context");
+    prepare(ctx, u, i, r, n);
+  });
+}
+
+int mf_dsgd_run(mf_ctx* ctx, int64_t supersteps) {
+  return guarded([&] {
+    MF_REQUIRE(ctx, "null context");
+    MF_REQUIRE(supersteps >= 0, "negative superstep count");
+    run_supersteps(ctx, supersteps);
+  });
+}
+
+int mf_dsgd_superstep(mf_ctx* ctx, int64_t* done) {
+  return guarded([&] {
+    MF_REQUIRE(ctx && done, "null argument");
+    *done = ctx->superstep_done;
+  });
+}
+
+int mf_dsgd_set_superstep(mf_ctx* ctx, int64_t done) {
+  return guarded([&] {
+    MF_REQUIRE(ctx && done >= 0, "bad argument");
+    MF_REQUIRE(ctx->prepared, "mf_dsgd_set_superstep before mf_dsgd_prepare");
+    sync_all(ctx);
+    ctx->superstep_done = done;
+    reset_item_loc(ctx);
+  });
+}
+
+int mf_sync(mf_ctx* ctx) {
+  return guarded([&] {
+    MF_REQUIRE(ctx, "null context");
+    sync_all(ctx);
+  });
+}
+
+int mf_dsgd_fit(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, int64_t n) {
+  return guarded([&] {
+    MF_REQUIRE(ctx, "null context");
+    prepare(ctx, u, i, r, n);
+    run_supersteps(ctx, static_cast<int64_t>(ctx->P.iterations) * ctx->nb);
+    sync_all(ctx);
+  });
+}
+
+int mf_num_factors(mf_ctx* ctx, int side, int64_t* count) {
+  return guarded([&] {
+    MF_REQUIRE(ctx && count, "null argument");
+    MF_REQUIRE(side == MF_SIDE_USER || side == MF_SIDE_ITEM, "bad side");
+    const SideLayout& S = side_of(ctx, side);
+    if (!ctx->rank_mode || side == MF_SIDE_ITEM || !ctx->prepared) { *count = S.rows(); return; }
+    const int me = ctx->shards[0].index;
+    *count = S.block_start[(me + 1) * ctx->c] - S.block_start[me * ctx->c];
+  });
+}
+
+int mf_get_factors(mf_ctx* ctx, int side, int32_t* ids, double* vecs, int64_t cap, int64_t* written) {
+  return guarded([&] {
+    MF_REQUIRE(ctx, "null context");
+    MF_REQUIRE(side == MF_SIDE_USER || side == MF_SIDE_ITEM, "bad side");
+    MF_REQUIRE(ctx->have_model, "The MatrixFactorization model has not been fitted to data.");
+    Shard& s = ctx->shards[0];
+    if (ctx->rank_mode) { if (side == MF_SIDE_ITEM) allgather_items(ctx); }
+    else consolidate(ctx, s);
+    sync_all(ctx);
+    ensure_order(ctx);
+    const SideLayout& S = side_of(ctx, side);
+    const int k = ctx->P.num_factors;
+    std::vector<double> all(static_cast<size_t>(std::max<int64_t>(S.rows(), 1)) * k);
+    download_rows(ctx, s, side, 0, S.rows(), all.data());
+    const auto& ord = side == kSideU ? ctx->rows_by_id_u : ctx->rows_by_id_i;
+    int64_t w = 0;
+    const int me = s.index;
+    for (int64_t x = 0; x < S.rows(); ++x) {
+      const int32_t row = ord[x];
+      if (ctx->rank_mode && side == kSideU && S.row_block[row] / ctx->c != me) continue;
+      if (w >= cap) fail(MF_ERR_CAPACITY, "output capacity too small");
+      if (ids) ids[w] = S.row_id[row];
+      if (vecs) std::memcpy(vecs + static_cast<size_t>(w) * k, all.data() + static_cast<size_t>(row) * k, sizeof(double) * k);
+      ++w;
+    }
+    if (written) *written = w;
+  });
+}
+
+int mf_set_factors(mf_ctx* ctx, int side, const int32_t* ids, const double* vecs, int64_t n) {
+  return guarded([&] {
+    MF_REQUIRE(ctx && (n == 0 || (ids && vecs)), "null argument");
+    MF_REQUIRE(side == MF_SIDE_USER || side == MF_SIDE_ITEM, "bad side");
+    if (!ctx->have_model) { ctx->U = SideLayout(); ctx->I = SideLayout(); ctx->have_model = true; }
+    SideLayout& S = side_of(ctx, side);
+    std::vector<int32_t> fresh;
+    std::vector<int32_t> rows(n);
+    for (int64_t j = 0; j < n; ++j) rows[j] = online_row(ctx, S, ids[j], fresh);
+    const int k = ctx->P.num_factors;
+    for (auto& s : ctx->shards) {
+      sync_all(ctx);
+      ensure_rows(ctx, s, side, std::max<int64_t>(S.rows(), 1));
+      for (int64_t j = 0; j < n; ++j) upload_rows(ctx, s, side, rows[j], vecs + static_cast<size_t>(j) * k, 1);
+    }
+  });
+}
+
+int mf_predict(mf_ctx* ctx, const int32_t* u, const int32_t* i, int64_t n, double* out, uint8_t* found) {
+  return guarded([&] {
+    MF_REQUIRE(ctx, "null context");
+    MF_REQUIRE(n == 0 || (u && i && out && found), "null argument");
+    evaluate(ctx, u, i, nullptr, n, nullptr, 0.0, out, found);
+  });
+}
+
+int mf_rmse(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, int64_t n, double* rmse,
+            int64_t* matched) {
+  return guarded([&] {
+    MF_REQUIRE(ctx && rmse, "null argument");
+    MF_REQUIRE(n == 0 || (u && i && r), "null argument");
+    EvalOut e = evaluate(ctx, u, i, r, n, nullptr, 0.0, nullptr, nullptr);
+    *rmse = e.cnt > 0 ? std::sqrt(e.sse / e.cnt) : std::nan("");
+    if (matched) *matched = static_cast<int64_t>(e.cnt);
+  });
+}
+
+int mf_empirical_risk(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, int64_t n,
+                      double lambda, double* risk) {
+  return guarded([&] {
+    MF_REQUIRE(ctx && risk, "null argument");
+    MF_REQUIRE(n == 0 || (u && i && r), "null argument");
+    // the (user, item)-keyed join multiplies duplicate pairs (MatrixFactorization.scala:175)
+    std::vector<uint64_t> key(n);
+    for (int64_t j = 0; j < n; ++j)
+      key[j] = (static_cast<uint64_t>(static_cast<uint32_t>(u[j])) << 32) | static_cast<uint32_t>(i[j]);
+    std::vector<uint64_t> sorted = key;
+    std::sort(sorted.begin(), sorted.end());
+    std::vector<int32_t> mult(n);
+    for (int64_t j = 0; j < n; ++j) {
+      auto rg = std::equal_range(sorted.begin(), sorted.end(), key[j]);
+      mult[j] = static_cast<int32_t>(rg.second - rg.first);
+    }
+    EvalOut e = evaluate(ctx, u, i, r, n, mult.data(), lambda, nullptr, nullptr);
+    *risk = e.risk;
+  });
+}
+
+int mf_block_update(mf_ctx* ctx, const double* r, const int32_t* uidx, const int32_t* iidx, int64_t len,
+                    double* users, const int32_t* uomega, int64_t nu, double* items, const int32_t* iomega,
+                    int64_t ni, int k, int iteration, int rating_block_id, int64_t seed, double lr,
+                    int lr_method, double lr_arg, double lambda) {
+  return guarded([&] {
+    MF_REQUIRE(ctx, "null context");
+    MF_REQUIRE(len >= 0 && nu >= 0 && ni >= 0 && k >= 1 && k <= 512, "bad sizes");
+    MF_REQUIRE(len == 0 || (r && uidx && iidx && users && items && uomega && iomega), "null argument");
+    for (int64_t j = 0; j < len; ++j)
+      MF_REQUIRE(uidx[j] >= 0 && uidx[j] < nu && iidx[j] >= 0 && iidx[j] < ni, "rating index out of block range");
+    if (len == 0) return;
+    Shard& s = ctx->shards[0];
+    DeviceGuard g(s.device);
+    std::vector<int32_t> order(len);
+    JavaRandom rng(static_cast<int64_t>(iteration ^ rating_block_id) ^ seed);  // DSGDforMF.scala:392
+    scala_shuffle(rng, order.data(), len);
+    std::vector<uint32_t> uu(uidx, uidx + len), ii(iidx, iidx + len);
+    OrderedSeq sq{uu.data(), ii.data(), r, order.data(), len, 0, static_cast<uint32_t>(nu), 0,
+                  static_cast<uint32_t>(ni)};
+    LevelPlan lp;
+    build_level_plan({sq}, lp);
+    std::vector<double> ru(nu), ri(ni);
+    for (int64_t x = 0; x < nu; ++x) ru[x] = lambda / static_cast<double>(uomega[x]);
+    for (int64_t x = 0; x < ni; ++x) ri[x] = lambda / static_cast<double>(iomega[x]);
+    const double eta = learning_rate(lr_method, lr, iteration + 1, lambda, lr_arg);  // :383-386
+    DevBuf du, di, dru, dri, de;
+    du.alloc(static_cast<size_t>(nu) * k * 8);
+    di.alloc(static_cast<size_t>(ni) * k * 8);
+    dru.alloc(static_cast<size_t>(nu) * 8);
+    dri.alloc(static_cast<size_t>(ni) * 8);
+    de.alloc(lp.entries.size() * sizeof(DetEntry));
+    MF_HIP(hipMemcpy(du.get(), users, static_cast<size_t>(nu) * k * 8, hipMemcpyHostToDevice));
+    MF_HIP(hipMemcpy(di.get(), items, static_cast<size_t>(ni) * k * 8, hipMemcpyHostToDevice));
+    MF_HIP(hipMemcpy(dru.get(), ru.data(), static_cast<size_t>(nu) * 8, hipMemcpyHostToDevice));
+    MF_HIP(hipMemcpy(dri.get(), ri.data(), static_cast<size_t>(ni) * 8, hipMemcpyHostToDevice));
+    MF_HIP(hipMemcpy(de.get(), lp.entries.data(), lp.entries.size() * sizeof(DetEntry), hipMemcpyHostToDevice));
+    for (int64_t l = 0; l < lp.levels(); ++l) {
+      const int64_t b0 = lp.level_start[l], cnt = lp.level_start[l + 1] - b0;
+      launch_level(s.stream, de.as<DetEntry>() + b0, cnt, du.get(), di.get(), dru.get(), dri.get(), k, eta,
+                   Arith::kDsgd, true);
+    }
+    MF_HIP(hipGetLastError());
+    MF_HIP(hipStreamSynchronize(s.stream));
+    MF_HIP(hipMemcpy(users, du.get(), static_cast<size_t>(nu) * k * 8, hipMemcpyDeviceToHost));
+    MF_HIP(hipMemcpy(items, di.get(), static_cast<size_t>(ni) * k * 8, hipMemcpyDeviceToHost));
+    ctx->stats.updates += len;
+    ctx->stats.levels += lp.levels();
+  });
+}
+
+int mf_online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, int64_t n, int flavour,
+                     int num_partitions, int64_t* touched_users, int64_t* touched_items) {
+  return guarded([&] {
+    MF_REQUIRE(ctx, "null context");
+    online_update(ctx, u, i, r, n, flavour, num_partitions, touched_users, touched_items);
+  });
+}
+
+int mf_lookup(mf_ctx* ctx, int side, const int32_t* ids, int64_t n, double* vecs_out, uint8_t* found) {
+  return guarded([&] {
+    MF_REQUIRE(ctx && (n == 0 || (ids && vecs_out && found)), "null argument");
+    MF_REQUIRE(side == MF_SIDE_USER || side == MF_SIDE_ITEM, "bad side");
+    MF_REQUIRE(ctx->have_model, "no model");
+    Shard& s = ctx->shards[0];
+    if (!ctx->rank_mode) consolidate(ctx, s);
+    else if (side == MF_SIDE_ITEM) allgather_items(ctx);
+    sync_all(ctx);
+    const SideLayout& S = side_of(ctx, side);
+    const int k = ctx->P.num_factors;
+    std::vector<double> row(k);
+    for (int64_t j = 0; j < n; ++j) {
+      const int32_t x = S.index.find(ids[j]);
+      found[j] = x >= 0;
+      if (x < 0) { std::fill(vecs_out + j * k, vecs_out + (j + 1) * k, 0.0); continue; }
+      download_rows(ctx, s, side, x, 1, vecs_out + static_cast<size_t>(j) * k);
+    }
+  });
+}
+
+int mf_set_profiling(mf_ctx* ctx, int on) {
+  return guarded([&] {
+    MF_REQUIRE(ctx, "null context");
+    sync_all(ctx);
+    ctx->profiling = on != 0;
+  });
+}
+
+int mf_get_stats(mf_ctx* ctx, mf_stats* out) {
+  return guarded([&] {
+    MF_REQUIRE(ctx && out, "null argument");
+    sync_all(ctx);
+    ctx->stats.algorithmic_bytes = static_cast<double>(ctx->stats.updates) * bytes_per_update(ctx);
+    *out = ctx->stats;
+  });
+}
+
+int mf_reset_stats(mf_ctx* ctx) {
+  return guarded([&] {
+    MF_REQUIRE(ctx, "null context");
+    sync_all(ctx);
+    const int32_t groups = ctx->stats.groups;
+    ctx->stats = mf_stats{};
+    ctx->stats.groups = groups;
+  });
+}
+
+int mf_jvm_shuffle(int64_t seed, int64_t len, int32_t* out) {
+  return guarded([&] {
+    MF_REQUIRE(len >= 0 && (len == 0 || out), "bad argument");
+    JavaRandom rng(seed);
+    scala_shuffle(rng, out, len);
+  });
+}
+
+int mf_jvm_block_of(int32_t id, int64_t seed, int32_t n_blocks, int32_t* out) {
+  return guarded([&] {
+    MF_REQUIRE(out && n_blocks >= 1, "bad argument");
+    JavaRandom rng(static_cast<int64_t>(id) ^ seed);
+    *out = rng.nextInt(n_blocks);
+  });
+}
+
+int mf_jvm_random_factors(int64_t rng_seed, int32_t k, double* out) {
+  return guarded([&] {
+    MF_REQUIRE(out && k >= 0, "bad argument");
+    JavaRandom rng(rng_seed);
+    for (int32_t f = 0; f < k; ++f) out[f] = rng.nextDouble();
+  });
+}
+
+int mf_debug_levels(const uint32_t* urow, const uint32_t* irow, const int32_t* order, int64_t n, int32_t* level_out) {
+  return guarded([&] {
+    MF_REQUIRE(n >= 0 && (n == 0 || (urow && irow && level_out)), "bad argument");
+    if (n == 0) return;
+    uint32_t umax = 0, imax = 0;
+    for (int64_t j = 0; j < n; ++j) { umax = std::max(umax, urow[j]); imax = std::max(imax, irow[j]); }
+    std::vector<double> zero(n, 0.0);
+    OrderedSeq sq{urow, irow, zero.data(), order, n, 0, umax + 1, 0, imax + 1};
+    // levels in sequence order: replay the same recurrence build_level_plan uses
+    LevelPlan lp;
+    build_level_plan({sq}, lp);
+    std::vector<int32_t> lu(umax + 1, 0), li(imax + 1, 0);
+    for (int64_t j = 0; j < n; ++j) {
+      const int64_t e = order ? order[j] : j;
+      const int32_t l = std::max(lu[urow[e]], li[irow[e]]) + 1;
+      lu[urow[e]] = l;
+      li[irow[e]] = l;
+      level_out[j] = l;
+    }
+    MF_REQUIRE(lp.levels() == (n ? *std::max_element(level_out, level_out + n) : 0), "level count mismatch");
+  });
+}
+
+int mf_debug_fast_schedule(const int32_t* u, const int32_t* i, int64_t n, int32_t n_blocks, int64_t seed,
+                           int32_t groups, int32_t* block_out, int32_t* substep_out, int32_t* group_out,
+                           int64_t* pos_out) {
+  return guarded([&] {
+    MF_REQUIRE(n >= 0 && n_blocks >= 1 && groups >= 1, "bad argument");
+    MF_REQUIRE(n == 0 || (u && i && block_out && substep_out && group_out && pos_out), "null argument");
+    SideLayout U, I;
+    build_side(U, u, n, n_blocks, seed, true);
+    build_side(I, i, n, n_blocks, seed, true);
+    std::vector<double> r(n, 1.0);
+    RatingBlocks rb;
+    build_rating_blocks(rb, U, I, u, i, r.data(), n, 0, n_blocks, false, true);
+    FastPlan fp;
+    std::vector<int64_t> src;
+    build_fast_plan(fp, rb, U, I, groups, 1.0, static_cast<uint64_t>(seed) * 0x9E3779B97F4A7C15ULL + 1, &src);
+    const int64_t nb2 = static_cast<int64_t>(n_blocks) * n_blocks;
+    const int64_t GG = static_cast<int64_t>(groups) * groups;
+    for (int64_t b = 0; b < nb2; ++b) {
+      if (fp.rec_base[b] < 0) continue;
+      const int32_t* off = fp.cell_off.data() + fp.cell_base[b];
+      for (int64_t cidx = 0; cidx < GG; ++cidx)
+        for (int64_t x = off[cidx]; x < off[cidx + 1]; ++x) {
+          const int64_t j = rb.src[src[fp.rec_base[b] + x]];
+          block_out[j] = static_cast<int32_t>(b);
+          substep_out[j] = static_cast<int32_t>(cidx / groups);
+          group_out[j] = static_cast<int32_t>(cidx % groups);
+          pos_out[j] = x - off[cidx];
+        }
+    }
+  });
+}
+
+int mf_learning_rate(int method, double lr, int32_t iteration, double lambda, double arg, double* out) {
+  return guarded([&] {
+    MF_REQUIRE(out, "null");
+    MF_REQUIRE(method >= MF_LR_DEFAULT && method <= MF_LR_XU, "unknown lr_method");
+    *out = learning_rate(method, lr, iteration, lambda, arg);
+  });
+}
+
+}  // extern "C"

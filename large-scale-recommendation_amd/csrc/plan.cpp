@@ -1,0 +1,352 @@
+// plan.cpp -- host-side DSGD blocking and device schedules (see plan.hpp).
+#include "plan.hpp"
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <numeric>
+#include <queue>
+#include <random>
+
+#include "common.hpp"
+#include "jvm_random.hpp"
+
+namespace mfhip {
+
+namespace {
+
+// Dense id->row table used while blocking when the id range is compact.
+struct DenseMap {
+  int32_t lo = 0;
+  std::vector<int32_t> rows;  // id - lo -> row or -1
+  bool ok() const { return !rows.empty(); }
+  int32_t find(int32_t id) const {
+    int64_t x = static_cast<int64_t>(id) - lo;
+    return (x >= 0 && x < static_cast<int64_t>(rows.size())) ? rows[x] : -1;
+  }
+};
+
+void minmax(const int32_t* ids, int64_t n, int32_t& mn, int32_t& mx) {
+  int w = host_threads();
+  std::vector<int32_t> a(w, INT32_MAX), b(w, INT32_MIN);
+  parallel_for(n, [&](int64_t s, int64_t e, int t) {
+    int32_t lo = INT32_MAX, hi = INT32_MIN;
+    for (int64_t j = s; j < e; ++j) { lo = std::min(lo, ids[j]); hi = std::max(hi, ids[j]); }
+    a[t] = lo; b[t] = hi;
+  }, w);
+  mn = *std::min_element(a.begin(), a.end());
+  mx = *std::max_element(b.begin(), b.end());
+}
+
+bool dense_ok(int32_t mn, int32_t mx, int64_t n) {
+  const int64_t range = static_cast<int64_t>(mx) - mn + 1;
+  return range <= std::max<int64_t>(4 * n, 1 << 22) && range <= (int64_t{1} << 30);
+}
+
+}  // namespace
+
+// initFactorBlockAndIndices (DSGDforMF.scala:513-588): distinct ids (:520), block per id
+// (:531-533), omega = rating count (:537-541), ids sorted within a block when seeded (:556).
+void build_side(SideLayout& s, const int32_t* ids, int64_t n, int32_t nb, int64_t seed, bool has_seed) {
+  s = SideLayout();
+  s.n_blocks = nb;
+  std::vector<int32_t> distinct, counts;
+  if (n > 0) {
+    int32_t mn, mx;
+    minmax(ids, n, mn, mx);
+    if (dense_ok(mn, mx, n)) {
+      const int64_t range = static_cast<int64_t>(mx) - mn + 1;
+      std::vector<int32_t> cnt(range, 0);
+      int32_t* c = cnt.data();
+      parallel_for(n, [&](int64_t b, int64_t e, int) {
+        for (int64_t j = b; j < e; ++j) __atomic_fetch_add(&c[static_cast<int64_t>(ids[j]) - mn], 1, __ATOMIC_RELAXED);
+      });
+      for (int64_t x = 0; x < range; ++x)
+        if (cnt[x]) { distinct.push_back(static_cast<int32_t>(x + mn)); counts.push_back(cnt[x]); }
+    } else {
+      std::vector<int32_t> tmp(ids, ids + n);
+      std::sort(tmp.begin(), tmp.end());
+      for (int64_t j = 0; j < n; ++j) {
+        if (j == 0 || tmp[j] != tmp[j - 1]) { distinct.push_back(tmp[j]); counts.push_back(0); }
+        counts.back()++;
+      }
+    }
+  }
+  const int64_t d = static_cast<int64_t>(distinct.size());
+  std::vector<int32_t> blk(d);
+  if (has_seed) {
+    parallel_for(d, [&](int64_t b, int64_t e, int) {
+      for (int64_t x = b; x < e; ++x) {
+        JavaRandom rng(static_cast<int64_t>(distinct[x]) ^ seed);
+        blk[x] = rng.nextInt(nb);
+      }
+    });
+  } else {
+    std::random_device rd;
+    JavaRandom rng((static_cast<int64_t>(rd()) << 32) ^ rd());
+    for (int64_t x = 0; x < d; ++x) blk[x] = rng.nextInt(nb);
+  }
+  s.block_start.assign(nb + 1, 0);
+  for (int64_t x = 0; x < d; ++x) s.block_start[blk[x] + 1]++;
+  for (int32_t b = 0; b < nb; ++b) s.block_start[b + 1] += s.block_start[b];
+  std::vector<int64_t> fill(s.block_start.begin(), s.block_start.end() - 1);
+  s.row_id.resize(d);
+  s.omega.resize(d);
+  s.row_block.resize(d);
+  s.index.reserve(d);
+  for (int64_t x = 0; x < d; ++x) {  // ascending ids => ascending within each block
+    const int64_t row = fill[blk[x]]++;
+    s.row_id[row] = distinct[x];
+    s.omega[row] = counts[x];
+    s.row_block[row] = blk[x];
+    s.index.insert(distinct[x], static_cast<int32_t>(row));
+  }
+}
+
+void lookup_rows(const SideLayout& s, const int32_t* ids, int64_t n, std::vector<uint32_t>& rows) {
+  rows.resize(n);
+  DenseMap dm;
+  if (s.rows() > 0) {
+    int32_t mn = *std::min_element(s.row_id.begin(), s.row_id.end());
+    int32_t mx = *std::max_element(s.row_id.begin(), s.row_id.end());
+    if (dense_ok(mn, mx, s.rows())) {
+      dm.lo = mn;
+      dm.rows.assign(static_cast<int64_t>(mx) - mn + 1, -1);
+      for (int64_t r = 0; r < s.rows(); ++r) dm.rows[static_cast<int64_t>(s.row_id[r]) - mn] = static_cast<int32_t>(r);
+    }
+  }
+  parallel_for(n, [&](int64_t b, int64_t e, int) {
+    if (dm.ok()) for (int64_t j = b; j < e; ++j) rows[j] = static_cast<uint32_t>(dm.find(ids[j]));
+    else for (int64_t j = b; j < e; ++j) rows[j] = static_cast<uint32_t>(s.index.find(ids[j]));
+  });
+}
+
+// Rating blocks (DSGDforMF.scala:301-327): block ub*n+ib, sorted by (user, item) when seeded.
+void build_rating_blocks(RatingBlocks& rb, const SideLayout& U, const SideLayout& I,
+                         const int32_t* u, const int32_t* i, const double* r, int64_t n,
+                         int32_t ub_lo, int32_t ub_hi, bool sort_ui, bool keep_src) {
+  const int32_t nb = U.n_blocks;
+  const int64_t nb2 = static_cast<int64_t>(nb) * nb;
+  rb = RatingBlocks();
+  rb.n_blocks = nb;
+  std::vector<uint32_t> ur, ir;
+  lookup_rows(U, u, n, ur);
+  lookup_rows(I, i, n, ir);
+  const int w = host_threads();
+  const int64_t chunk = (n + w - 1) / std::max(w, 1);
+  std::vector<std::vector<int64_t>> hist(w, std::vector<int64_t>(nb2 + 1, 0));
+  auto block_of = [&](int64_t j) -> int64_t {
+    const int32_t ub = U.row_block[ur[j]];
+    if (ub < ub_lo || ub >= ub_hi) return -1;
+    return static_cast<int64_t>(ub) * nb + I.row_block[ir[j]];
+  };
+  parallel_for(n, [&](int64_t b, int64_t e, int t) {
+    for (int64_t j = b; j < e; ++j) { int64_t k = block_of(j); if (k >= 0) hist[t][k]++; }
+  }, w, chunk);
+  rb.start.assign(nb2 + 1, 0);
+  for (int64_t k = 0; k < nb2; ++k)
+    for (int t = 0; t < w; ++t) rb.start[k + 1] += hist[t][k];
+  for (int64_t k = 0; k < nb2; ++k) rb.start[k + 1] += rb.start[k];
+  const int64_t total = rb.start[nb2];
+  // per (worker, block) write cursors: worker t writes after workers < t (stable)
+  for (int64_t k = 0; k < nb2; ++k) {
+    int64_t pos = rb.start[k];
+    for (int t = 0; t < w; ++t) { int64_t c = hist[t][k]; hist[t][k] = pos; pos += c; }
+  }
+  rb.urow.resize(total);
+  rb.irow.resize(total);
+  rb.r.resize(total);
+  if (keep_src) rb.src.resize(total);
+  std::vector<uint64_t> key;
+  if (sort_ui) key.resize(total);
+  parallel_for(n, [&](int64_t b, int64_t e, int t) {
+    for (int64_t j = b; j < e; ++j) {
+      int64_t k = block_of(j);
+      if (k < 0) continue;
+      int64_t pos = hist[t][k]++;
+      rb.urow[pos] = ur[j];
+      rb.irow[pos] = ir[j];
+      rb.r[pos] = r[j];
+      if (keep_src) rb.src[pos] = j;
+      if (sort_ui)
+        key[pos] = (static_cast<uint64_t>(static_cast<uint32_t>(u[j]) ^ 0x80000000u) << 32) |
+                   (static_cast<uint32_t>(i[j]) ^ 0x80000000u);
+    }
+  }, w, chunk);
+  if (!sort_ui) return;
+  parallel_tasks(nb2, [&](int64_t k) {
+    const int64_t s = rb.start[k], len = rb.start[k + 1] - s;
+    if (len < 2) return;
+    std::vector<int32_t> idx(len);
+    std::iota(idx.begin(), idx.end(), 0);
+    const uint64_t* kk = key.data() + s;
+    std::stable_sort(idx.begin(), idx.end(), [&](int32_t a, int32_t b) { return kk[a] < kk[b]; });
+    std::vector<uint32_t> tu(len), ti(len);
+    std::vector<double> tr(len);
+    std::vector<int64_t> ts(keep_src ? len : 0);
+    for (int64_t x = 0; x < len; ++x) {
+      tu[x] = rb.urow[s + idx[x]]; ti[x] = rb.irow[s + idx[x]]; tr[x] = rb.r[s + idx[x]];
+      if (keep_src) ts[x] = rb.src[s + idx[x]];
+    }
+    std::copy(tu.begin(), tu.end(), rb.urow.begin() + s);
+    std::copy(ti.begin(), ti.end(), rb.irow.begin() + s);
+    std::copy(tr.begin(), tr.end(), rb.r.begin() + s);
+    if (keep_src) std::copy(ts.begin(), ts.end(), rb.src.begin() + s);
+  });
+}
+
+// Level schedule: level(j) = 1 + max(level of the previous update of the same user row,
+// level of the previous update of the same item row) along each sequence's order.  Updates
+// of one level touch pairwise-distinct rows, so running a level in parallel and the levels
+// in order reproduces the sequential result bit for bit.
+void build_level_plan(const std::vector<OrderedSeq>& seqs, LevelPlan& out) {
+  const int64_t ns = static_cast<int64_t>(seqs.size());
+  std::vector<std::vector<int32_t>> lvl(ns);
+  std::vector<std::vector<int64_t>> cnt(ns);
+  parallel_tasks(ns, [&](int64_t x) {
+    const OrderedSeq& q = seqs[x];
+    std::vector<int32_t> lu(q.u_hi - q.u_lo, 0), li(q.i_hi - q.i_lo, 0);
+    lvl[x].resize(q.len);
+    int32_t maxl = 0;
+    for (int64_t j = 0; j < q.len; ++j) {
+      const int64_t e = q.order ? q.order[j] : j;
+      int32_t& a = lu[q.u[e] - q.u_lo];
+      int32_t& b = li[q.i[e] - q.i_lo];
+      const int32_t l = std::max(a, b) + 1;
+      a = l;
+      b = l;
+      lvl[x][j] = l;
+      maxl = std::max(maxl, l);
+    }
+    cnt[x].assign(maxl + 1, 0);
+    for (int64_t j = 0; j < q.len; ++j) cnt[x][lvl[x][j]]++;
+  });
+  int64_t L = 0;
+  for (auto& c : cnt) L = std::max<int64_t>(L, static_cast<int64_t>(c.size()) - 1);
+  out.level_start.assign(L + 1, 0);
+  // cursor[x][l] = where sequence x writes its level-l entries (level-major, then sequence order)
+  std::vector<std::vector<int64_t>> cur(ns);
+  int64_t pos = 0;
+  for (int64_t l = 1; l <= L; ++l) {
+    out.level_start[l - 1] = pos;
+    for (int64_t x = 0; x < ns; ++x) {
+      if (cur[x].empty()) cur[x].assign(cnt[x].size(), 0);
+      if (l < static_cast<int64_t>(cnt[x].size())) { cur[x][l] = pos; pos += cnt[x][l]; }
+    }
+  }
+  out.level_start[L] = pos;
+  out.entries.resize(pos);
+  parallel_tasks(ns, [&](int64_t x) {
+    const OrderedSeq& q = seqs[x];
+    for (int64_t j = 0; j < q.len; ++j) {
+      const int64_t e = q.order ? q.order[j] : j;
+      out.entries[cur[x][lvl[x][j]]++] = DetEntry{q.u[e], q.i[e], q.r[e]};
+    }
+  });
+}
+
+int32_t choose_groups(int64_t avg_block_ratings, int32_t blocks_per_device, int32_t fast_waves) {
+  if (fast_waves < 0) return std::clamp(-fast_waves, 1, 4096);
+  const int32_t waves = fast_waves > 0 ? fast_waves : 2048;
+  int64_t g = waves / std::max(blocks_per_device, 1);
+  const int64_t cap = static_cast<int64_t>(std::sqrt(std::max<double>(avg_block_ratings, 1.0) / 8.0));
+  g = std::min(g, cap);
+  g = (g / 4) * 4;
+  return static_cast<int32_t>(std::clamp<int64_t>(g, 4, 1024));
+}
+
+namespace {
+// Longest-processing-time greedy: heaviest rows first into the least-loaded group.
+void lpt_groups(const std::vector<int64_t>& load, int32_t G, std::vector<int32_t>& group) {
+  const int64_t n = static_cast<int64_t>(load.size());
+  group.assign(n, 0);
+  std::vector<int32_t> order;
+  order.reserve(n);
+  for (int64_t x = 0; x < n; ++x) if (load[x] > 0) order.push_back(static_cast<int32_t>(x));
+  std::sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
+    return load[a] != load[b] ? load[a] > load[b] : a < b;
+  });
+  using E = std::pair<int64_t, int32_t>;
+  std::priority_queue<E, std::vector<E>, std::greater<E>> pq;
+  for (int32_t g = 0; g < G; ++g) pq.emplace(0, g);
+  for (int32_t x : order) {
+    E e = pq.top();
+    pq.pop();
+    group[x] = e.second;
+    e.first += load[x];
+    pq.push(e);
+  }
+}
+
+inline uint32_t mix32(uint64_t x) {
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;
+  return static_cast<uint32_t>(x);
+}
+}  // namespace
+
+// Fast-mode rotation schedule.  Within rating block (p, q): items of block q are split into
+// G groups and users of block p into G groups (both LPT-balanced by rating count in the
+// block); cell (t, g) holds the ratings with item group g and user group (g + t) mod G.
+// Cells of one sub-step t share no user or item row.  Inside a cell the ratings are ordered
+// by item (one contiguous run per item, so the item row stays in registers) and by a hash
+// of the user inside an item run.
+void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, const SideLayout& I,
+                     int32_t G, double lambda, uint64_t order_seed, std::vector<int64_t>* rec_src) {
+  const int32_t nb = rb.n_blocks;
+  const int64_t nb2 = static_cast<int64_t>(nb) * nb;
+  fp = FastPlan();
+  fp.G = G;
+  fp.rec_base.assign(nb2, -1);
+  fp.cell_base.assign(nb2, -1);
+  int64_t total = 0, cells = 0;
+  std::vector<int64_t> blocks;
+  for (int64_t b = 0; b < nb2; ++b) {
+    if (rb.size(b) <= 0) continue;
+    fp.rec_base[b] = total;
+    fp.cell_base[b] = cells;
+    total += rb.size(b);
+    cells += static_cast<int64_t>(G) * G + 1;
+    blocks.push_back(b);
+  }
+  fp.recs.resize(total);
+  fp.cell_off.assign(cells, 0);
+  if (rec_src) rec_src->assign(total, -1);
+  const int64_t GG = static_cast<int64_t>(G) * G;
+  parallel_tasks(static_cast<int64_t>(blocks.size()), [&](int64_t bx) {
+    const int64_t b = blocks[bx];
+    const int32_t p = static_cast<int32_t>(b / nb), q = static_cast<int32_t>(b % nb);
+    const int64_t ub = U.block_start[p], nu = U.block_start[p + 1] - ub;
+    const int64_t ib = I.block_start[q], ni = I.block_start[q + 1] - ib;
+    const int64_t s = rb.start[b], len = rb.size(b);
+    std::vector<int64_t> lu(nu, 0), li(ni, 0);
+    for (int64_t j = s; j < s + len; ++j) { lu[rb.urow[j] - ub]++; li[rb.irow[j] - ib]++; }
+    std::vector<int32_t> gu, gi;
+    lpt_groups(lu, G, gu);
+    lpt_groups(li, G, gi);
+    std::vector<std::pair<uint64_t, int64_t>> key(len);
+    for (int64_t x = 0; x < len; ++x) {
+      const int64_t j = s + x;
+      const uint32_t il = rb.irow[j] - static_cast<uint32_t>(ib);
+      const uint32_t ul = rb.urow[j] - static_cast<uint32_t>(ub);
+      const int32_t g = gi[il], h = gu[ul];
+      const int64_t t = ((h - g) % G + G) % G;
+      const uint64_t cell = static_cast<uint64_t>(t * G + g);
+      const uint64_t tie = mix32(order_seed ^ (static_cast<uint64_t>(rb.urow[j]) << 20)) & 0xFFFFu;
+      key[x] = {(cell << 40) | (static_cast<uint64_t>(il) << 16) | tie, x};
+    }
+    std::sort(key.begin(), key.end());
+    int32_t* off = fp.cell_off.data() + fp.cell_base[b];
+    FastRec* out = fp.recs.data() + fp.rec_base[b];
+    for (int64_t x = 0; x < len; ++x) {
+      const int64_t j = s + key[x].second;
+      const uint32_t urow = rb.urow[j];
+      out[x] = FastRec{urow, rb.irow[j], static_cast<float>(rb.r[j]),
+                       static_cast<float>(lambda / static_cast<double>(U.omega[urow]))};
+      if (rec_src) (*rec_src)[fp.rec_base[b] + x] = j;
+      off[(key[x].first >> 40) + 1]++;
+    }
+    for (int64_t c = 0; c < GG; ++c) off[c + 1] += off[c];
+  });
+}
+
+}  // namespace mfhip

@@ -1,0 +1,104 @@
+// plan.hpp -- host-side DSGD blocking and the two device schedules.
+//
+//  * SideLayout       initFactorBlockAndIndices (DSGDforMF.scala:513-588)
+//  * RatingBlocks     rating-block construction (DSGDforMF.scala:301-327, toRatingBlockId :597-601)
+//  * DetStratum       deterministic mode: one superstep's rating blocks in the reference's
+//                     shuffled order (:392-393), grouped into dependency levels so that a level
+//                     holds no two updates sharing a user or item row (bitwise == sequential)
+//  * FastBlock        fast mode: each rating block split into G item groups x G user groups;
+//                     sub-step t pairs item group g with user group (g+t) mod G, so every
+//                     in-flight update owns its user and item row (conflict-free batching)
+#pragma once
+#include <cstdint>
+#include <vector>
+
+#include "id_index.hpp"
+
+namespace mfhip {
+
+struct SideLayout {
+  int32_t n_blocks = 1;
+  std::vector<int32_t> row_id;       // row -> id; rows grouped by block, ids ascending in a block
+  std::vector<int32_t> omega;        // row -> number of ratings of the id (:537-541)
+  std::vector<int32_t> row_block;    // row -> factor block
+  std::vector<int64_t> block_start;  // n_blocks + 1
+  IdIndex index;                     // id -> row
+  int64_t rows() const { return static_cast<int64_t>(row_id.size()); }
+};
+
+// Builds the factor-block layout of one side from the rating column `ids`.
+// has_seed: block = new Random(id ^ seed).nextInt(n) and ids sorted in a block;
+// otherwise blocks come from an unseeded generator (the reference's scala.util.Random).
+void build_side(SideLayout& s, const int32_t* ids, int64_t n, int32_t n_blocks, int64_t seed,
+                bool has_seed);
+
+// Per-rating global rows (parallel lookup).
+void lookup_rows(const SideLayout& s, const int32_t* ids, int64_t n, std::vector<uint32_t>& rows);
+
+struct RatingBlocks {
+  int32_t n_blocks = 1;
+  std::vector<int64_t> start;   // n*n + 1, block b = ub*n + ib
+  std::vector<uint32_t> urow;   // global user row
+  std::vector<uint32_t> irow;   // global item row
+  std::vector<double> r;
+  std::vector<int64_t> src;     // input index per position (only when requested)
+  int64_t size(int64_t b) const { return start[b + 1] - start[b]; }
+};
+
+// Rating blocks for user blocks [ub_lo, ub_hi).  sort_ui reproduces the (user, item) order
+// the reference imposes when seeded (:319-323; ties keep input order).
+void build_rating_blocks(RatingBlocks& rb, const SideLayout& U, const SideLayout& I,
+                         const int32_t* u, const int32_t* i, const double* r, int64_t n,
+                         int32_t ub_lo, int32_t ub_hi, bool sort_ui, bool keep_src = false);
+
+// ---------------------------------------------------------------------------------------
+// Deterministic mode.
+struct DetEntry {
+  uint32_t u;  // global user row
+  uint32_t i;  // global item row
+  double r;
+};
+
+struct LevelPlan {
+  std::vector<DetEntry> entries;      // level-major
+  std::vector<int64_t> level_start;   // levels + 1
+  int64_t levels() const { return static_cast<int64_t>(level_start.size()) - 1; }
+};
+
+// Appends a sequence (in its exact sequential order) to per-row last-level trackers and
+// returns per-entry levels; rows of distinct sequences must be disjoint.
+// Groups a set of independent ordered sequences into one level plan.
+struct OrderedSeq {
+  const uint32_t* u;
+  const uint32_t* i;
+  const double* r;
+  const int32_t* order;  // may be null (identity)
+  int64_t len;
+  uint32_t u_lo, u_hi, i_lo, i_hi;  // row ranges touched (for the level trackers)
+};
+void build_level_plan(const std::vector<OrderedSeq>& seqs, LevelPlan& out);
+
+// ---------------------------------------------------------------------------------------
+// Fast mode.
+struct FastRec {
+  uint32_t u;   // global user row
+  uint32_t i;   // global item row
+  float r;
+  float ru;     // lambda / omega_u (f32)
+};
+
+struct FastPlan {
+  int32_t G = 4;                       // rotation groups per rating block
+  std::vector<FastRec> recs;           // all rating blocks of this shard, cell-major per block
+  std::vector<int64_t> rec_base;       // per rating block (n*n), -1 if not on this shard
+  std::vector<int32_t> cell_off;       // per included rating block: G*G+1 relative offsets
+  std::vector<int64_t> cell_base;      // per rating block: index into cell_off (-1 if absent)
+};
+
+int32_t choose_groups(int64_t avg_block_ratings, int32_t blocks_per_device, int32_t fast_waves);
+
+// rec_src (optional): for every record, its position in the RatingBlocks arrays.
+void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, const SideLayout& I,
+                     int32_t G, double lambda, uint64_t order_seed, std::vector<int64_t>* rec_src = nullptr);
+
+}  // namespace mfhip

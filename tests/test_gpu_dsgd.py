@@ -1,0 +1,216 @@
+"""Parity of the HIP DSGD path (libmfhip on the GPU) against the CPU oracle."""
+import numpy as np
+import pytest
+
+import coracle
+import mf_oracle as O
+import mfhip
+from conftest import golden
+from mfhip import _lib as L
+from mfhip import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def params(k, iterations, nb, seed, mode=L.MODE_DETERMINISTIC_F64, lam=1.0, lr=0.001, fast_waves=0, has_seed=1):
+    p = L.default_params()
+    p.num_factors, p.iterations, p.num_blocks, p.seed, p.mode = k, iterations, nb, seed, mode
+    p.lambda_, p.learning_rate, p.fast_waves, p.has_seed = lam, lr, fast_waves, has_seed
+    return p
+
+
+def assert_factors_equal(ctx, g):
+    ids, vecs = ctx.factors(L.SIDE_USER)
+    assert np.array_equal(ids, g["user_ids"])
+    assert np.array_equal(vecs, g["user_factors"]), np.abs(vecs - g["user_factors"]).max()
+    ids, vecs = ctx.factors(L.SIDE_ITEM)
+    assert np.array_equal(ids, g["item_ids"])
+    assert np.array_equal(vecs, g["item_factors"]), np.abs(vecs - g["item_factors"]).max()
+
+
+@pytest.mark.parametrize("name", ["spark_example_dsgd_n1", "spark_example_dsgd_n2", "spark_example_dsgd_n3",
+                                  "synthetic1k_dsgd_n3", "synthetic1k_dsgd_n4_seed_neg", "ml100k_like_dsgd_n4"])
+def test_deterministic_fit_bit_exact_vs_golden(name):
+    g = golden(name)
+    with mfhip.Context(params(int(g["k"]), int(g["iterations"]), int(g["n_blocks"]), int(g["seed"]),
+                              lam=float(g["lam"]), lr=float(g["lr"]))) as ctx:
+        ctx.fit(g["u"], g["i"], g["r"])
+        assert_factors_equal(ctx, g)
+        if "test_u" in g:
+            pred, found = ctx.predict(g["pred_u"], g["pred_i"])
+            assert found.all() and np.array_equal(pred, g["pred"])  # predictRating ddot, bit-exact
+            rm, cnt = ctx.rmse(g["test_u"], g["test_i"], g["test_r"])
+            assert cnt == int(g["test_matched"]) and abs(rm - float(g["test_rmse"])) <= 1e-12 * max(1, rm)
+            risk = ctx.empirical_risk(g["test_u"], g["test_i"], g["test_r"], float(g["lam"]))
+            assert abs(risk - float(g["risk"])) <= 1e-9 * abs(float(g["risk"]))
+
+
+def test_mirror_api_round_trip():
+    g = golden("spark_example_dsgd_n3")
+    ratings = list(zip(g["u"].tolist(), g["i"].tolist(), g["r"].tolist()))
+    sgd = mfhip.DSGDforMF().setNumFactors(4).setIterations(10).setBlocks(3).setSeed(0)
+    sgd.fit(ratings)
+    users, items = sgd.factorsOption
+    assert [f.id for f in users] == g["user_ids"].tolist()
+    assert np.array_equal(np.stack([f.vector for f in items]), g["item_factors"])
+    out = sgd.predict([(2, 13), (1, 1), (99, 1)])   # unknown user dropped (inner join)
+    assert [(a, b) for a, b, _ in out] == [(2, 13), (1, 1)]
+
+
+@pytest.mark.parametrize("k,nb,seed", [(1, 2, 0), (64, 4, 5), (100, 2, 1), (128, 8, 0), (130, 3, 2), (256, 2, 9)])
+def test_deterministic_vs_c_oracle_shapes(k, nb, seed):
+    d = synth.generate(700, 300, 15000, seed=seed + 10)
+    m = coracle.dsgd_fit(d.u, d.i, d.r, k=k, iterations=2, n_blocks=nb, seed=seed, lam=0.9, lr=0.002, threads=4)
+    with mfhip.Context(params(k, 2, nb, seed, lam=0.9, lr=0.002)) as ctx:
+        ctx.fit(d.u, d.i, d.r)
+        for side in (0, 1):
+            ids, vecs = ctx.factors(side)
+            rids, rvecs = m.factors(side)
+            assert np.array_equal(ids, rids)
+            assert np.array_equal(vecs, rvecs)
+
+
+@pytest.mark.parametrize("method,arg", [(1, 0.0), (2, 50.0), (3, 0.5), (4, 0.7)])
+def test_learning_rate_methods_bit_exact(method, arg):
+    d = synth.generate(200, 100, 4000, seed=4)
+    m = coracle.dsgd_fit(d.u, d.i, d.r, k=8, iterations=3, n_blocks=2, seed=1, lr=0.003, lr_method=method,
+                         lr_arg=arg)
+    p = params(8, 3, 2, 1, lr=0.003)
+    p.lr_method, p.lr_arg = method, arg
+    with mfhip.Context(p) as ctx:
+        ctx.fit(d.u, d.i, d.r)
+        assert np.array_equal(ctx.factors(0)[1], m.factors(0)[1])
+
+
+@pytest.mark.parametrize("shards", [2, 4])
+def test_multi_shard_ring_bit_exact(shards):
+    """n blocks over several shards (here virtual shards on device 0): the item-block ring must give the
+    same bits as one device (deterministic results identical at 1/2/4/8 GPUs)."""
+    d = synth.generate(900, 400, 30000, seed=21)
+    m = coracle.dsgd_fit(d.u, d.i, d.r, k=32, iterations=2, n_blocks=4, seed=3, threads=4)
+    with mfhip.Context(params(32, 2, 4, 3), devices=[0] * shards) as ctx:
+        ctx.fit(d.u, d.i, d.r)
+        for side in (0, 1):
+            assert np.array_equal(ctx.factors(side)[1], m.factors(side)[1])
+        pred, found = ctx.predict(d.u[:500], d.i[:500])
+        rp, rf = m.predict(d.u[:500], d.i[:500])
+        assert np.array_equal(pred, rp) and np.array_equal(found, rf)
+
+
+def test_staged_run_and_resume_equal_one_shot():
+    d = synth.generate(300, 150, 8000, seed=2)
+    m = coracle.dsgd_fit(d.u, d.i, d.r, k=16, iterations=3, n_blocks=3, seed=4)
+    with mfhip.Context(params(16, 3, 3, 4)) as ctx:
+        ctx.prepare(d.u, d.i, d.r)
+        ctx.run(4)
+        assert ctx.superstep == 4
+        uids, uv = ctx.factors(0)
+        iids, iv = ctx.factors(1)
+    with mfhip.Context(params(16, 3, 3, 4)) as ctx2:   # checkpoint restore
+        ctx2.prepare(d.u, d.i, d.r)
+        ctx2.set_factors(0, uids, uv)
+        ctx2.set_factors(1, iids, iv)
+        ctx2.superstep = 4
+        ctx2.run(5)
+        for side in (0, 1):
+            assert np.array_equal(ctx2.factors(side)[1], m.factors(side)[1])
+
+
+def test_block_update_exact():
+    rng = np.random.default_rng(8)
+    nu, ni, k, n = 30, 20, 12, 400
+    uidx = rng.integers(0, nu, n).astype(np.int32)
+    iidx = rng.integers(0, ni, n).astype(np.int32)
+    r = rng.random(n) * 5
+    users, items = rng.random((nu, k)), rng.random((ni, k))
+    uom = np.bincount(uidx, minlength=nu).astype(np.int32) + 1
+    iom = np.bincount(iidx, minlength=ni).astype(np.int32) + 1
+    a = mfhip.block_update(r, uidx, iidx, users, uom, items, iom, k, 2, 7, 5, 0.01, 0, 0.0, 1.0)
+    b = coracle.block_update(r, uidx, iidx, users, uom, items, iom, k, 2, 7, 5, 0.01, 0, 0.0, 1.0)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+def test_edge_cases():
+    with mfhip.Context(params(4, 2, 3, 0)) as ctx:   # empty input: empty model
+        ctx.fit(np.empty(0, np.int32), np.empty(0, np.int32), np.empty(0))
+        assert ctx.num_factors(0) == 0
+        pred, found = ctx.predict([1], [1])
+        assert not found.any()
+    # more blocks than ids -> empty rating blocks pass through (DSGDforMF.scala:482-487)
+    R = [(1, 1, 3.0), (2, 2, 4.0), (3, 1, 5.0)]
+    us, it = O.dsgd_fit(R, k=3, iterations=4, n_blocks=7, seed=1)
+    with mfhip.Context(params(3, 4, 7, 1)) as ctx:
+        ctx.fit([a for a, _, _ in R], [b for _, b, _ in R], [c for _, _, c in R])
+        ids, vecs = ctx.factors(0)
+        assert np.array_equal(vecs, np.array([us[x] for x in ids.tolist()]))
+    with pytest.raises(mfhip.MFError):
+        mfhip.Context(params(4, 1, 3, 0), devices=[0, 0])  .fit([1], [1], [1.0])  # 3 blocks on 2 shards
+
+
+def fast_replay_reference(d, k, nb, seed, G, iterations, lam, lr):
+    """Serialise the fast plan (superstep, sub-step, group, position) and replay it in f64."""
+    from test_schedule import fast_schedule
+    b, t, g, p = fast_schedule(d.u, d.i, nb, seed, G)
+    uids = np.unique(d.u); iids = np.unique(d.i)
+    urow = np.searchsorted(uids, d.u).astype(np.int32)
+    irow = np.searchsorted(iids, d.i).astype(np.int32)
+    U = np.stack([O.random_factors(k, O.JavaRandom(int(x) ^ seed)) for x in uids])
+    I = np.stack([O.random_factors(k, O.JavaRandom(int(x) ^ seed)) for x in iids])
+    ru = lam / np.bincount(urow).astype(np.float64)
+    ri = lam / np.bincount(irow).astype(np.float64)
+    for s in range(1, iterations * nb + 1):
+        eta = O.learning_rate(0, lr, s // nb + 1, lam)
+        in_stratum = ((b // nb + s - 1) % nb) == (b % nb)
+        idx = np.where(in_stratum)[0]
+        order = idx[np.lexsort((p[idx], g[idx], b[idx], t[idx]))]
+        coracle.dsgd_apply(urow[order], irow[order], d.r[order], U, I, ru, ri, k, eta)
+    return uids, U, iids, I
+
+
+@pytest.mark.parametrize("k,nb,G", [(64, 2, 8), (128, 3, 4), (40, 2, 4), (256, 1, 8)])
+def test_fast_kernel_equals_its_schedule(k, nb, G):
+    """The f32 sweep kernel (register ring, forwarding, item runs) == sequential replay of its plan."""
+    d = synth.generate(400, 120, 12000, seed=k)
+    seed, lam, lr, iters = 3, 1.0, 0.002, 2
+    uids, U, iids, I = fast_replay_reference(d, k, nb, seed, G, iters, lam, lr)
+    with mfhip.Context(params(k, iters, nb, seed, mode=L.MODE_FAST_F32, lam=lam, lr=lr, fast_waves=-G)) as ctx:
+        ctx.fit(d.u, d.i, d.r)
+        a_ids, a_u = ctx.factors(0)
+        b_ids, a_i = ctx.factors(1)
+    assert np.array_equal(a_ids, uids) and np.array_equal(b_ids, iids)
+    np.testing.assert_allclose(a_u, U, rtol=2e-4, atol=2e-5)
+    np.testing.assert_allclose(a_i, I, rtol=2e-4, atol=2e-5)
+
+
+def test_fast_mode_rmse_within_half_percent_of_reference():
+    d = synth.generate(20000, 3000, 1_000_000, seed=11)
+    (tu, ti, tr), (eu, ei, er) = d.split()
+    m = coracle.dsgd_fit(tu, ti, tr, k=32, iterations=10, n_blocks=4, seed=0, threads=4)
+    ref, _ = m.rmse(eu, ei, er)
+    with mfhip.Context(params(32, 10, 4, 0, mode=L.MODE_FAST_F32)) as ctx:
+        ctx.fit(tu, ti, tr)
+        fast, cnt = ctx.rmse(eu, ei, er)
+    assert abs(fast - ref) / ref < 0.005, (fast, ref)
+
+
+@pytest.mark.parametrize("shards", [2, 4])
+def test_fast_multi_shard_matches_single(shards):
+    d = synth.generate(2000, 500, 60000, seed=9)
+    outs = []
+    for devs in ([0], [0] * shards):
+        with mfhip.Context(params(64, 2, 4, 1, mode=L.MODE_FAST_F32, fast_waves=-8), devices=devs) as ctx:
+            ctx.fit(d.u, d.i, d.r)
+            outs.append((ctx.factors(0)[1], ctx.factors(1)[1]))
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+
+
+def test_profiling_stats():
+    d = synth.generate(3000, 800, 50000, seed=5)
+    with mfhip.Context(params(128, 1, 2, 0, mode=L.MODE_FAST_F32)) as ctx:
+        ctx.prepare(d.u, d.i, d.r)
+        ctx.set_profiling(True)
+        ctx.run(2)
+        st = ctx.stats()
+    assert st["updates"] == 50000 and st["supersteps"] == 2
+    assert st["kernel_launches"] == 2 * st["groups"] and st["kernel_ms"] > 0
+    assert st["algorithmic_bytes"] == 50000 * (16 * 128 + 20)

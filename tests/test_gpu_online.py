@@ -1,0 +1,72 @@
+"""Online micro-batch path on the GPU vs the oracle (SGDUpdater arithmetic, bit-exact in f64)."""
+import numpy as np
+import pytest
+
+import coracle
+import mf_oracle as O
+import mfhip
+from conftest import golden
+from mfhip import _lib as L
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name,flavour,P", [("spark_example_online_flink", "flink", 0),
+                                            ("spark_example_online_ps", "ps", 0),
+                                            ("spark_example_online_spark_p1", "spark", 1),
+                                            ("spark_example_online_spark_p2", "spark", 2),
+                                            ("spark_example_online_spark_p4", "spark", 4)])
+def test_spark_example_batches_bit_exact(name, flavour, P):
+    g = golden(name)
+    model = mfhip.OnlineMF(int(g["k"]), float(g["lr"]), flavour=flavour, num_partitions=max(P, 1))
+    start = 0
+    for sz in g["batch_sizes"].tolist():
+        sl = slice(start, start + sz)
+        model.update((g["u"][sl], g["i"][sl], g["r"][sl]))
+        start += sz
+    ids, vecs = model.ctx.factors(L.SIDE_USER)
+    assert np.array_equal(ids, g["user_ids"]) and np.array_equal(vecs, g["user_factors"])
+    ids, vecs = model.ctx.factors(L.SIDE_ITEM)
+    assert np.array_equal(ids, g["item_ids"]) and np.array_equal(vecs, g["item_factors"])
+
+
+def test_large_batch_arrival_order_bit_exact():
+    rng = np.random.default_rng(1)
+    n, k = 60000, 48
+    u = rng.integers(0, 3000, n).astype(np.int32)
+    i = (rng.zipf(1.3, n) % 500).astype(np.int32)
+    r = rng.integers(1, 6, n).astype(np.float64)
+    model = mfhip.OnlineMF(k, 0.005)
+    for s in range(0, n, 20000):
+        model.update((u[s:s + 20000], i[s:s + 20000], r[s:s + 20000]))
+    uids, iids = np.unique(u), np.unique(i)
+    U = np.stack([O.pseudo_random_factor(int(x), k) for x in uids])
+    I = np.stack([O.pseudo_random_factor(int(x), k) for x in iids])
+    coracle.online_apply(np.searchsorted(uids, u), np.searchsorted(iids, i), r, U, I, k, 0.005)
+    assert np.array_equal(model.ctx.factors(0)[1], U)
+    assert np.array_equal(model.ctx.factors(1)[1], I)
+
+
+def test_online_on_top_of_offline_model():
+    """Combined path: DSGD fit, then online micro-batches on the same GPU-resident model."""
+    from mfhip import synth
+    d = synth.generate(500, 200, 10000, seed=3)
+    p = L.default_params()
+    p.num_factors, p.iterations, p.num_blocks, p.online_learning_rate = 8, 2, 2, 0.01
+    ctx = mfhip.Context(p)
+    ctx.fit(d.u, d.i, d.r)
+    uids0, U0 = ctx.factors(0)
+    iids0, I0 = ctx.factors(1)
+    batch_u = np.array([d.u[0], 10**6, d.u[1]], np.int32)   # one unseen user
+    batch_i = np.array([d.i[0], d.i[0], 10**6 + 1], np.int32)  # one unseen item
+    batch_r = np.array([4.0, 2.0, 5.0])
+    tu, ti = ctx.online_update(batch_u, batch_i, batch_r)
+    assert (tu, ti) == (3, 2)
+    users = {int(a): v.tolist() for a, v in zip(uids0, U0)}
+    items = {int(a): v.tolist() for a, v in zip(iids0, I0)}
+    O.online_sequential(list(zip(batch_u.tolist(), batch_i.tolist(), batch_r.tolist())), users, items, 8, 0.01)
+    ids, vecs = ctx.factors(0)
+    assert np.array_equal(vecs, np.array([users[x] for x in ids.tolist()]))
+    ids, vecs = ctx.factors(1)
+    assert np.array_equal(vecs, np.array([items[x] for x in ids.tolist()]))
+    ctx.close()

@@ -1,0 +1,87 @@
+"""Host-side schedules (no GPU): dependency levels and the fast-mode rotation plan."""
+import numpy as np
+import pytest
+
+import coracle
+import mfhip
+from mfhip import _lib as L
+from mfhip import synth
+import ctypes as C
+
+
+def levels(u, i, order=None):
+    u = np.ascontiguousarray(u, np.uint32)
+    i = np.ascontiguousarray(i, np.uint32)
+    out = np.empty(max(len(u), 1), np.int32)
+    o = None if order is None else L.ptr(np.ascontiguousarray(order, np.int32), C.c_int32)
+    L.check(L.lib().mf_debug_levels(u.ctypes.data_as(C.POINTER(C.c_uint32)), i.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                    o, len(u), L.ptr(out, C.c_int32)))
+    return out[:len(u)]
+
+
+def test_levels_are_conflict_free_and_replay_sequential_order():
+    rng = np.random.default_rng(0)
+    nu, ni, n, k = 40, 25, 3000, 5
+    u = rng.integers(0, nu, n).astype(np.int32)
+    i = (rng.zipf(1.6, n) % ni).astype(np.int32)
+    r = rng.random(n) * 5
+    order = coracle.scala_shuffle(77, n)
+    lv = levels(u, i, order)
+    uo, io, ro = u[order], i[order], r[order]
+    for l in np.unique(lv):  # no two updates of a level share a row
+        m = lv == l
+        assert len(set(uo[m].tolist())) == m.sum() and len(set(io[m].tolist())) == m.sum()
+    # replaying level by level (stable inside a level) == the sequential order, bit for bit
+    U0 = rng.random((nu, k)); I0 = rng.random((ni, k))
+    ru = np.full(nu, 0.1); ri = np.full(ni, 0.2)
+    A_u, A_i = U0.copy(), I0.copy()
+    coracle.dsgd_apply(uo, io, ro, A_u, A_i, ru, ri, k, 0.01)
+    perm = np.argsort(lv, kind="stable")
+    B_u, B_i = U0.copy(), I0.copy()
+    coracle.dsgd_apply(uo[perm], io[perm], ro[perm], B_u, B_i, ru, ri, k, 0.01)
+    assert np.array_equal(A_u, B_u) and np.array_equal(A_i, B_i)
+
+
+def test_level_count_is_longest_row_chain_lower_bound():
+    u = np.zeros(50, np.int32)            # one hot user: a pure chain
+    i = np.arange(50, dtype=np.int32)
+    assert levels(u, i).max() == 50
+    assert levels(np.arange(50), np.arange(50)).max() == 1
+
+
+def fast_schedule(u, i, nb, seed, G):
+    n = len(u)
+    b = np.empty(n, np.int32); t = np.empty(n, np.int32); g = np.empty(n, np.int32); p = np.empty(n, np.int64)
+    L.check(L.lib().mf_debug_fast_schedule(L.ptr(L.as_i32(u), C.c_int32), L.ptr(L.as_i32(i), C.c_int32), n, nb,
+                                           seed, G, L.ptr(b, C.c_int32), L.ptr(t, C.c_int32), L.ptr(g, C.c_int32),
+                                           L.ptr(p, C.c_int64)))
+    return b, t, g, p
+
+
+@pytest.mark.parametrize("nb,G", [(1, 4), (3, 8), (4, 16)])
+def test_fast_rotation_is_conflict_free(nb, G):
+    d = synth.generate(500, 200, 20000, seed=1)
+    b, t, g, p = fast_schedule(d.u, d.i, nb, 3, G)
+    # blocks follow DSGD blocking of the reference
+    ub = np.array([mfhip.jvm.block_of(int(x), 3, nb) for x in d.u])
+    ib = np.array([mfhip.jvm.block_of(int(x), 3, nb) for x in d.i])
+    assert np.array_equal(b, ub * nb + ib)
+    # the stratum of superstep s holds blocks (p, p+s-1); within one (stratum, sub-step) no user or
+    # item row appears in two different cells
+    for s in range(nb):
+        in_stratum = ((b // nb + s) % nb) == (b % nb)
+        for tt in range(G):
+            m = in_stratum & (t == tt)
+            cell = b[m].astype(np.int64) * G + g[m]
+            for ids in (d.u[m], d.i[m]):
+                owner = {}
+                for x, c in zip(ids.tolist(), cell.tolist()):
+                    assert owner.setdefault(x, c) == c
+    # every item group owns its items for the whole block; every cell is item-contiguous
+    key = b.astype(np.int64) * G * G + t.astype(np.int64) * G + g
+    for c in np.unique(key)[:200]:
+        m = np.where(key == c)[0]
+        items_in_order = d.i[m[np.argsort(p[m])]]
+        runs = [items_in_order[0]] + [x for a, x in zip(items_in_order, items_in_order[1:]) if x != a]
+        assert len(runs) == len(set(runs))
+        assert sorted(p[m].tolist()) == list(range(len(m)))
