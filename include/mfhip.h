@@ -96,7 +96,9 @@ typedef struct mf_stats {
   double algorithmic_bytes;  /* updates x B(k) (16k+20 f32, 32k+24 f64)          */
   int64_t levels;            /* deterministic mode: dependency levels launched   */
   int32_t groups;            /* fast mode: rotation groups per rating block      */
-  int32_t reserved[5];
+  int32_t reserved0;
+  int64_t pads;              /* fast mode: no-op records the plan inserted       */
+  int32_t reserved[2];
 } mf_stats;
 
 typedef struct mf_ctx mf_ctx;

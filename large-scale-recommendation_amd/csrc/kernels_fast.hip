@@ -1,19 +1,29 @@
-// kernels_fast.hip -- fast-mode DSGD sweep (f32), one rotation sub-step per launch.
+// kernels_fast.hip -- fast-mode DSGD sweep (f32).
 //
 // Schedule (plan.cpp build_fast_plan): a rating block is split into G item groups x G user
-// groups; in sub-step t, wave g of a block sweeps cell (item group g, user group (g+t) mod G).
-// No two waves of a launch share a user or item row (conflict-free batching), so plain loads
-// and stores are race-free and kernel boundaries order the sub-steps.
+// groups; in rotation sub-step t, wave g of a block sweeps cell (item group g, user group
+// (g+t) mod G).  Cells of one sub-step share no user or item row (conflict-free batching).
+//
+// Two drivers of the same schedule (identical results, bit for bit):
+//  * k_fast_superstep (default): ONE persistent launch per superstep.  Wave g sweeps its G
+//    cells in order; before cell t it waits until wave g+1 has finished cell t-1 -- the only
+//    earlier user of user group (g+t) mod G in this superstep -- so the rotation runs as a
+//    systolic pipeline instead of G grid-wide barriers, and a wave holding a hot item never
+//    waits for the slowest cell of every sub-step.  Hand-off (MI355X_MICROARCH.md, Valid
+//    forms, row 1): every user-row byte is stored and loaded with sc1 (write-through, L1
+//    bypass), the wave drains with s_waitcnt vmcnt(0), then one lane stores the progress word
+//    with an agent-scope relaxed atomic; the consumer polls that word with sc1 loads.  Each
+//    workgroup is one wave.  Spins are bounded by s_memrealtime; a timeout sets err[0].
+//  * k_fast_substep: one launch per sub-step (kernel boundaries order the sub-steps).
 //
 // Inside a cell the ratings form one contiguous run per item: the item row lives in VGPRs
-// for the whole run (hot items never leave registers), user rows are gathered D ratings
-// ahead into a register ring and written back after their update.  A user that reappears
-// within the ring window gets the fresh row forwarded register-to-register, so the wave's
-// result equals the sequential sweep of its cell.
+// for the whole run (hot items never leave registers), user rows are gathered D ratings ahead
+// into a register ring and written back after their update.  The host orders each cell so a
+// user never repeats within the ring window (plan.cpp), so a wave's result equals the
+// sequential sweep of its cell.
 //
-// Per update (k=128): dot (KPL FMAs + DPP row reduction + 4 readlanes), two axpy rows,
-// one 512-B user-row gather and one 512-B scatter; B_f32(k) = 16k + 20 algorithmic bytes.
-// HBM-bound: roofline = 8 TB/s / B_f32(k) updates/s.
+// Per update (k=128): dot (KPL FMAs + DPP row reduction + 4 readlanes), two axpy rows, one
+// 512-B user-row gather and one 512-B scatter.  B_f32(k) = 16k + 20 algorithmic bytes.
 #include <hip/hip_runtime.h>
 
 #include "kernels.hpp"
@@ -22,6 +32,7 @@ namespace mfhip {
 namespace {
 
 constexpr uint32_t kNone = 0xffffffffu;
+constexpr uint32_t kPad = kPadBit;
 
 __device__ __forceinline__ uint32_t rl(uint32_t v, int l) {
   return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), l));
@@ -46,190 +57,337 @@ __device__ __forceinline__ float wave_sum(float v) {
   return (a + b) + (c + d);
 }
 
-// Row access: lane holds elements [lane*KPL, lane*KPL + KPL).  FULL: k == 64*KPL (vector I/O).
-template <int KPL, bool FULL>
-__device__ __forceinline__ void load_row(const float* __restrict__ row, int lane, int k, float (&v)[KPL]) {
+// ---- row I/O ------------------------------------------------------------------------------
+// A lane holds elements [lane*KPL, lane*KPL + KPL) of a row.  FULL: k == 64*KPL (vector I/O);
+// otherwise loads read a clamped in-row address and the k-tail is masked at use.  Rows are
+// read and written through buffer descriptors; AUX = 16 sets sc1 (write-through stores,
+// L1-bypassing loads) for rows handed between waves inside one launch.
+template <int KPL>
+struct Row {
+  float v[KPL];
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint64_t bytes) {
+  const uint32_t n = bytes > 0xffffffffull ? 0xffffffffu : static_cast<uint32_t>(bytes);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, n, 0x00020000);
+}
+
+template <int KPL, bool FULL, int AUX>
+__device__ __forceinline__ Row<KPL> load_row(__amdgpu_buffer_rsrc_t rs, uint32_t row, int lane, int k) {
+  Row<KPL> r;
+  const uint32_t base = row * static_cast<uint32_t>(k) * 4u;
   if constexpr (FULL) {
+    const uint32_t off = base + static_cast<uint32_t>(lane) * KPL * 4u;
     if constexpr (KPL == 1) {
-      v[0] = row[lane];
+      r.v[0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, AUX));
     } else if constexpr (KPL == 2) {
-      const float2 x = reinterpret_cast<const float2*>(row)[lane];
-      v[0] = x.x; v[1] = x.y;
+      const auto x = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, AUX);
+      r.v[0] = __uint_as_float(x[0]); r.v[1] = __uint_as_float(x[1]);
     } else {
 #pragma unroll
       for (int c = 0; c < KPL; c += 4) {
-        const float4 x = reinterpret_cast<const float4*>(row)[lane * (KPL / 4) + c / 4];
-        v[c] = x.x; v[c + 1] = x.y; v[c + 2] = x.z; v[c + 3] = x.w;
+        const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, off + c * 4u, 0, AUX);
+        r.v[c] = __uint_as_float(x[0]); r.v[c + 1] = __uint_as_float(x[1]);
+        r.v[c + 2] = __uint_as_float(x[2]); r.v[c + 3] = __uint_as_float(x[3]);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < KPL; ++c) {
+      const int f = min(lane * KPL + c, k - 1);  // clamped: the tail is masked at use
+      r.v[c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, base + static_cast<uint32_t>(f) * 4u, 0, AUX));
+    }
+  }
+  return r;
+}
+
+template <int KPL, bool FULL>
+__device__ __forceinline__ void mask_row(Row<KPL>& r, int lane, int k) {
+  if constexpr (!FULL) {
+#pragma unroll
+    for (int c = 0; c < KPL; ++c) r.v[c] = (lane * KPL + c < k) ? r.v[c] : 0.f;
+  }
+}
+
+template <int KPL, bool FULL, int AUX>
+__device__ __forceinline__ void store_row(__amdgpu_buffer_rsrc_t rs, uint32_t row, int lane, int k, const Row<KPL>& r) {
+  const uint32_t base = row * static_cast<uint32_t>(k) * 4u;
+  if constexpr (FULL) {
+    const uint32_t off = base + static_cast<uint32_t>(lane) * KPL * 4u;
+    if constexpr (KPL == 1) {
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.v[0]), rs, off, 0, AUX);
+    } else if constexpr (KPL == 2) {
+      using u2 = uint32_t __attribute__((ext_vector_type(2)));
+      u2 x = {__float_as_uint(r.v[0]), __float_as_uint(r.v[1])};
+      __builtin_amdgcn_raw_buffer_store_b64(x, rs, off, 0, AUX);
+    } else {
+      using u4 = uint32_t __attribute__((ext_vector_type(4)));
+#pragma unroll
+      for (int c = 0; c < KPL; c += 4) {
+        u4 x = {__float_as_uint(r.v[c]), __float_as_uint(r.v[c + 1]), __float_as_uint(r.v[c + 2]),
+                __float_as_uint(r.v[c + 3])};
+        __builtin_amdgcn_raw_buffer_store_b128(x, rs, off + c * 4u, 0, AUX);
       }
     }
   } else {
 #pragma unroll
     for (int c = 0; c < KPL; ++c) {
       const int f = lane * KPL + c;
-      v[c] = f < k ? row[f] : 0.f;
+      if (f < k) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.v[c]), rs, base + static_cast<uint32_t>(f) * 4u, 0, AUX);
     }
   }
 }
 
-template <int KPL, bool FULL>
-__device__ __forceinline__ void store_row(float* __restrict__ row, int lane, int k, const float (&v)[KPL]) {
-  if constexpr (FULL) {
-    if constexpr (KPL == 1) {
-      row[lane] = v[0];
-    } else if constexpr (KPL == 2) {
-      reinterpret_cast<float2*>(row)[lane] = make_float2(v[0], v[1]);
-    } else {
-#pragma unroll
-      for (int c = 0; c < KPL; c += 4)
-        reinterpret_cast<float4*>(row)[lane * (KPL / 4) + c / 4] = make_float4(v[c], v[c + 1], v[c + 2], v[c + 3]);
-    }
-  } else {
-#pragma unroll
-    for (int c = 0; c < KPL; ++c) {
-      const int f = lane * KPL + c;
-      if (f < k) row[f] = v[c];
+// Bounded wait until *flag >= want (sc1 polls).  Returns false on timeout (sets *err).
+__device__ __forceinline__ bool wait_flag(const int32_t* flag, int32_t want, int32_t* err) {
+  if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) return true;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+  while (true) {
+    __builtin_amdgcn_s_sleep(1);
+    if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) return true;
+    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {  // 1 s: a wave never arrived
+      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
     }
   }
 }
 
+// A record is 32 B = two uint4: {user row, item row | kPad, rating, lambda/omega_u} and
+// {lambda/omega_i, 0, 0, 0}.  The first two 64-record chunks of a cell go through VGPRs.
+__device__ __forceinline__ void stage_load(const uint4* __restrict__ recs, int64_t b, int64_t len, int lane,
+                                           uint4 (&st)[4]) {
+  const int64_t x0 = b + min<int64_t>(lane, len - 1), x1 = b + min<int64_t>(64 + lane, len - 1);
+  st[0] = recs[2 * x0];
+  st[1] = recs[2 * x0 + 1];
+  st[2] = recs[2 * x1];
+  st[3] = recs[2 * x1 + 1];
+}
+__device__ __forceinline__ void stage_store(uint4* lds, int lane, const uint4 (&st)[4]) {
+  lds[2 * lane] = st[0];
+  lds[2 * lane + 1] = st[1];
+  lds[2 * (64 + lane)] = st[2];
+  lds[2 * (64 + lane) + 1] = st[3];
+}
+
+// Sequential sweep of one cell: `len` records starting at recs[beg].  On entry the LDS
+// double buffer (128 records) holds the cell's first two 64-record chunks; chunk c+2 streams in
+// through VGPRs while chunk c is swept.  Every step issues the same memory operations
+// unconditionally -- prefetch of the user row and the item row of record j+D, store of the
+// updated user row and item row of record j -- so the compiler's vmcnt waits
+// stay counted (no control-flow join ever forces a full drain).  The item row is kept in VGPRs
+// across its run and written back every step (L2-resident); a record whose item differs from
+// the previous one adopts the prefetched row.  Host-side the cell order guarantees that a user
+// never repeats within kHazardWindow records (plan.cpp), and kPad records are no-ops (select,
+// NaN-safe), so the prefetched user row is always the current one.
+template <int KPL, bool FULL, int D, int UAUX>
+__device__ __forceinline__ void sweep_cell(int64_t beg, int64_t len, const uint4* __restrict__ recs,
+                                           uint4* lds, __amdgpu_buffer_rsrc_t urs, __amdgpu_buffer_rsrc_t irs,
+                                           int k, float eta, int lane) {
+  static_assert(D <= kHazardWindow && 64 % D == 0, "ring depth");
+  uint32_t su[D], si[D];
+  float sr[D], sru[D];
+  bool spad[D];
+  Row<KPL> rp[D], rq[D];
+  float rri[D];  // lambda / omega_i of the record (uniform)
+
+  // record of the next prefetch, read from LDS one step ahead of its use
+  uint4 nrec;
+  uint32_t nri;
+#define MF_FETCH(s, idx)                                                                  \
+  do {                                                                                    \
+    const uint4 rec_ = nrec;                                                              \
+    const uint32_t rri_ = nri;                                                            \
+    nrec = lds[2 * (((idx) + 1) & 127)];                                                  \
+    nri = lds[2 * (((idx) + 1) & 127) + 1].x;                                             \
+    su[s] = __builtin_amdgcn_readfirstlane(rec_.x);                                       \
+    const uint32_t iw_ = __builtin_amdgcn_readfirstlane(rec_.y);                          \
+    si[s] = iw_ & ~kPad;                                                                  \
+    spad[s] = (iw_ & kPad) != 0;                                                          \
+    sr[s] = __uint_as_float(__builtin_amdgcn_readfirstlane(rec_.z));                      \
+    sru[s] = __uint_as_float(__builtin_amdgcn_readfirstlane(rec_.w));                     \
+    rri[s] = __uint_as_float(__builtin_amdgcn_readfirstlane(rri_));                       \
+    rp[s] = load_row<KPL, FULL, UAUX>(urs, su[s], lane, k);                               \
+    rq[s] = load_row<KPL, FULL, 0>(irs, si[s], lane, k);                                  \
+  } while (0)
+
+  nrec = lds[0];
+  nri = lds[1].x;
+#pragma unroll
+  for (int s = 0; s < D; ++s) MF_FETCH(s, s);
+
+  Row<KPL> q;
+#pragma unroll
+  for (int c = 0; c < KPL; ++c) q.v[c] = 0.f;
+  float regi = 0.f;
+  uint32_t cur_i = kNone;
+  int64_t idx = 0;
+  for (int64_t c = 0;; ++c) {
+    // chunk c+2 is staged now (clamped, unconditional) and written to LDS after chunk c; the
+    // chunk's 64 steps are fully unrolled so the compiler counts vmcnt exactly across them.
+    const bool more = (c + 2) * 64 < len;
+    const int64_t sx = beg + min((c + 2) * 64 + lane, len - 1);
+    const uint4 stage0 = recs[2 * sx], stage1 = recs[2 * sx + 1];
+#pragma unroll
+    for (int jb = 0; jb < 64; jb += D) {
+#pragma unroll
+      for (int s = 0; s < D; ++s) {
+        if (idx >= len) goto done;
+        const bool nr = si[s] != cur_i;
+        cur_i = si[s];
+        Row<KPL> p = rp[s];
+        mask_row<KPL, FULL>(p, lane, k);
+        Row<KPL> qi = rq[s];
+        mask_row<KPL, FULL>(qi, lane, k);
+#pragma unroll
+        for (int e = 0; e < KPL; ++e) q.v[e] = nr ? qi.v[e] : q.v[e];
+        regi = nr ? rri[s] : regi;
+        float part = 0.f;
+#pragma unroll
+        for (int e = 0; e < KPL; ++e) part = fmaf(p.v[e], q.v[e], part);
+        const float err = sr[s] - wave_sum(part);
+        const bool pad = spad[s];
+        Row<KPL> pn;
+#pragma unroll
+        for (int e = 0; e < KPL; ++e) {
+          const float pv = p.v[e], qv = q.v[e];
+          const float np = pv - eta * (sru[s] * pv - err * qv);
+          const float nq = qv - eta * (regi * qv - err * pv);
+          pn.v[e] = pad ? pv : np;
+          q.v[e] = pad ? qv : nq;
+        }
+        store_row<KPL, FULL, UAUX>(urs, su[s], lane, k, pn);
+        store_row<KPL, FULL, 0>(irs, cur_i, lane, k, q);
+        MF_FETCH(s, idx + D);
+        ++idx;
+      }
+    }
+    if (more) {
+      lds[2 * ((c & 1) * 64 + lane)] = stage0;
+      lds[2 * ((c & 1) * 64 + lane) + 1] = stage1;
+    }
+  }
+done:
+#undef MF_FETCH
+  return;
+}
+
+// ---- one launch per sub-step ---------------------------------------------------------------
+// amdgpu_waves_per_eu(1, 4): the register budget of 4 waves/SIMD lets the scheduler keep the
+// ring loads D records ahead instead of sinking them toward their use to save VGPRs.
 template <int KPL, bool FULL>
-__global__ __launch_bounds__(256) void k_fast_substep(const FastBlk* __restrict__ blks, int nblk, int G,
-                                                      int t, const uint4* __restrict__ recs,
-                                                      const int32_t* __restrict__ cell_off,
-                                                      float* __restrict__ U, float* __restrict__ I,
-                                                      const float* __restrict__ regI, int k, float eta) {
-  constexpr int D = 4;  // user-row prefetch depth (register ring)
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_fast_substep(const FastBlk* __restrict__ blks, int nblk, int G,
+                                                     int t, const uint4* __restrict__ recs,
+                                                     const int32_t* __restrict__ cell_off,
+                                                     float* __restrict__ U, float* __restrict__ I,
+                                                     const float* __restrict__ regI, int k, float eta,
+                                                     uint64_t u_bytes, uint64_t i_bytes, uint64_t r_bytes) {
+  __shared__ uint4 lds[256];
+  const int lane = threadIdx.x;
   // blockIdx % nblk picks the rating block: with 8 blocks a block's waves share one XCD's L2.
   const int slot = static_cast<int>(blockIdx.x % static_cast<unsigned>(nblk));
-  const int g = static_cast<int>(blockIdx.x / static_cast<unsigned>(nblk)) * 4 + wave;
+  const int g = static_cast<int>(blockIdx.x / static_cast<unsigned>(nblk));
   if (g >= G) return;
   const FastBlk d = blks[slot];
   if (d.rec_base < 0) return;
   const int32_t* off = cell_off + d.cell_base + static_cast<int64_t>(t) * G + g;
-  const int64_t beg = d.rec_base + off[0];
-  const int64_t end = d.rec_base + off[1];
-  if (beg >= end) return;
+  const int64_t beg = d.rec_base + off[0], len = off[1] - off[0];
+  if (len <= 0) return;
+  uint4 st[4];
+  stage_load(recs, beg, len, lane, st);
+  stage_store(lds, lane, st);
+  sweep_cell<KPL, FULL, 8, 0>(beg, len, recs, lds, make_rsrc(U, u_bytes), make_rsrc(I, i_bytes), k, eta, lane);
+}
 
-  // Two 64-record chunks of the cell's record stream in VGPRs (lane l holds record cbase+l).
-  int64_t cbase = beg;
-  uint4 cur = make_uint4(kNone, kNone, 0u, 0u), nxt = cur;
-  if (cbase + lane < end) cur = recs[cbase + lane];
-  if (cbase + 64 + lane < end) nxt = recs[cbase + 64 + lane];
-
-  // Prefetch ring (slot s holds the record to be processed at position ≡ s mod D).
-  uint32_t ru[D], ri[D];
-  float rr[D], rreg[D], rregi[D];
-  bool rnew[D];
-  float rp[D][KPL], rq[D][KPL];
-  uint32_t last_item = kNone;
-
-  float q[KPL];
-  float regi = 0.f;
-  uint32_t cur_item = kNone;
-
-  auto fetch = [&](int64_t jj, uint32_t& u_o, uint32_t& i_o, float& r_o, float& reg_o, bool& new_o,
-                   float& regi_o, float (&p_o)[KPL], float (&q_o)[KPL], uint32_t just_u,
-                   const float (&just_p)[KPL]) {
-    if (jj >= end) { u_o = kNone; i_o = kNone; new_o = false; return; }
-    if (jj - cbase >= 128) {  // slide the record window by one chunk
-      cur = nxt;
-      cbase += 64;
-      nxt = make_uint4(kNone, kNone, 0u, 0u);
-      if (cbase + 64 + lane < end) nxt = recs[cbase + 64 + lane];
-    }
-    const int o = static_cast<int>(jj - cbase);
-    const uint4 x = o < 64 ? cur : nxt;
-    const int l = o & 63;
-    u_o = rl(x.x, l);
-    i_o = rl(x.y, l);
-    r_o = rlf(x.z, l);
-    reg_o = rlf(x.w, l);
-    if (u_o == just_u) {
-#pragma unroll
-      for (int c = 0; c < KPL; ++c) p_o[c] = just_p[c];
-    } else {
-      load_row<KPL, FULL>(U + static_cast<size_t>(u_o) * k, lane, k, p_o);
-    }
-    new_o = i_o != last_item;
-    if (new_o) {
-      load_row<KPL, FULL>(I + static_cast<size_t>(i_o) * k, lane, k, q_o);
-      regi_o = regI[i_o];
-      last_item = i_o;
-    }
-  };
-
+// ---- one persistent launch per superstep (systolic rotation) --------------------------------
+template <int KPL, bool FULL, int D>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_fast_superstep(const FastBlk* __restrict__ blks, int nblk, int G,
+                                                       const uint4* __restrict__ recs,
+                                                       const int32_t* __restrict__ cell_off,
+                                                       float* __restrict__ U, float* __restrict__ I,
+                                                       const float* __restrict__ regI, int k, float eta,
+                                                       uint64_t u_bytes, uint64_t i_bytes, uint64_t r_bytes,
+                                                       int32_t* __restrict__ progress, int32_t* __restrict__ err) {
+  __shared__ uint4 lds[256];
+  const int lane = threadIdx.x;
+  const int slot = static_cast<int>(blockIdx.x % static_cast<unsigned>(nblk));
+  const int g = static_cast<int>(blockIdx.x / static_cast<unsigned>(nblk));
+  if (g >= G) return;
+  const FastBlk d = blks[slot];
+  if (d.rec_base < 0) return;  // empty rating block: nobody waits on it
+  int32_t* prog = progress + static_cast<int64_t>(slot) * G;
+  const int32_t* off = cell_off + d.cell_base;
+  const int32_t* next_prog = prog + (g + 1 == G ? 0 : g + 1);
+  const __amdgpu_buffer_rsrc_t urs = make_rsrc(U, u_bytes), irs = make_rsrc(I, i_bytes);
+  // the first two record chunks of the next cell are staged in VGPRs one cell ahead
+  uint4 st[4];
   {
-    float dummy[KPL];
-#pragma unroll
-    for (int c = 0; c < KPL; ++c) dummy[c] = 0.f;
-#pragma unroll
-    for (int s = 0; s < D; ++s)
-      fetch(beg + s, ru[s], ri[s], rr[s], rreg[s], rnew[s], rregi[s], rp[s], rq[s], kNone, dummy);
+    const int64_t l0 = off[g + 1] - off[g];
+    if (l0 > 0) stage_load(recs, d.rec_base + off[g], l0, lane, st);
   }
-
-  for (int64_t j0 = beg; j0 < end; j0 += D) {
-#pragma unroll
-    for (int s = 0; s < D; ++s) {
-      const int64_t jj = j0 + s;
-      if (jj < end) {
-        if (rnew[s]) {  // a new item run starts: retire the old item row, adopt the prefetched one
-          if (cur_item != kNone) store_row<KPL, FULL>(I + static_cast<size_t>(cur_item) * k, lane, k, q);
-#pragma unroll
-          for (int c = 0; c < KPL; ++c) q[c] = rq[s][c];
-          regi = rregi[s];
-          cur_item = ri[s];
-        }
-        float part = 0.f;
-#pragma unroll
-        for (int c = 0; c < KPL; ++c) part = fmaf(rp[s][c], q[c], part);
-        const float e = rr[s] - wave_sum(part);
-        float pn[KPL];
-#pragma unroll
-        for (int c = 0; c < KPL; ++c) {
-          const float p = rp[s][c], qq = q[c];
-          pn[c] = p - eta * (rreg[s] * p - e * qq);
-          q[c] = qq - eta * (regi * qq - e * p);
-        }
-        const uint32_t u_now = ru[s];
-        store_row<KPL, FULL>(U + static_cast<size_t>(u_now) * k, lane, k, pn);
-        // forward the fresh user row to pending ring slots of the same user
-#pragma unroll
-        for (int s2 = 0; s2 < D; ++s2) {
-          if (s2 != s && ru[s2] == u_now) {
-#pragma unroll
-            for (int c = 0; c < KPL; ++c) rp[s2][c] = pn[c];
-          }
-        }
-        fetch(jj + D, ru[s], ri[s], rr[s], rreg[s], rnew[s], rregi[s], rp[s], rq[s], u_now, pn);
-      }
+  for (int t = 0; t < G; ++t) {
+    const int64_t cb = static_cast<int64_t>(t) * G + g;
+    const int64_t beg = d.rec_base + off[cb], len = off[cb + 1] - off[cb];
+    if (len > 0) stage_store(lds, lane, st);
+    if (t + 1 < G) {
+      const int64_t nb = static_cast<int64_t>(t + 1) * G + g;
+      const int64_t l1 = off[nb + 1] - off[nb];
+      if (l1 > 0) stage_load(recs, d.rec_base + off[nb], l1, lane, st);
     }
+    // user group (g+t) mod G was last swept by wave g+1 in sub-step t-1
+    if (t > 0 && G > 1 && !wait_flag(next_prog, t, err)) return;
+    if (len > 0) sweep_cell<KPL, FULL, D, 16>(beg, len, recs, lds, urs, irs, k, eta, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every user-row store of this wave has landed
+    if (lane == 0) __hip_atomic_store(prog + g, t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (cur_item != kNone) store_row<KPL, FULL>(I + static_cast<size_t>(cur_item) * k, lane, k, q);
 }
 
 template <int KPL>
 void fast_dispatch(hipStream_t st, dim3 grid, const FastBlk* blks, int nblk, int G, int t,
                    const FastRec* recs, const int32_t* off, float* U, float* I, const float* regI,
-                   int k, float eta) {
+                   int k, float eta, uint64_t ub, uint64_t ib, uint64_t rb) {
   const uint4* r = reinterpret_cast<const uint4*>(recs);
   if (k == 64 * KPL)
-    hipLaunchKernelGGL((k_fast_substep<KPL, true>), grid, dim3(256), 0, st, blks, nblk, G, t, r, off, U, I, regI, k, eta);
+    hipLaunchKernelGGL((k_fast_substep<KPL, true>), grid, dim3(64), 0, st, blks, nblk, G, t, r, off, U, I, regI, k, eta, ub, ib, rb);
   else
-    hipLaunchKernelGGL((k_fast_substep<KPL, false>), grid, dim3(256), 0, st, blks, nblk, G, t, r, off, U, I, regI, k, eta);
+    hipLaunchKernelGGL((k_fast_substep<KPL, false>), grid, dim3(64), 0, st, blks, nblk, G, t, r, off, U, I, regI, k, eta, ub, ib, rb);
+}
+
+template <int KPL, int D>
+void persistent_dispatch(hipStream_t st, const FastBlk* blks, int nblk, int G, const FastRec* recs,
+                         const int32_t* off, float* U, float* I, const float* regI, int k, float eta,
+                         uint64_t ub, uint64_t ib, uint64_t rb, int32_t* progress, int32_t* err) {
+  const uint4* r = reinterpret_cast<const uint4*>(recs);
+  const dim3 grid(static_cast<unsigned>(nblk * G)), block(64);
+  if (k == 64 * KPL)
+    hipLaunchKernelGGL((k_fast_superstep<KPL, true, D>), grid, block, 0, st, blks, nblk, G, r, off, U, I, regI, k,
+                       eta, ub, ib, rb, progress, err);
+  else
+    hipLaunchKernelGGL((k_fast_superstep<KPL, false, D>), grid, block, 0, st, blks, nblk, G, r, off, U, I, regI, k,
+                       eta, ub, ib, rb, progress, err);
 }
 
 }  // namespace
 
 void launch_fast_substep(hipStream_t st, const FastBlk* blks, int nblk, int G, int t,
                          const FastRec* recs, const int32_t* cell_off, float* U, float* I,
-                         const float* regI, int k, float eta) {
-  const dim3 grid(static_cast<unsigned>(nblk * ((G + 3) / 4)));
-  if (k <= 64) fast_dispatch<1>(st, grid, blks, nblk, G, t, recs, cell_off, U, I, regI, k, eta);
-  else if (k <= 128) fast_dispatch<2>(st, grid, blks, nblk, G, t, recs, cell_off, U, I, regI, k, eta);
-  else if (k <= 256) fast_dispatch<4>(st, grid, blks, nblk, G, t, recs, cell_off, U, I, regI, k, eta);
-  else fast_dispatch<8>(st, grid, blks, nblk, G, t, recs, cell_off, U, I, regI, k, eta);
+                         const float* regI, int k, float eta, uint64_t u_bytes, uint64_t i_bytes,
+                         uint64_t r_bytes) {
+  const dim3 grid(static_cast<unsigned>(nblk * G));
+  if (k <= 64) fast_dispatch<1>(st, grid, blks, nblk, G, t, recs, cell_off, U, I, regI, k, eta, u_bytes, i_bytes, r_bytes);
+  else if (k <= 128) fast_dispatch<2>(st, grid, blks, nblk, G, t, recs, cell_off, U, I, regI, k, eta, u_bytes, i_bytes, r_bytes);
+  else if (k <= 256) fast_dispatch<4>(st, grid, blks, nblk, G, t, recs, cell_off, U, I, regI, k, eta, u_bytes, i_bytes, r_bytes);
+  else fast_dispatch<8>(st, grid, blks, nblk, G, t, recs, cell_off, U, I, regI, k, eta, u_bytes, i_bytes, r_bytes);
+}
+
+void launch_fast_superstep(hipStream_t st, const FastBlk* blks, int nblk, int G, const FastRec* recs,
+                           const int32_t* cell_off, float* U, float* I, const float* regI, int k, float eta,
+                           uint64_t u_bytes, uint64_t i_bytes, uint64_t r_bytes, int32_t* progress,
+                           int32_t* err) {
+  if (k <= 64) persistent_dispatch<1, 8>(st, blks, nblk, G, recs, cell_off, U, I, regI, k, eta, u_bytes, i_bytes, r_bytes, progress, err);
+  else if (k <= 128) persistent_dispatch<2, 8>(st, blks, nblk, G, recs, cell_off, U, I, regI, k, eta, u_bytes, i_bytes, r_bytes, progress, err);
+  else if (k <= 256) persistent_dispatch<4, 8>(st, blks, nblk, G, recs, cell_off, U, I, regI, k, eta, u_bytes, i_bytes, r_bytes, progress, err);
+  else persistent_dispatch<8, 4>(st, blks, nblk, G, recs, cell_off, U, I, regI, k, eta, u_bytes, i_bytes, r_bytes, progress, err);
 }
 
 }  // namespace mfhip

@@ -59,6 +59,7 @@ struct Shard {
   PinnedBuf det_pin;
   // fast mode
   DevBuf fast_recs, fast_cells, fast_blks;
+  DevBuf fast_prog, fast_err;  // persistent sweep: progress words + timeout flag
   // evaluation scratch
   DevBuf ev_u, ev_i, ev_r, ev_mult, ev_out, ev_part;
   // profiling
@@ -86,6 +87,7 @@ struct mf_ctx {
   std::vector<int> item_loc;  // item block -> shard holding it
   mfhip::RatingBlocks rb;     // deterministic mode keeps the rating blocks on the host
   int32_t G_fast = 0;
+  bool fast_persistent = true;  // MFHIP_FAST_KERNEL=substep selects one launch per sub-step
   std::vector<int64_t> fast_rb_size;  // per rating block (fast mode)
   mf_stats stats{};
   bool profiling = false;
@@ -284,6 +286,15 @@ void sync_all(mf_ctx* ctx) {
   for (auto& s : ctx->shards) {
     DeviceGuard g(s.device);
     MF_HIP(hipStreamSynchronize(s.stream));
+    if (s.fast_err.get()) {
+      int32_t err = 0;
+      MF_HIP(hipMemcpy(&err, s.fast_err.get(), sizeof(err), hipMemcpyDeviceToHost));
+      if (err) {
+        MF_HIP(hipMemset(s.fast_err.get(), 0, sizeof(err)));
+        fail(MF_ERR_TIMEOUT, "fast sweep: a wave waited > 1 s for its neighbour (workgroups not co-resident?); "
+                             "set MFHIP_FAST_KERNEL=substep");
+      }
+    }
   }
   collect_profile(ctx);
 }
@@ -413,14 +424,25 @@ void fast_superstep(mf_ctx* ctx, Shard& s, int64_t superstep, double eta) {
     ups += ctx->fast_rb_size[static_cast<int64_t>(p) * n + q];
   }
   if (ups == 0) return;
-  for (int32_t t = 0; t < ctx->G_fast; ++t) {
+  if (ctx->fast_persistent) {
+    MF_HIP(hipMemsetAsync(s.fast_prog.get(), 0, s.fast_prog.bytes(), s.stream));
     LaunchTimer tm(s, ctx->profiling);
-    launch_fast_substep(s.stream, blks, ctx->c, ctx->G_fast, t, s.fast_recs.as<FastRec>(),
-                        s.fast_cells.as<int32_t>(), s.uf.as<float>(), s.itf.as<float>(),
-                        s.regi.as<float>(), ctx->P.num_factors, static_cast<float>(eta));
+    launch_fast_superstep(s.stream, blks, ctx->c, ctx->G_fast, s.fast_recs.as<FastRec>(), s.fast_cells.as<int32_t>(),
+                          s.uf.as<float>(), s.itf.as<float>(), s.regi.as<float>(), ctx->P.num_factors,
+                          static_cast<float>(eta), s.uf.bytes(), s.itf.bytes(), s.regi.bytes(),
+                          s.fast_prog.as<int32_t>(), s.fast_err.as<int32_t>());
+    ctx->stats.kernel_launches += 1;
+  } else {
+    for (int32_t t = 0; t < ctx->G_fast; ++t) {
+      LaunchTimer tm(s, ctx->profiling);
+      launch_fast_substep(s.stream, blks, ctx->c, ctx->G_fast, t, s.fast_recs.as<FastRec>(),
+                          s.fast_cells.as<int32_t>(), s.uf.as<float>(), s.itf.as<float>(),
+                          s.regi.as<float>(), ctx->P.num_factors, static_cast<float>(eta), s.uf.bytes(),
+                          s.itf.bytes(), s.regi.bytes());
+    }
+    ctx->stats.kernel_launches += ctx->G_fast;
   }
   MF_HIP(hipGetLastError());
-  ctx->stats.kernel_launches += ctx->G_fast;
   ctx->stats.updates += ups;
 }
 
@@ -531,13 +553,18 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
     const int64_t blocks_local = static_cast<int64_t>(hi - lo) * ctx->nb;
     ctx->G_fast = choose_groups(local / std::max<int64_t>(blocks_local, 1), ctx->c, ctx->P.fast_waves);
     FastPlan fp;
+    const uint32_t dummy = static_cast<uint32_t>(ctx->U.rows());  // zeroed row used by padding records
     build_fast_plan(fp, ctx->rb, ctx->U, ctx->I, ctx->G_fast, ctx->P.lambda,
-                    static_cast<uint64_t>(ctx->P.seed) * 0x9E3779B97F4A7C15ULL + 1);
+                    static_cast<uint64_t>(ctx->P.seed) * 0x9E3779B97F4A7C15ULL + 1, dummy);
+    ctx->stats.pads = fp.pads;
     ctx->fast_rb_size.assign(nb2, 0);
     for (int64_t b = 0; b < nb2; ++b) ctx->fast_rb_size[b] = ctx->rb.size(b);
     ctx->stats.groups = ctx->G_fast;
     for (auto& s : ctx->shards) {
+      ensure_rows(ctx, s, kSideU, ctx->U.rows() + 1);
       DeviceGuard g(s.device);
+      MF_HIP(hipMemset(s.uf.as<char>() + static_cast<size_t>(dummy) * ctx->P.num_factors * ctx->es, 0,
+                       static_cast<size_t>(ctx->P.num_factors) * ctx->es));
       s.fast_recs.alloc(std::max<size_t>(fp.recs.size(), 1) * sizeof(FastRec));
       s.fast_cells.alloc(std::max<size_t>(fp.cell_off.size(), 1) * sizeof(int32_t));
       if (!fp.recs.empty())
@@ -553,6 +580,9 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
           const int64_t b = static_cast<int64_t>(p) * ctx->nb + q;
           blks[static_cast<size_t>(sm) * ctx->c + j] = FastBlk{fp.rec_base[b], fp.cell_base[b] < 0 ? 0 : fp.cell_base[b]};
         }
+      s.fast_prog.alloc(static_cast<size_t>(ctx->c) * ctx->G_fast * sizeof(int32_t));
+      s.fast_err.alloc(16);
+      MF_HIP(hipMemset(s.fast_err.get(), 0, 16));
       s.fast_blks.alloc(blks.size() * sizeof(FastBlk));
       MF_HIP(hipMemcpy(s.fast_blks.get(), blks.data(), blks.size() * sizeof(FastBlk), hipMemcpyHostToDevice));
     }
@@ -814,6 +844,7 @@ mf_ctx* new_ctx(const mf_params* p) {
   ctx->P = *p;
   ctx->f64 = p->mode == MF_MODE_DETERMINISTIC_F64;
   ctx->es = ctx->f64 ? 8 : 4;
+  if (const char* v = std::getenv("MFHIP_FAST_KERNEL")) ctx->fast_persistent = std::string(v) != "substep";
   return ctx;
 }
 
@@ -1178,8 +1209,10 @@ int mf_reset_stats(mf_ctx* ctx) {
     MF_REQUIRE(ctx, "null context");
     sync_all(ctx);
     const int32_t groups = ctx->stats.groups;
+    const int64_t pads = ctx->stats.pads;
     ctx->stats = mf_stats{};
     ctx->stats.groups = groups;
+    ctx->stats.pads = pads;
   });
 }
 
@@ -1244,7 +1277,8 @@ int mf_debug_fast_schedule(const int32_t* u, const int32_t* i, int64_t n, int32_
     build_rating_blocks(rb, U, I, u, i, r.data(), n, 0, n_blocks, false, true);
     FastPlan fp;
     std::vector<int64_t> src;
-    build_fast_plan(fp, rb, U, I, groups, 1.0, static_cast<uint64_t>(seed) * 0x9E3779B97F4A7C15ULL + 1, &src);
+    build_fast_plan(fp, rb, U, I, groups, 1.0, static_cast<uint64_t>(seed) * 0x9E3779B97F4A7C15ULL + 1,
+                    static_cast<uint32_t>(U.rows()), &src);
     const int64_t nb2 = static_cast<int64_t>(n_blocks) * n_blocks;
     const int64_t GG = static_cast<int64_t>(groups) * groups;
     for (int64_t b = 0; b < nb2; ++b) {
@@ -1252,6 +1286,7 @@ int mf_debug_fast_schedule(const int32_t* u, const int32_t* i, int64_t n, int32_
       const int32_t* off = fp.cell_off.data() + fp.cell_base[b];
       for (int64_t cidx = 0; cidx < GG; ++cidx)
         for (int64_t x = off[cidx]; x < off[cidx + 1]; ++x) {
+          if (src[fp.rec_base[b] + x] < 0) continue;  // padding
           const int64_t j = rb.src[src[fp.rec_base[b] + x]];
           block_out[j] = static_cast<int32_t>(b);
           substep_out[j] = static_cast<int32_t>(cidx / groups);

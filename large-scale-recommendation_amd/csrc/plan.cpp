@@ -291,28 +291,24 @@ inline uint32_t mix32(uint64_t x) {
 // by item (one contiguous run per item, so the item row stays in registers) and by a hash
 // of the user inside an item run.
 void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, const SideLayout& I,
-                     int32_t G, double lambda, uint64_t order_seed, std::vector<int64_t>* rec_src) {
+                     int32_t G, double lambda, uint64_t order_seed, uint32_t dummy_row,
+                     std::vector<int64_t>* rec_src) {
   const int32_t nb = rb.n_blocks;
   const int64_t nb2 = static_cast<int64_t>(nb) * nb;
+  const int64_t GG = static_cast<int64_t>(G) * G;
   fp = FastPlan();
   fp.G = G;
   fp.rec_base.assign(nb2, -1);
   fp.cell_base.assign(nb2, -1);
-  int64_t total = 0, cells = 0;
   std::vector<int64_t> blocks;
-  for (int64_t b = 0; b < nb2; ++b) {
-    if (rb.size(b) <= 0) continue;
-    fp.rec_base[b] = total;
-    fp.cell_base[b] = cells;
-    total += rb.size(b);
-    cells += static_cast<int64_t>(G) * G + 1;
-    blocks.push_back(b);
-  }
-  fp.recs.resize(total);
-  fp.cell_off.assign(cells, 0);
-  if (rec_src) rec_src->assign(total, -1);
-  const int64_t GG = static_cast<int64_t>(G) * G;
-  parallel_tasks(static_cast<int64_t>(blocks.size()), [&](int64_t bx) {
+  for (int64_t b = 0; b < nb2; ++b)
+    if (rb.size(b) > 0) blocks.push_back(b);
+  const int64_t nblk = static_cast<int64_t>(blocks.size());
+  std::vector<std::vector<FastRec>> outs(nblk);
+  std::vector<std::vector<int64_t>> srcs(nblk);
+  std::vector<std::vector<int32_t>> offs(nblk);
+  std::vector<int64_t> pads(nblk, 0);
+  parallel_tasks(nblk, [&](int64_t bx) {
     const int64_t b = blocks[bx];
     const int32_t p = static_cast<int32_t>(b / nb), q = static_cast<int32_t>(b % nb);
     const int64_t ub = U.block_start[p], nu = U.block_start[p + 1] - ub;
@@ -335,17 +331,69 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
       key[x] = {(cell << 40) | (static_cast<uint64_t>(il) << 16) | tie, x};
     }
     std::sort(key.begin(), key.end());
-    int32_t* off = fp.cell_off.data() + fp.cell_base[b];
-    FastRec* out = fp.recs.data() + fp.rec_base[b];
-    for (int64_t x = 0; x < len; ++x) {
-      const int64_t j = s + key[x].second;
-      const uint32_t urow = rb.urow[j];
-      out[x] = FastRec{urow, rb.irow[j], static_cast<float>(rb.r[j]),
-                       static_cast<float>(lambda / static_cast<double>(U.omega[urow]))};
-      if (rec_src) (*rec_src)[fp.rec_base[b] + x] = j;
-      off[(key[x].first >> 40) + 1]++;
+    // Emit each cell run by run.  Inside an item run pick the first pending rating whose user
+    // has not been emitted within the last kHazardWindow positions; if none qualifies emit a
+    // no-op padding record.  last[ul] = (cell, position) of the user's latest emission.
+    std::vector<FastRec>& out = outs[bx];
+    std::vector<int64_t>& src = srcs[bx];
+    std::vector<int32_t>& off = offs[bx];
+    out.reserve(len + len / 64 + 16);
+    if (rec_src) src.reserve(len + len / 64 + 16);
+    off.assign(GG + 1, 0);
+    std::vector<std::pair<int64_t, int64_t>> last(nu, {-1, 0});
+    std::vector<int64_t> pend;
+    int64_t x = 0;
+    for (int64_t c = 0; c < GG; ++c) {
+      const int64_t cell_begin = static_cast<int64_t>(out.size());
+      while (x < len && static_cast<int64_t>(key[x].first >> 40) == c) {
+        const uint64_t il = (key[x].first >> 16) & 0xFFFFFFu;
+        pend.clear();
+        while (x < len && (key[x].first >> 16) == ((static_cast<uint64_t>(c) << 24) | il)) pend.push_back(key[x++].second);
+        size_t head = 0;
+        const uint32_t irow = static_cast<uint32_t>(ib + il);
+        while (head < pend.size()) {
+          const int64_t pos = static_cast<int64_t>(out.size()) - cell_begin;
+          size_t pick = pend.size();
+          for (size_t y = head; y < pend.size() && y < head + 4 * kHazardWindow; ++y) {
+            const auto& l = last[rb.urow[s + pend[y]] - ub];
+            if (l.first != c || pos - l.second >= kHazardWindow) { pick = y; break; }
+          }
+          if (pick == pend.size()) {  // every candidate conflicts: no-op record
+            out.push_back(FastRec{dummy_row, irow | kPadBit, 0.f, 0.f, 0.f, {0, 0, 0}});
+            if (rec_src) src.push_back(-1);
+            pads[bx]++;
+            continue;
+          }
+          std::swap(pend[head], pend[pick]);
+          const int64_t j = s + pend[head++];
+          const uint32_t urow = rb.urow[j];
+          last[urow - ub] = {c, pos};
+          out.push_back(FastRec{urow, rb.irow[j], static_cast<float>(rb.r[j]),
+                                static_cast<float>(lambda / static_cast<double>(U.omega[urow])),
+                                static_cast<float>(lambda / static_cast<double>(I.omega[rb.irow[j]])), {0, 0, 0}});
+          if (rec_src) src.push_back(j);
+        }
+      }
+      off[c + 1] = static_cast<int32_t>(out.size());
     }
-    for (int64_t c = 0; c < GG; ++c) off[c + 1] += off[c];
+  });
+  int64_t total = 0, cells = 0;
+  for (int64_t bx = 0; bx < nblk; ++bx) {
+    fp.rec_base[blocks[bx]] = total;
+    fp.cell_base[blocks[bx]] = cells;
+    total += static_cast<int64_t>(outs[bx].size());
+    cells += GG + 1;
+    fp.pads += pads[bx];
+  }
+  fp.recs.resize(total);
+  fp.cell_off.resize(cells);
+  if (rec_src) rec_src->resize(total);
+  parallel_tasks(nblk, [&](int64_t bx) {
+    const int64_t b = blocks[bx];
+    std::copy(outs[bx].begin(), outs[bx].end(), fp.recs.begin() + fp.rec_base[b]);
+    std::copy(offs[bx].begin(), offs[bx].end(), fp.cell_off.begin() + fp.cell_base[b]);
+    if (rec_src) std::copy(srcs[bx].begin(), srcs[bx].end(), rec_src->begin() + fp.rec_base[b]);
+    std::vector<FastRec>().swap(outs[bx]);
   });
 }
 

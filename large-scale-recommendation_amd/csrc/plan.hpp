@@ -80,12 +80,21 @@ void build_level_plan(const std::vector<OrderedSeq>& seqs, LevelPlan& out);
 
 // ---------------------------------------------------------------------------------------
 // Fast mode.
+// Fast-mode record.  Inside a cell no user occurs twice within kHazardWindow consecutive
+// records (the kernel prefetches user rows that far ahead); where reordering inside an item
+// run cannot achieve that, the plan inserts no-op records flagged kPadBit in `i` whose user
+// row is the zeroed dummy row (row index = user rows at plan time).
+constexpr uint32_t kPadBit = 0x80000000u;
+constexpr int kHazardWindow = 8;
 struct FastRec {
-  uint32_t u;   // global user row
-  uint32_t i;   // global item row
+  uint32_t u;   // global user row (the dummy row for padding)
+  uint32_t i;   // global item row (| kPadBit)
   float r;
   float ru;     // lambda / omega_u (f32)
+  float ri;     // lambda / omega_i (f32)
+  uint32_t pad_[3];
 };
+static_assert(sizeof(FastRec) == 32, "FastRec is two 16-B words");
 
 struct FastPlan {
   int32_t G = 4;                       // rotation groups per rating block
@@ -93,12 +102,15 @@ struct FastPlan {
   std::vector<int64_t> rec_base;       // per rating block (n*n), -1 if not on this shard
   std::vector<int32_t> cell_off;       // per included rating block: G*G+1 relative offsets
   std::vector<int64_t> cell_base;      // per rating block: index into cell_off (-1 if absent)
+  int64_t pads = 0;                    // padding records inserted
 };
 
 int32_t choose_groups(int64_t avg_block_ratings, int32_t blocks_per_device, int32_t fast_waves);
 
-// rec_src (optional): for every record, its position in the RatingBlocks arrays.
+// rec_src (optional): for every record, its position in the RatingBlocks arrays (-1: padding).
+// dummy_row: user row used by padding records (kept zero by the caller).
 void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, const SideLayout& I,
-                     int32_t G, double lambda, uint64_t order_seed, std::vector<int64_t>* rec_src = nullptr);
+                     int32_t G, double lambda, uint64_t order_seed, uint32_t dummy_row,
+                     std::vector<int64_t>* rec_src = nullptr);
 
 }  // namespace mfhip

@@ -76,7 +76,9 @@ class mf_stats(C.Structure):
         ("algorithmic_bytes", C.c_double),
         ("levels", C.c_int64),
         ("groups", C.c_int32),
-        ("reserved", C.c_int32 * 5),
+        ("reserved0", C.c_int32),
+        ("pads", C.c_int64),
+        ("reserved", C.c_int32 * 2),
     ]
 
 

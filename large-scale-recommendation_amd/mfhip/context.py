@@ -146,7 +146,7 @@ class Context:
     def stats(self) -> dict:
         s = L.mf_stats()
         check(L.lib().mf_get_stats(self._h, C.byref(s)))
-        return {f: getattr(s, f) for f, _ in L.mf_stats._fields_ if f != "reserved"}
+        return {f: getattr(s, f) for f, _ in L.mf_stats._fields_ if not f.startswith("reserved")}
 
     def reset_stats(self) -> None:
         check(L.lib().mf_reset_stats(self._h))
