@@ -179,7 +179,8 @@ def main():
             "config": {"workload": f"{a.config}-shaped DSGD {'fast' if a.mode == 'fast' else 'deterministic'}",
                        "users": int(nu * a.scale), "items": int(ni * a.scale), "ratings": int(nr * a.scale),
                        "train_ratings": int(len(tr)), "rank": k, "num_blocks": nb, "lambda": 1.0, "lr": 0.001,
-                       "lr_method": "Default", "groups": st["groups"], "parallelism": f"dsgd-ring{D.world}"},
+                       "lr_method": "Default", "groups": st["groups"], "pad_records": st["pads"],
+                       "parallelism": f"dsgd-ring{D.world}"},
             "rmse": round(rmse, 6), "rmse_epochs": a.warmup + a.steps, "rmse_matched": matched,
             "roofline": roof, "cpu_baseline": cpu,
             "setup_s": {"generate": round(t_gen, 2), "prepare": round(t_prep, 2)},

@@ -27,17 +27,19 @@ struct FastBlk {
   int64_t cell_base;  // its G*G+1 cell offsets in the cell table
 };
 // Factor slabs are addressed through 32-bit buffer offsets (u_bytes/i_bytes < 4 GiB each).
-void launch_fast_substep(hipStream_t st, const FastBlk* blks, int nblk, int G, int t,
-                         const FastRec* recs, const int32_t* cell_off, float* U, float* I,
-                         const float* regI, int k, float eta, uint64_t u_bytes, uint64_t i_bytes,
-                         uint64_t r_bytes);
+// dummy_i: an item row that is never written; dummy_u_store: a user row that is never read.
+// Cells of at least prio_len records run at raised wave priority (s_setprio 3).
+void launch_fast_substep(hipStream_t st, const FastBlk* blks, int nblk, int G, int t, const FastRec* recs,
+                         const int32_t* cell_off, float* U, float* I, int k, float eta, uint64_t u_bytes,
+                         uint64_t i_bytes, uint32_t dummy_i, uint32_t dummy_u_store, int prio_len);
 
 // Fast-mode sweep, one persistent launch per superstep: wave g of a block sweeps its G cells in
-// order and waits on wave g+1's progress word before each cell (progress: nblk*G int32, zeroed
-// before every launch; err[0] != 0 after a bounded wait timed out).
+// order and waits on wave g+1's progress word before each cell (progress: nblk*G*kProgStride
+// int32, zeroed before every launch; err[0] != 0 after a bounded wait timed out).
+constexpr int kProgStride = 32;  // one 128-B line per progress word
 void launch_fast_superstep(hipStream_t st, const FastBlk* blks, int nblk, int G, const FastRec* recs,
-                           const int32_t* cell_off, float* U, float* I, const float* regI, int k, float eta,
-                           uint64_t u_bytes, uint64_t i_bytes, uint64_t r_bytes, int32_t* progress,
+                           const int32_t* cell_off, float* U, float* I, int k, float eta, uint64_t u_bytes,
+                           uint64_t i_bytes, uint32_t dummy_i, uint32_t dummy_u_store, int32_t* progress,
                            int32_t* err);
 
 // Gather-dot over resolved pairs (row -1 = unknown id).  out[j] = p.q summed left to right in

@@ -143,7 +143,7 @@ __device__ __forceinline__ bool wait_flag(const int32_t* flag, int32_t want, int
   if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) return true;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
   while (true) {
-    __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_s_sleep(8);  // ~0.25 us back-off between polls
     if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) return true;
     if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
     if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {  // 1 s: a wave never arrived
@@ -183,7 +183,8 @@ __device__ __forceinline__ void stage_store(uint4* lds, int lane, const uint4 (&
 template <int KPL, bool FULL, int D, int UAUX>
 __device__ __forceinline__ void sweep_cell(int64_t beg, int64_t len, const uint4* __restrict__ recs,
                                            uint4* lds, __amdgpu_buffer_rsrc_t urs, __amdgpu_buffer_rsrc_t irs,
-                                           int k, float eta, int lane) {
+                                           int k, float eta, int lane, uint32_t dummy_i,
+                                           uint32_t dummy_u_store) {
   static_assert(D <= kHazardWindow && 64 % D == 0, "ring depth");
   uint32_t su[D], si[D];
   float sr[D], sru[D];
@@ -208,9 +209,13 @@ __device__ __forceinline__ void sweep_cell(int64_t beg, int64_t len, const uint4
     sru[s] = __uint_as_float(__builtin_amdgcn_readfirstlane(rec_.w));                     \
     rri[s] = __uint_as_float(__builtin_amdgcn_readfirstlane(rri_));                       \
     rp[s] = load_row<KPL, FULL, UAUX>(urs, su[s], lane, k);                               \
-    rq[s] = load_row<KPL, FULL, 0>(irs, si[s], lane, k);                                  \
+    /* the item row is only needed when a new run starts; otherwise read the never-written \
+       dummy row so no load ever trails a store to the row the run keeps updating */       \
+    rq[s] = load_row<KPL, FULL, 0>(irs, si[s] != last_fetched ? si[s] : dummy_i, lane, k); \
+    last_fetched = si[s];                                                                 \
   } while (0)
 
+  uint32_t last_fetched = kNone;
   nrec = lds[0];
   nri = lds[1].x;
 #pragma unroll
@@ -256,7 +261,8 @@ __device__ __forceinline__ void sweep_cell(int64_t beg, int64_t len, const uint4
           pn.v[e] = pad ? pv : np;
           q.v[e] = pad ? qv : nq;
         }
-        store_row<KPL, FULL, UAUX>(urs, su[s], lane, k, pn);
+        // padding stores go to a second dummy row that is never loaded (no store->load trail)
+        store_row<KPL, FULL, UAUX>(urs, pad ? dummy_u_store : su[s], lane, k, pn);
         store_row<KPL, FULL, 0>(irs, cur_i, lane, k, q);
         MF_FETCH(s, idx + D);
         ++idx;
@@ -280,8 +286,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
                                                      int t, const uint4* __restrict__ recs,
                                                      const int32_t* __restrict__ cell_off,
                                                      float* __restrict__ U, float* __restrict__ I,
-                                                     const float* __restrict__ regI, int k, float eta,
-                                                     uint64_t u_bytes, uint64_t i_bytes, uint64_t r_bytes) {
+                                                     int k, float eta, uint64_t u_bytes, uint64_t i_bytes,
+                                                     uint32_t dummy_i, uint32_t dummy_u_store, int prio_len) {
   __shared__ uint4 lds[256];
   const int lane = threadIdx.x;
   // blockIdx % nblk picks the rating block: with 8 blocks a block's waves share one XCD's L2.
@@ -293,10 +299,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
   const int32_t* off = cell_off + d.cell_base + static_cast<int64_t>(t) * G + g;
   const int64_t beg = d.rec_base + off[0], len = off[1] - off[0];
   if (len <= 0) return;
+  // the longest cells set the sub-step's length: give their waves issue priority on the SIMD
+  if (len >= prio_len) __builtin_amdgcn_s_setprio(3);
   uint4 st[4];
   stage_load(recs, beg, len, lane, st);
   stage_store(lds, lane, st);
-  sweep_cell<KPL, FULL, 8, 0>(beg, len, recs, lds, make_rsrc(U, u_bytes), make_rsrc(I, i_bytes), k, eta, lane);
+  sweep_cell<KPL, FULL, 8, 0>(beg, len, recs, lds, make_rsrc(U, u_bytes), make_rsrc(I, i_bytes), k, eta, lane,
+                              dummy_i, dummy_u_store);
 }
 
 // ---- one persistent launch per superstep (systolic rotation) --------------------------------
@@ -305,8 +314,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
                                                        const uint4* __restrict__ recs,
                                                        const int32_t* __restrict__ cell_off,
                                                        float* __restrict__ U, float* __restrict__ I,
-                                                       const float* __restrict__ regI, int k, float eta,
-                                                       uint64_t u_bytes, uint64_t i_bytes, uint64_t r_bytes,
+                                                       int k, float eta, uint64_t u_bytes, uint64_t i_bytes,
+                                                       uint32_t dummy_i, uint32_t dummy_u_store,
                                                        int32_t* __restrict__ progress, int32_t* __restrict__ err) {
   __shared__ uint4 lds[256];
   const int lane = threadIdx.x;
@@ -315,9 +324,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
   if (g >= G) return;
   const FastBlk d = blks[slot];
   if (d.rec_base < 0) return;  // empty rating block: nobody waits on it
-  int32_t* prog = progress + static_cast<int64_t>(slot) * G;
+  // one 128-B line per progress word: pollers of different waves never share a line
+  int32_t* prog = progress + static_cast<int64_t>(slot) * G * kProgStride;
   const int32_t* off = cell_off + d.cell_base;
-  const int32_t* next_prog = prog + (g + 1 == G ? 0 : g + 1);
+  const int32_t* next_prog = prog + static_cast<int64_t>(g + 1 == G ? 0 : g + 1) * kProgStride;
   const __amdgpu_buffer_rsrc_t urs = make_rsrc(U, u_bytes), irs = make_rsrc(I, i_bytes);
   // the first two record chunks of the next cell are staged in VGPRs one cell ahead
   uint4 st[4];
@@ -336,58 +346,62 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
     }
     // user group (g+t) mod G was last swept by wave g+1 in sub-step t-1
     if (t > 0 && G > 1 && !wait_flag(next_prog, t, err)) return;
-    if (len > 0) sweep_cell<KPL, FULL, D, 16>(beg, len, recs, lds, urs, irs, k, eta, lane);
+    if (len > 0) sweep_cell<KPL, FULL, D, 16>(beg, len, recs, lds, urs, irs, k, eta, lane, dummy_i, dummy_u_store);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every user-row store of this wave has landed
-    if (lane == 0) __hip_atomic_store(prog + g, t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) __hip_atomic_store(prog + static_cast<int64_t>(g) * kProgStride, t + 1, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
 template <int KPL>
 void fast_dispatch(hipStream_t st, dim3 grid, const FastBlk* blks, int nblk, int G, int t,
-                   const FastRec* recs, const int32_t* off, float* U, float* I, const float* regI,
-                   int k, float eta, uint64_t ub, uint64_t ib, uint64_t rb) {
+                   const FastRec* recs, const int32_t* off, float* U, float* I, int k, float eta, uint64_t ub,
+                   uint64_t ib, uint32_t di, uint32_t du, int prio_len) {
   const uint4* r = reinterpret_cast<const uint4*>(recs);
   if (k == 64 * KPL)
-    hipLaunchKernelGGL((k_fast_substep<KPL, true>), grid, dim3(64), 0, st, blks, nblk, G, t, r, off, U, I, regI, k, eta, ub, ib, rb);
+    hipLaunchKernelGGL((k_fast_substep<KPL, true>), grid, dim3(64), 0, st, blks, nblk, G, t, r, off, U, I, k, eta, ub, ib, di, du, prio_len);
   else
-    hipLaunchKernelGGL((k_fast_substep<KPL, false>), grid, dim3(64), 0, st, blks, nblk, G, t, r, off, U, I, regI, k, eta, ub, ib, rb);
+    hipLaunchKernelGGL((k_fast_substep<KPL, false>), grid, dim3(64), 0, st, blks, nblk, G, t, r, off, U, I, k, eta, ub, ib, di, du, prio_len);
 }
 
 template <int KPL, int D>
 void persistent_dispatch(hipStream_t st, const FastBlk* blks, int nblk, int G, const FastRec* recs,
-                         const int32_t* off, float* U, float* I, const float* regI, int k, float eta,
-                         uint64_t ub, uint64_t ib, uint64_t rb, int32_t* progress, int32_t* err) {
+                         const int32_t* off, float* U, float* I, int k, float eta, uint64_t ub, uint64_t ib,
+                         uint32_t di, uint32_t du, int32_t* progress, int32_t* err) {
   const uint4* r = reinterpret_cast<const uint4*>(recs);
   const dim3 grid(static_cast<unsigned>(nblk * G)), block(64);
   if (k == 64 * KPL)
-    hipLaunchKernelGGL((k_fast_superstep<KPL, true, D>), grid, block, 0, st, blks, nblk, G, r, off, U, I, regI, k,
-                       eta, ub, ib, rb, progress, err);
+    hipLaunchKernelGGL((k_fast_superstep<KPL, true, D>), grid, block, 0, st, blks, nblk, G, r, off, U, I, k, eta, ub,
+                       ib, di, du, progress, err);
   else
-    hipLaunchKernelGGL((k_fast_superstep<KPL, false, D>), grid, block, 0, st, blks, nblk, G, r, off, U, I, regI, k,
-                       eta, ub, ib, rb, progress, err);
+    hipLaunchKernelGGL((k_fast_superstep<KPL, false, D>), grid, block, 0, st, blks, nblk, G, r, off, U, I, k, eta, ub,
+                       ib, di, du, progress, err);
 }
 
 }  // namespace
 
-void launch_fast_substep(hipStream_t st, const FastBlk* blks, int nblk, int G, int t,
-                         const FastRec* recs, const int32_t* cell_off, float* U, float* I,
-                         const float* regI, int k, float eta, uint64_t u_bytes, uint64_t i_bytes,
-                         uint64_t r_bytes) {
+void launch_fast_substep(hipStream_t st, const FastBlk* blks, int nblk, int G, int t, const FastRec* recs,
+                         const int32_t* cell_off, float* U, float* I, int k, float eta, uint64_t u_bytes,
+                         uint64_t i_bytes, uint32_t dummy_i, uint32_t dummy_u_store, int prio_len) {
   const dim3 grid(static_cast<unsigned>(nblk * G));
-  if (k <= 64) fast_dispatch<1>(st, grid, blks, nblk, G, t, recs, cell_off, U, I, regI, k, eta, u_bytes, i_bytes, r_bytes);
-  else if (k <= 128) fast_dispatch<2>(st, grid, blks, nblk, G, t, recs, cell_off, U, I, regI, k, eta, u_bytes, i_bytes, r_bytes);
-  else if (k <= 256) fast_dispatch<4>(st, grid, blks, nblk, G, t, recs, cell_off, U, I, regI, k, eta, u_bytes, i_bytes, r_bytes);
-  else fast_dispatch<8>(st, grid, blks, nblk, G, t, recs, cell_off, U, I, regI, k, eta, u_bytes, i_bytes, r_bytes);
+#define MF_ARGS st, grid, blks, nblk, G, t, recs, cell_off, U, I, k, eta, u_bytes, i_bytes, dummy_i, dummy_u_store, prio_len
+  if (k <= 64) fast_dispatch<1>(MF_ARGS);
+  else if (k <= 128) fast_dispatch<2>(MF_ARGS);
+  else if (k <= 256) fast_dispatch<4>(MF_ARGS);
+  else fast_dispatch<8>(MF_ARGS);
+#undef MF_ARGS
 }
 
 void launch_fast_superstep(hipStream_t st, const FastBlk* blks, int nblk, int G, const FastRec* recs,
-                           const int32_t* cell_off, float* U, float* I, const float* regI, int k, float eta,
-                           uint64_t u_bytes, uint64_t i_bytes, uint64_t r_bytes, int32_t* progress,
+                           const int32_t* cell_off, float* U, float* I, int k, float eta, uint64_t u_bytes,
+                           uint64_t i_bytes, uint32_t dummy_i, uint32_t dummy_u_store, int32_t* progress,
                            int32_t* err) {
-  if (k <= 64) persistent_dispatch<1, 8>(st, blks, nblk, G, recs, cell_off, U, I, regI, k, eta, u_bytes, i_bytes, r_bytes, progress, err);
-  else if (k <= 128) persistent_dispatch<2, 8>(st, blks, nblk, G, recs, cell_off, U, I, regI, k, eta, u_bytes, i_bytes, r_bytes, progress, err);
-  else if (k <= 256) persistent_dispatch<4, 8>(st, blks, nblk, G, recs, cell_off, U, I, regI, k, eta, u_bytes, i_bytes, r_bytes, progress, err);
-  else persistent_dispatch<8, 4>(st, blks, nblk, G, recs, cell_off, U, I, regI, k, eta, u_bytes, i_bytes, r_bytes, progress, err);
+#define MF_ARGS st, blks, nblk, G, recs, cell_off, U, I, k, eta, u_bytes, i_bytes, dummy_i, dummy_u_store, progress, err
+  if (k <= 64) persistent_dispatch<1, 8>(MF_ARGS);
+  else if (k <= 128) persistent_dispatch<2, 8>(MF_ARGS);
+  else if (k <= 256) persistent_dispatch<4, 8>(MF_ARGS);
+  else persistent_dispatch<8, 4>(MF_ARGS);
+#undef MF_ARGS
 }
 
 }  // namespace mfhip

@@ -87,7 +87,9 @@ struct mf_ctx {
   std::vector<int> item_loc;  // item block -> shard holding it
   mfhip::RatingBlocks rb;     // deterministic mode keeps the rating blocks on the host
   int32_t G_fast = 0;
-  bool fast_persistent = true;  // MFHIP_FAST_KERNEL=substep selects one launch per sub-step
+  uint32_t fast_dummy_u = 0, fast_dummy_i = 0;  // zeroed rows past the real ones (padding / idle prefetch)
+  int32_t fast_prio_len = 1 << 30;  // cells at least this long run at raised priority
+  bool fast_persistent = false;  // MFHIP_FAST_KERNEL=persistent selects the systolic single launch
   std::vector<int64_t> fast_rb_size;  // per rating block (fast mode)
   mf_stats stats{};
   bool profiling = false;
@@ -428,17 +430,17 @@ void fast_superstep(mf_ctx* ctx, Shard& s, int64_t superstep, double eta) {
     MF_HIP(hipMemsetAsync(s.fast_prog.get(), 0, s.fast_prog.bytes(), s.stream));
     LaunchTimer tm(s, ctx->profiling);
     launch_fast_superstep(s.stream, blks, ctx->c, ctx->G_fast, s.fast_recs.as<FastRec>(), s.fast_cells.as<int32_t>(),
-                          s.uf.as<float>(), s.itf.as<float>(), s.regi.as<float>(), ctx->P.num_factors,
-                          static_cast<float>(eta), s.uf.bytes(), s.itf.bytes(), s.regi.bytes(),
+                          s.uf.as<float>(), s.itf.as<float>(), ctx->P.num_factors, static_cast<float>(eta),
+                          s.uf.bytes(), s.itf.bytes(), ctx->fast_dummy_i, ctx->fast_dummy_u + 1,
                           s.fast_prog.as<int32_t>(), s.fast_err.as<int32_t>());
     ctx->stats.kernel_launches += 1;
   } else {
     for (int32_t t = 0; t < ctx->G_fast; ++t) {
       LaunchTimer tm(s, ctx->profiling);
       launch_fast_substep(s.stream, blks, ctx->c, ctx->G_fast, t, s.fast_recs.as<FastRec>(),
-                          s.fast_cells.as<int32_t>(), s.uf.as<float>(), s.itf.as<float>(),
-                          s.regi.as<float>(), ctx->P.num_factors, static_cast<float>(eta), s.uf.bytes(),
-                          s.itf.bytes(), s.regi.bytes());
+                          s.fast_cells.as<int32_t>(), s.uf.as<float>(), s.itf.as<float>(), ctx->P.num_factors,
+                          static_cast<float>(eta), s.uf.bytes(), s.itf.bytes(), ctx->fast_dummy_i,
+                          ctx->fast_dummy_u + 1, ctx->fast_prio_len);
     }
     ctx->stats.kernel_launches += ctx->G_fast;
   }
@@ -557,14 +559,29 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
     build_fast_plan(fp, ctx->rb, ctx->U, ctx->I, ctx->G_fast, ctx->P.lambda,
                     static_cast<uint64_t>(ctx->P.seed) * 0x9E3779B97F4A7C15ULL + 1, dummy);
     ctx->stats.pads = fp.pads;
+    {  // priority threshold: 3x the mean non-empty cell length
+      int64_t cells = 0, recs = 0;
+      for (int64_t b = 0; b < nb2; ++b)
+        if (fp.cell_base[b] >= 0) {
+          const int32_t* o = fp.cell_off.data() + fp.cell_base[b];
+          for (int64_t c2 = 0; c2 < static_cast<int64_t>(ctx->G_fast) * ctx->G_fast; ++c2) cells += o[c2 + 1] > o[c2];
+          recs += o[static_cast<int64_t>(ctx->G_fast) * ctx->G_fast];
+        }
+      ctx->fast_prio_len = cells ? static_cast<int32_t>(std::max<int64_t>(16, 3 * recs / cells)) : (1 << 30);
+      if (const char* v = std::getenv("MFHIP_PRIO_LEN")) ctx->fast_prio_len = std::atoi(v);
+    }
     ctx->fast_rb_size.assign(nb2, 0);
     for (int64_t b = 0; b < nb2; ++b) ctx->fast_rb_size[b] = ctx->rb.size(b);
     ctx->stats.groups = ctx->G_fast;
+    ctx->fast_dummy_u = dummy;
+    ctx->fast_dummy_i = static_cast<uint32_t>(ctx->I.rows());
     for (auto& s : ctx->shards) {
-      ensure_rows(ctx, s, kSideU, ctx->U.rows() + 1);
+      ensure_rows(ctx, s, kSideU, ctx->U.rows() + 2);
+      ensure_rows(ctx, s, MF_SIDE_ITEM, ctx->I.rows() + 1);
       DeviceGuard g(s.device);
-      MF_HIP(hipMemset(s.uf.as<char>() + static_cast<size_t>(dummy) * ctx->P.num_factors * ctx->es, 0,
-                       static_cast<size_t>(ctx->P.num_factors) * ctx->es));
+      const size_t row_bytes = static_cast<size_t>(ctx->P.num_factors) * ctx->es;
+      MF_HIP(hipMemset(s.uf.as<char>() + static_cast<size_t>(dummy) * row_bytes, 0, 2 * row_bytes));
+      MF_HIP(hipMemset(s.itf.as<char>() + static_cast<size_t>(ctx->fast_dummy_i) * row_bytes, 0, row_bytes));
       s.fast_recs.alloc(std::max<size_t>(fp.recs.size(), 1) * sizeof(FastRec));
       s.fast_cells.alloc(std::max<size_t>(fp.cell_off.size(), 1) * sizeof(int32_t));
       if (!fp.recs.empty())
@@ -580,7 +597,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
           const int64_t b = static_cast<int64_t>(p) * ctx->nb + q;
           blks[static_cast<size_t>(sm) * ctx->c + j] = FastBlk{fp.rec_base[b], fp.cell_base[b] < 0 ? 0 : fp.cell_base[b]};
         }
-      s.fast_prog.alloc(static_cast<size_t>(ctx->c) * ctx->G_fast * sizeof(int32_t));
+      s.fast_prog.alloc(static_cast<size_t>(ctx->c) * ctx->G_fast * kProgStride * sizeof(int32_t));
       s.fast_err.alloc(16);
       MF_HIP(hipMemset(s.fast_err.get(), 0, 16));
       s.fast_blks.alloc(blks.size() * sizeof(FastBlk));
@@ -844,7 +861,7 @@ mf_ctx* new_ctx(const mf_params* p) {
   ctx->P = *p;
   ctx->f64 = p->mode == MF_MODE_DETERMINISTIC_F64;
   ctx->es = ctx->f64 ? 8 : 4;
-  if (const char* v = std::getenv("MFHIP_FAST_KERNEL")) ctx->fast_persistent = std::string(v) != "substep";
+  if (const char* v = std::getenv("MFHIP_FAST_KERNEL")) ctx->fast_persistent = std::string(v) == "persistent";
   return ctx;
 }
 

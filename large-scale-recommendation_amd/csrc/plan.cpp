@@ -245,11 +245,15 @@ void build_level_plan(const std::vector<OrderedSeq>& seqs, LevelPlan& out) {
   });
 }
 
+// G trades launch/cell overhead and the record padding forced by heavy users (large G) against
+// cell imbalance (small G).  The per-superstep critical path is the sum over sub-steps of the
+// longest cell; on the NFLX-shaped synthetic it is minimal near ~90 ratings per average cell
+// (G = 128 for 1.4M-rating blocks), which this rule targets.
 int32_t choose_groups(int64_t avg_block_ratings, int32_t blocks_per_device, int32_t fast_waves) {
   if (fast_waves < 0) return std::clamp(-fast_waves, 1, 4096);
   const int32_t waves = fast_waves > 0 ? fast_waves : 2048;
   int64_t g = waves / std::max(blocks_per_device, 1);
-  const int64_t cap = static_cast<int64_t>(std::sqrt(std::max<double>(avg_block_ratings, 1.0) / 8.0));
+  const int64_t cap = static_cast<int64_t>(std::sqrt(std::max<double>(avg_block_ratings, 1.0) / 90.0));
   g = std::min(g, cap);
   g = (g / 4) * 4;
   return static_cast<int32_t>(std::clamp<int64_t>(g, 4, 1024));
@@ -331,41 +335,65 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
       key[x] = {(cell << 40) | (static_cast<uint64_t>(il) << 16) | tie, x};
     }
     std::sort(key.begin(), key.end());
-    // Emit each cell run by run.  Inside an item run pick the first pending rating whose user
-    // has not been emitted within the last kHazardWindow positions; if none qualifies emit a
-    // no-op padding record.  last[ul] = (cell, position) of the user's latest emission.
+    // Emit each cell run by run.  A user must not recur within kHazardWindow positions.  At a
+    // run boundary choose, among the cell's remaining item runs (longest first), one whose
+    // pending ratings offer a non-conflicting user; inside a run pick the first
+    // non-conflicting pending rating.  Only when nothing qualifies emit a no-op record.
+    // last[ul] = (cell, position) of the user's latest emission.
     std::vector<FastRec>& out = outs[bx];
     std::vector<int64_t>& src = srcs[bx];
     std::vector<int32_t>& off = offs[bx];
-    out.reserve(len + len / 64 + 16);
-    if (rec_src) src.reserve(len + len / 64 + 16);
+    out.reserve(len + len / 16 + 16);
+    if (rec_src) src.reserve(len + len / 16 + 16);
     off.assign(GG + 1, 0);
     std::vector<std::pair<int64_t, int64_t>> last(nu, {-1, 0});
-    std::vector<int64_t> pend;
+    struct Run { uint32_t irow; std::vector<int64_t> pend; size_t head = 0; };
+    std::vector<Run> runs;
+    std::vector<int32_t> alive;
     int64_t x = 0;
     for (int64_t c = 0; c < GG; ++c) {
       const int64_t cell_begin = static_cast<int64_t>(out.size());
+      runs.clear();
       while (x < len && static_cast<int64_t>(key[x].first >> 40) == c) {
         const uint64_t il = (key[x].first >> 16) & 0xFFFFFFu;
-        pend.clear();
-        while (x < len && (key[x].first >> 16) == ((static_cast<uint64_t>(c) << 24) | il)) pend.push_back(key[x++].second);
-        size_t head = 0;
-        const uint32_t irow = static_cast<uint32_t>(ib + il);
-        while (head < pend.size()) {
-          const int64_t pos = static_cast<int64_t>(out.size()) - cell_begin;
-          size_t pick = pend.size();
-          for (size_t y = head; y < pend.size() && y < head + 4 * kHazardWindow; ++y) {
-            const auto& l = last[rb.urow[s + pend[y]] - ub];
-            if (l.first != c || pos - l.second >= kHazardWindow) { pick = y; break; }
-          }
-          if (pick == pend.size()) {  // every candidate conflicts: no-op record
-            out.push_back(FastRec{dummy_row, irow | kPadBit, 0.f, 0.f, 0.f, {0, 0, 0}});
-            if (rec_src) src.push_back(-1);
-            pads[bx]++;
-            continue;
-          }
-          std::swap(pend[head], pend[pick]);
-          const int64_t j = s + pend[head++];
+        Run rn;
+        rn.irow = static_cast<uint32_t>(ib + il);
+        while (x < len && (key[x].first >> 16) == ((static_cast<uint64_t>(c) << 24) | il)) rn.pend.push_back(key[x++].second);
+        runs.push_back(std::move(rn));
+      }
+      alive.resize(runs.size());
+      std::iota(alive.begin(), alive.end(), 0);
+      std::stable_sort(alive.begin(), alive.end(), [&](int32_t a2, int32_t b2) {
+        return runs[a2].pend.size() > runs[b2].pend.size();
+      });
+      auto candidate = [&](Run& rn, int64_t pos) -> size_t {  // index of a non-conflicting rating or npos
+        for (size_t y = rn.head; y < rn.pend.size() && y < rn.head + 4 * kHazardWindow; ++y) {
+          const auto& l = last[rb.urow[s + rn.pend[y]] - ub];
+          if (l.first != c || pos - l.second >= kHazardWindow) return y;
+        }
+        return static_cast<size_t>(-1);
+      };
+      auto emit_pad = [&](uint32_t irow) {
+        out.push_back(FastRec{dummy_row, irow | kPadBit, 0.f, 0.f, 0.f, {0, 0, 0}});
+        if (rec_src) src.push_back(-1);
+        pads[bx]++;
+      };
+      uint32_t cur_irow = runs.empty() ? 0u : runs[alive[0]].irow;
+      while (!alive.empty()) {
+        int64_t pos = static_cast<int64_t>(out.size()) - cell_begin;
+        size_t ai = alive.size();
+        for (size_t z = 0; z < alive.size(); ++z)
+          if (candidate(runs[alive[z]], pos) != static_cast<size_t>(-1)) { ai = z; break; }
+        if (ai == alive.size()) { emit_pad(cur_irow); continue; }
+        Run& rn = runs[alive[ai]];
+        alive.erase(alive.begin() + ai);
+        cur_irow = rn.irow;
+        while (rn.head < rn.pend.size()) {
+          pos = static_cast<int64_t>(out.size()) - cell_begin;
+          const size_t pick = candidate(rn, pos);
+          if (pick == static_cast<size_t>(-1)) { emit_pad(cur_irow); continue; }
+          std::swap(rn.pend[rn.head], rn.pend[pick]);
+          const int64_t j = s + rn.pend[rn.head++];
           const uint32_t urow = rb.urow[j];
           last[urow - ub] = {c, pos};
           out.push_back(FastRec{urow, rb.irow[j], static_cast<float>(rb.r[j]),
