@@ -83,6 +83,21 @@ class Dist:
             self.dist.destroy_process_group()
 
 
+def pmc_traffic(a, k, groups):
+    """HBM bytes per launch of the dominant kernel from a committed rocprofv3 --pmc summary
+    (tools/pmc_summary.py) of the same workload, or (None, None)."""
+    import glob
+    paths = [a.traffic_json] if a.traffic_json else sorted(
+        glob.glob(os.path.join(ROOT, "profiles", f"r*_traffic_{a.config}_{a.mode}.json")))
+    for path in reversed(paths):
+        if not path or not os.path.exists(path):
+            continue
+        rec = json.load(open(path))
+        if rec.get("rank") == k and rec.get("groups") in (groups, 0) and a.scale == 1.0:
+            return rec["bytes_per_launch"], os.path.relpath(path, ROOT)
+    return None, None
+
+
 def cpu_baseline(tu, ti, tr, k, nb, supersteps):
     """Oracle C restatement (f64, exact reference order), one thread per block of a stratum."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -119,7 +134,8 @@ def main():
     p.fast_waves = a.fast_waves
     if D.world > 1:
         uid = D.bcast_bytes(mfhip.Context.unique_id() if D.rank == 0 else None)
-        ctx = mfhip.Context(p, rank=(D.local_rank, D.world, D.rank, uid))
+        dev = D.local_rank % max(1, mfhip.device_count())  # identity on a full node
+        ctx = mfhip.Context(p, rank=(dev, D.world, D.rank, uid))
     else:
         ctx = mfhip.Context(p)
     t0 = time.time()
@@ -156,14 +172,12 @@ def main():
     roof = None
     if st["kernel_ms"] > 0:
         achieved = alg_bytes_local / (st["kernel_ms"] / 1e3) / 1e9  # GB/s, this rank's dominant kernel
-        traffic = None
-        if a.traffic_json and os.path.exists(a.traffic_json):
-            traffic = json.load(open(a.traffic_json)).get("bytes_per_launch")
+        traffic, traffic_src = pmc_traffic(a, k, st["groups"])
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "kernel": "k_fast_substep" if a.mode == "fast" else "k_level",
                 "bytes_per_update": bpu, "avg_launch_us": round(st["kernel_ms"] * 1e3 / max(launches, 1), 2),
-                "launches": launches}
+                "launches": launches, "traffic_source": traffic_src}
 
     cpu = None
     if D.rank == 0 and D.world == 1 and not a.no_cpu_baseline:
