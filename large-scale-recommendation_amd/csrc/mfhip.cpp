@@ -431,7 +431,7 @@ void fast_superstep(mf_ctx* ctx, Shard& s, int64_t superstep, double eta) {
     LaunchTimer tm(s, ctx->profiling);
     launch_fast_superstep(s.stream, blks, ctx->c, ctx->G_fast, s.fast_recs.as<FastRec>(), s.fast_cells.as<int32_t>(),
                           s.uf.as<float>(), s.itf.as<float>(), ctx->P.num_factors, static_cast<float>(eta),
-                          s.uf.bytes(), s.itf.bytes(), ctx->fast_dummy_i, ctx->fast_dummy_u + 1,
+                          s.uf.bytes(), s.itf.bytes(), ctx->fast_dummy_i * 4u * ctx->P.num_factors,
                           s.fast_prog.as<int32_t>(), s.fast_err.as<int32_t>());
     ctx->stats.kernel_launches += 1;
   } else {
@@ -439,8 +439,8 @@ void fast_superstep(mf_ctx* ctx, Shard& s, int64_t superstep, double eta) {
       LaunchTimer tm(s, ctx->profiling);
       launch_fast_substep(s.stream, blks, ctx->c, ctx->G_fast, t, s.fast_recs.as<FastRec>(),
                           s.fast_cells.as<int32_t>(), s.uf.as<float>(), s.itf.as<float>(), ctx->P.num_factors,
-                          static_cast<float>(eta), s.uf.bytes(), s.itf.bytes(), ctx->fast_dummy_i,
-                          ctx->fast_dummy_u + 1, ctx->fast_prio_len);
+                          static_cast<float>(eta), s.uf.bytes(), s.itf.bytes(),
+                          ctx->fast_dummy_i * 4u * ctx->P.num_factors, ctx->fast_prio_len);
     }
     ctx->stats.kernel_launches += ctx->G_fast;
   }
@@ -556,7 +556,10 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
     ctx->G_fast = choose_groups(local / std::max<int64_t>(blocks_local, 1), ctx->c, ctx->P.fast_waves);
     FastPlan fp;
     const uint32_t dummy = static_cast<uint32_t>(ctx->U.rows());  // zeroed row used by padding records
-    build_fast_plan(fp, ctx->rb, ctx->U, ctx->I, ctx->G_fast, ctx->P.lambda,
+    MF_REQUIRE(static_cast<uint64_t>(ctx->U.rows() + 2) * ctx->P.num_factors * 4 < (1ull << 32) &&
+                   static_cast<uint64_t>(ctx->I.rows() + 1) * ctx->P.num_factors * 4 < (1ull << 32),
+               "fast mode addresses each factor slab with 32-bit offsets (< 4 GiB)");
+    build_fast_plan(fp, ctx->rb, ctx->U, ctx->I, ctx->G_fast, ctx->P.num_factors, ctx->P.lambda,
                     static_cast<uint64_t>(ctx->P.seed) * 0x9E3779B97F4A7C15ULL + 1, dummy);
     ctx->stats.pads = fp.pads;
     {  // priority threshold: 3x the mean non-empty cell length
@@ -1294,7 +1297,7 @@ int mf_debug_fast_schedule(const int32_t* u, const int32_t* i, int64_t n, int32_
     build_rating_blocks(rb, U, I, u, i, r.data(), n, 0, n_blocks, false, true);
     FastPlan fp;
     std::vector<int64_t> src;
-    build_fast_plan(fp, rb, U, I, groups, 1.0, static_cast<uint64_t>(seed) * 0x9E3779B97F4A7C15ULL + 1,
+    build_fast_plan(fp, rb, U, I, groups, 1, 1.0, static_cast<uint64_t>(seed) * 0x9E3779B97F4A7C15ULL + 1,
                     static_cast<uint32_t>(U.rows()), &src);
     const int64_t nb2 = static_cast<int64_t>(n_blocks) * n_blocks;
     const int64_t GG = static_cast<int64_t>(groups) * groups;

@@ -295,8 +295,9 @@ inline uint32_t mix32(uint64_t x) {
 // by item (one contiguous run per item, so the item row stays in registers) and by a hash
 // of the user inside an item run.
 void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, const SideLayout& I,
-                     int32_t G, double lambda, uint64_t order_seed, uint32_t dummy_row,
+                     int32_t G, int32_t k, double lambda, uint64_t order_seed, uint32_t dummy_row,
                      std::vector<int64_t>* rec_src) {
+  const uint32_t row_bytes = static_cast<uint32_t>(k) * 4u;
   const int32_t nb = rb.n_blocks;
   const int64_t nb2 = static_cast<int64_t>(nb) * nb;
   const int64_t GG = static_cast<int64_t>(G) * G;
@@ -374,7 +375,7 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
         return static_cast<size_t>(-1);
       };
       auto emit_pad = [&](uint32_t irow) {
-        out.push_back(FastRec{dummy_row, irow | kPadBit, 0.f, 0.f, 0.f, {0, 0, 0}});
+        out.push_back(FastRec{dummy_row * row_bytes, irow * row_bytes, 0.f, 0.f, 0.f, dummy_row, irow | kPadBit, 0});
         if (rec_src) src.push_back(-1);
         pads[bx]++;
       };
@@ -396,9 +397,10 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
           const int64_t j = s + rn.pend[rn.head++];
           const uint32_t urow = rb.urow[j];
           last[urow - ub] = {c, pos};
-          out.push_back(FastRec{urow, rb.irow[j], static_cast<float>(rb.r[j]),
+          out.push_back(FastRec{urow * row_bytes, rb.irow[j] * row_bytes, static_cast<float>(rb.r[j]),
                                 static_cast<float>(lambda / static_cast<double>(U.omega[urow])),
-                                static_cast<float>(lambda / static_cast<double>(I.omega[rb.irow[j]])), {0, 0, 0}});
+                                static_cast<float>(lambda / static_cast<double>(I.omega[rb.irow[j]])), urow,
+                                rb.irow[j], 0});
           if (rec_src) src.push_back(j);
         }
       }

@@ -80,19 +80,24 @@ void build_level_plan(const std::vector<OrderedSeq>& seqs, LevelPlan& out);
 
 // ---------------------------------------------------------------------------------------
 // Fast mode.
-// Fast-mode record.  Inside a cell no user occurs twice within kHazardWindow consecutive
-// records (the kernel prefetches user rows that far ahead); where reordering inside an item
-// run cannot achieve that, the plan inserts no-op records flagged kPadBit in `i` whose user
-// row is the zeroed dummy row (row index = user rows at plan time).
+// Fast-mode record (32 B).  The kernel reads the first five words: byte offsets of the user
+// and item rows in their slabs (row * k * 4) and the three per-update scalars.  Inside a cell
+// no user occurs twice within kHazardWindow consecutive records (the kernel prefetches user
+// rows that far ahead); where reordering inside an item run cannot achieve that, the plan
+// inserts padding records: user = the zeroed dummy row, r = ru = ri = 0, item = the run's item.
+// Such a record is an exact no-op of the update arithmetic (e = 0, the item row scaled by 1),
+// so the kernel needs no flag; kPadBit in `i` marks it for host-side tools and tests.
 constexpr uint32_t kPadBit = 0x80000000u;
 constexpr int kHazardWindow = 8;
 struct FastRec {
-  uint32_t u;   // global user row (the dummy row for padding)
-  uint32_t i;   // global item row (| kPadBit)
+  uint32_t u_off;  // user row byte offset in the user slab
+  uint32_t i_off;  // item row byte offset in the item slab
   float r;
-  float ru;     // lambda / omega_u (f32)
-  float ri;     // lambda / omega_i (f32)
-  uint32_t pad_[3];
+  float ru;        // lambda / omega_u (f32)
+  float ri;        // lambda / omega_i (f32)
+  uint32_t u;      // global user row (the dummy row for padding)
+  uint32_t i;      // global item row (| kPadBit for padding)
+  uint32_t pad_;
 };
 static_assert(sizeof(FastRec) == 32, "FastRec is two 16-B words");
 
@@ -108,9 +113,10 @@ struct FastPlan {
 int32_t choose_groups(int64_t avg_block_ratings, int32_t blocks_per_device, int32_t fast_waves);
 
 // rec_src (optional): for every record, its position in the RatingBlocks arrays (-1: padding).
-// dummy_row: user row used by padding records (kept zero by the caller).
+// dummy_row: user row used by padding records (kept zero by the caller).  k: row length in
+// floats (record offsets are row * k * 4 and must stay below 4 GiB).
 void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, const SideLayout& I,
-                     int32_t G, double lambda, uint64_t order_seed, uint32_t dummy_row,
+                     int32_t G, int32_t k, double lambda, uint64_t order_seed, uint32_t dummy_row,
                      std::vector<int64_t>* rec_src = nullptr);
 
 }  // namespace mfhip
