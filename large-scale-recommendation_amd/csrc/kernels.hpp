@@ -27,11 +27,12 @@ struct FastBlk {
   int64_t cell_base;  // its G*G+1 cell offsets in the cell table
 };
 // Factor slabs are addressed through 32-bit buffer offsets (u_bytes/i_bytes < 4 GiB each).
-// dummy_i_off: byte offset of an item row that is never written (idle item prefetches).
+// dummy_u_off / dummy_i_off: byte offsets of rows that are never written (idle prefetches of
+// rows forwarded in registers).
 // Cells of at least prio_len records run at raised wave priority (s_setprio 3).
 void launch_fast_substep(hipStream_t st, const FastBlk* blks, int nblk, int G, int t, const FastRec* recs,
                          const int32_t* cell_off, float* U, float* I, int k, float eta, uint64_t u_bytes,
-                         uint64_t i_bytes, uint32_t dummy_i_off, int prio_len);
+                         uint64_t i_bytes, uint32_t dummy_u_off, uint32_t dummy_i_off, int prio_len);
 
 // Fast-mode sweep, one persistent launch per superstep: wave g of a block sweeps its G cells in
 // order and waits on wave g+1's progress word before each cell (progress: nblk*G*kProgStride
@@ -39,7 +40,8 @@ void launch_fast_substep(hipStream_t st, const FastBlk* blks, int nblk, int G, i
 constexpr int kProgStride = 32;  // one 128-B line per progress word
 void launch_fast_superstep(hipStream_t st, const FastBlk* blks, int nblk, int G, const FastRec* recs,
                            const int32_t* cell_off, float* U, float* I, int k, float eta, uint64_t u_bytes,
-                           uint64_t i_bytes, uint32_t dummy_i_off, int32_t* progress, int32_t* err);
+                           uint64_t i_bytes, uint32_t dummy_u_off, uint32_t dummy_i_off, int32_t* progress,
+                           int32_t* err);
 
 // Gather-dot over resolved pairs (row -1 = unknown id).  out[j] = p.q summed left to right in
 // f64 (predictRating's ddot).  When r != nullptr every workgroup writes partials[3*wg + c]:

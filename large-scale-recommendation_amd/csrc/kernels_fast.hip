@@ -194,7 +194,7 @@ __device__ __forceinline__ float wave_sum(float v) {
 template <int KPL, bool FULL, int D, int UAUX>
 __device__ __forceinline__ void sweep_cell(int64_t beg, int len, const uint32_t* __restrict__ recw,
                                            __amdgpu_buffer_rsrc_t urs, __amdgpu_buffer_rsrc_t irs, int k,
-                                           float eta, int lane, uint32_t dummy_i_off) {
+                                           float eta, int lane, uint32_t dummy_u_off, uint32_t dummy_i_off) {
   static_assert(D <= kHazardWindow && D <= CH && CH % D == 0, "ring depth");
   uint32_t su[D], si[D];
   Row<KPL> rp[D], rq[D];
@@ -202,25 +202,31 @@ __device__ __forceinline__ void sweep_cell(int64_t beg, int len, const uint32_t*
   chunk_load(recw, beg, len, 0, lane, A);
   chunk_load(recw, beg, len, 1, lane, B);
   chunk_prep(A, eta);
-  uint32_t last_fetched = kNone;
+  uint32_t last_u = kNone, last_i = kNone;
 
+  // A row that continues the previous record's run is forwarded in registers; its ring slot
+  // reads a never-written dummy row instead (no load ever trails a store to a live row).
 #define MF_FETCH(slot, X, y)                                                                  \
   do {                                                                                      \
-    su[slot] = rl(X.u, (y));                                                                \
+    const uint32_t uo_ = rl(X.u, (y));                                                      \
     const uint32_t io_ = rl(X.i, (y));                                                      \
+    su[slot] = uo_;                                                                         \
     si[slot] = io_;                                                                         \
-    rp[slot] = load_row<KPL, FULL, UAUX>(urs, su[slot], lane, k);                           \
-    rq[slot] = load_row<KPL, FULL, 0>(irs, io_ != last_fetched ? io_ : dummy_i_off, lane, k); \
-    last_fetched = io_;                                                                     \
+    rp[slot] = load_row<KPL, FULL, UAUX>(urs, uo_ != last_u ? uo_ : dummy_u_off, lane, k);  \
+    rq[slot] = load_row<KPL, FULL, 0>(irs, io_ != last_i ? io_ : dummy_i_off, lane, k);     \
+    last_u = uo_;                                                                           \
+    last_i = io_;                                                                           \
   } while (0)
 
 #define MF_STEP(slot, X, y)                                                                 \
   do {                                                                                      \
     const uint32_t uo_ = su[slot], io_ = si[slot];                                          \
-    const bool nr_ = io_ != cur_i;                                                          \
+    const bool nr_ = io_ != cur_i, nu_ = uo_ != cur_u;                                      \
     cur_i = io_;                                                                            \
+    cur_u = uo_;                                                                            \
     Row<KPL> p_ = rp[slot];                                                                 \
     mask_row<KPL, FULL>(p_, lane, k);                                                       \
+    _Pragma("unroll") for (int e = 0; e < KPL; ++e) p_.v[e] = nu_ ? p_.v[e] : pl.v[e];      \
     Row<KPL> ql_ = rq[slot];                                                                \
     mask_row<KPL, FULL>(ql_, lane, k);                                                      \
     _Pragma("unroll") for (int e = 0; e < KPL; ++e) q.v[e] = nr_ ? ql_.v[e] : q.v[e];       \
@@ -235,15 +241,16 @@ __device__ __forceinline__ void sweep_cell(int64_t beg, int len, const uint32_t*
     }                                                                                       \
     store_row<KPL, FULL, UAUX>(urs, uo_, lane, k, pn_);                                     \
     store_row<KPL, FULL, 0>(irs, io_, lane, k, q);                                          \
+    pl = pn_;                                                                               \
   } while (0)
 
 #pragma unroll
   for (int s = 0; s < D; ++s) MF_FETCH(s, A, s);
 
-  Row<KPL> q;
+  Row<KPL> q, pl;  // the item row of the current run, the last updated user row
 #pragma unroll
-  for (int c = 0; c < KPL; ++c) q.v[c] = 0.f;
-  uint32_t cur_i = kNone;
+  for (int c = 0; c < KPL; ++c) q.v[c] = pl.v[c] = 0.f;
+  uint32_t cur_i = kNone, cur_u = kNone;
   for (int base = 0;; base += 2 * CH) {
     // A holds records [base, base+CH) (prepared), B holds [base+CH, base+2CH)
 #pragma unroll
@@ -278,7 +285,7 @@ template <int KPL, bool FULL, int D>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_fast_substep(
     const FastBlk* __restrict__ blks, int nblk, int G, int t, const uint32_t* __restrict__ recw,
     const int32_t* __restrict__ cell_off, float* __restrict__ U, float* __restrict__ I, int k, float eta,
-    uint64_t u_bytes, uint64_t i_bytes, uint32_t dummy_i_off, int prio_len) {
+    uint64_t u_bytes, uint64_t i_bytes, uint32_t dummy_u_off, uint32_t dummy_i_off, int prio_len) {
   const int lane = threadIdx.x;
   // blockIdx % nblk picks the rating block: with 8 blocks a block's waves share one XCD's L2.
   const int slot = static_cast<int>(blockIdx.x % static_cast<unsigned>(nblk));
@@ -293,7 +300,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
   // the longest cells set the sub-step's length: give their waves issue priority on the SIMD
   if (len >= prio_len) __builtin_amdgcn_s_setprio(3);
   sweep_cell<KPL, FULL, D, 0>(beg, len, recw, make_rsrc(U, u_bytes), make_rsrc(I, i_bytes), k, eta, lane,
-                              dummy_i_off);
+                              dummy_u_off, dummy_i_off);
 }
 
 // ---- one persistent launch per superstep (systolic rotation) --------------------------------
@@ -301,7 +308,7 @@ template <int KPL, bool FULL, int D>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_fast_superstep(
     const FastBlk* __restrict__ blks, int nblk, int G, const uint32_t* __restrict__ recw,
     const int32_t* __restrict__ cell_off, float* __restrict__ U, float* __restrict__ I, int k, float eta,
-    uint64_t u_bytes, uint64_t i_bytes, uint32_t dummy_i_off, int32_t* __restrict__ progress,
+    uint64_t u_bytes, uint64_t i_bytes, uint32_t dummy_u_off, uint32_t dummy_i_off, int32_t* __restrict__ progress,
     int32_t* __restrict__ err) {
   const int lane = threadIdx.x;
   const int slot = static_cast<int>(blockIdx.x % static_cast<unsigned>(nblk));
@@ -320,7 +327,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
     const int len = off[cb + 1] - off[cb];
     // user group (g+t) mod G was last swept by wave g+1 in sub-step t-1
     if (t > 0 && G > 1 && !wait_flag(next_prog, t, err)) return;
-    if (len > 0) sweep_cell<KPL, FULL, D, 16>(beg, len, recw, urs, irs, k, eta, lane, dummy_i_off);
+    if (len > 0) sweep_cell<KPL, FULL, D, 16>(beg, len, recw, urs, irs, k, eta, lane, dummy_u_off, dummy_i_off);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every user-row store of this wave has landed
     if (lane == 0) __hip_atomic_store(prog + static_cast<int64_t>(g) * kProgStride, t + 1, __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_AGENT);
@@ -330,35 +337,35 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
 template <int KPL, int D>
 void fast_dispatch(hipStream_t st, dim3 grid, const FastBlk* blks, int nblk, int G, int t,
                    const FastRec* recs, const int32_t* off, float* U, float* I, int k, float eta, uint64_t ub,
-                   uint64_t ib, uint32_t di, int prio_len) {
+                   uint64_t ib, uint32_t du, uint32_t di, int prio_len) {
   const uint32_t* r = reinterpret_cast<const uint32_t*>(recs);
   if (k == 64 * KPL)
-    hipLaunchKernelGGL((k_fast_substep<KPL, true, D>), grid, dim3(64), 0, st, blks, nblk, G, t, r, off, U, I, k, eta, ub, ib, di, prio_len);
+    hipLaunchKernelGGL((k_fast_substep<KPL, true, D>), grid, dim3(64), 0, st, blks, nblk, G, t, r, off, U, I, k, eta, ub, ib, du, di, prio_len);
   else
-    hipLaunchKernelGGL((k_fast_substep<KPL, false, D>), grid, dim3(64), 0, st, blks, nblk, G, t, r, off, U, I, k, eta, ub, ib, di, prio_len);
+    hipLaunchKernelGGL((k_fast_substep<KPL, false, D>), grid, dim3(64), 0, st, blks, nblk, G, t, r, off, U, I, k, eta, ub, ib, du, di, prio_len);
 }
 
 template <int KPL, int D>
 void persistent_dispatch(hipStream_t st, const FastBlk* blks, int nblk, int G, const FastRec* recs,
                          const int32_t* off, float* U, float* I, int k, float eta, uint64_t ub, uint64_t ib,
-                         uint32_t di, int32_t* progress, int32_t* err) {
+                         uint32_t du, uint32_t di, int32_t* progress, int32_t* err) {
   const uint32_t* r = reinterpret_cast<const uint32_t*>(recs);
   const dim3 grid(static_cast<unsigned>(nblk * G)), block(64);
   if (k == 64 * KPL)
     hipLaunchKernelGGL((k_fast_superstep<KPL, true, D>), grid, block, 0, st, blks, nblk, G, r, off, U, I, k, eta, ub,
-                       ib, di, progress, err);
+                       ib, du, di, progress, err);
   else
     hipLaunchKernelGGL((k_fast_superstep<KPL, false, D>), grid, block, 0, st, blks, nblk, G, r, off, U, I, k, eta, ub,
-                       ib, di, progress, err);
+                       ib, du, di, progress, err);
 }
 
 }  // namespace
 
 void launch_fast_substep(hipStream_t st, const FastBlk* blks, int nblk, int G, int t, const FastRec* recs,
                          const int32_t* cell_off, float* U, float* I, int k, float eta, uint64_t u_bytes,
-                         uint64_t i_bytes, uint32_t dummy_i_off, int prio_len) {
+                         uint64_t i_bytes, uint32_t dummy_u_off, uint32_t dummy_i_off, int prio_len) {
   const dim3 grid(static_cast<unsigned>(nblk * G));
-#define MF_ARGS st, grid, blks, nblk, G, t, recs, cell_off, U, I, k, eta, u_bytes, i_bytes, dummy_i_off, prio_len
+#define MF_ARGS st, grid, blks, nblk, G, t, recs, cell_off, U, I, k, eta, u_bytes, i_bytes, dummy_u_off, dummy_i_off, prio_len
   if (k <= 64) fast_dispatch<1, 8>(MF_ARGS);
   else if (k <= 128) fast_dispatch<2, 8>(MF_ARGS);
   else if (k <= 256) fast_dispatch<4, 8>(MF_ARGS);
@@ -368,8 +375,9 @@ void launch_fast_substep(hipStream_t st, const FastBlk* blks, int nblk, int G, i
 
 void launch_fast_superstep(hipStream_t st, const FastBlk* blks, int nblk, int G, const FastRec* recs,
                            const int32_t* cell_off, float* U, float* I, int k, float eta, uint64_t u_bytes,
-                           uint64_t i_bytes, uint32_t dummy_i_off, int32_t* progress, int32_t* err) {
-#define MF_ARGS st, blks, nblk, G, recs, cell_off, U, I, k, eta, u_bytes, i_bytes, dummy_i_off, progress, err
+                           uint64_t i_bytes, uint32_t dummy_u_off, uint32_t dummy_i_off, int32_t* progress,
+                           int32_t* err) {
+#define MF_ARGS st, blks, nblk, G, recs, cell_off, U, I, k, eta, u_bytes, i_bytes, dummy_u_off, dummy_i_off, progress, err
   if (k <= 64) persistent_dispatch<1, 8>(MF_ARGS);
   else if (k <= 128) persistent_dispatch<2, 8>(MF_ARGS);
   else if (k <= 256) persistent_dispatch<4, 8>(MF_ARGS);

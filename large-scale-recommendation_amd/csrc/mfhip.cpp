@@ -431,8 +431,9 @@ void fast_superstep(mf_ctx* ctx, Shard& s, int64_t superstep, double eta) {
     LaunchTimer tm(s, ctx->profiling);
     launch_fast_superstep(s.stream, blks, ctx->c, ctx->G_fast, s.fast_recs.as<FastRec>(), s.fast_cells.as<int32_t>(),
                           s.uf.as<float>(), s.itf.as<float>(), ctx->P.num_factors, static_cast<float>(eta),
-                          s.uf.bytes(), s.itf.bytes(), ctx->fast_dummy_i * 4u * ctx->P.num_factors,
-                          s.fast_prog.as<int32_t>(), s.fast_err.as<int32_t>());
+                          s.uf.bytes(), s.itf.bytes(), (ctx->fast_dummy_u + 1) * 4u * ctx->P.num_factors,
+                          ctx->fast_dummy_i * 4u * ctx->P.num_factors, s.fast_prog.as<int32_t>(),
+                          s.fast_err.as<int32_t>());
     ctx->stats.kernel_launches += 1;
   } else {
     for (int32_t t = 0; t < ctx->G_fast; ++t) {
@@ -440,6 +441,7 @@ void fast_superstep(mf_ctx* ctx, Shard& s, int64_t superstep, double eta) {
       launch_fast_substep(s.stream, blks, ctx->c, ctx->G_fast, t, s.fast_recs.as<FastRec>(),
                           s.fast_cells.as<int32_t>(), s.uf.as<float>(), s.itf.as<float>(), ctx->P.num_factors,
                           static_cast<float>(eta), s.uf.bytes(), s.itf.bytes(),
+                          (ctx->fast_dummy_u + 1) * 4u * ctx->P.num_factors,
                           ctx->fast_dummy_i * 4u * ctx->P.num_factors, ctx->fast_prio_len);
     }
     ctx->stats.kernel_launches += ctx->G_fast;

@@ -247,13 +247,13 @@ void build_level_plan(const std::vector<OrderedSeq>& seqs, LevelPlan& out) {
 
 // G trades launch/cell overhead and the record padding forced by heavy users (large G) against
 // cell imbalance (small G).  The per-superstep critical path is the sum over sub-steps of the
-// longest cell; on the NFLX-shaped synthetic it is minimal near ~90 ratings per average cell
-// (G = 128 for 1.4M-rating blocks), which this rule targets.
+// longest cell; on the NFLX-shaped synthetic it is minimal near ~150 ratings per average cell
+// (G = 96 for 1.4M-rating blocks), which this rule targets.
 int32_t choose_groups(int64_t avg_block_ratings, int32_t blocks_per_device, int32_t fast_waves) {
   if (fast_waves < 0) return std::clamp(-fast_waves, 1, 4096);
   const int32_t waves = fast_waves > 0 ? fast_waves : 2048;
   int64_t g = waves / std::max(blocks_per_device, 1);
-  const int64_t cap = static_cast<int64_t>(std::sqrt(std::max<double>(avg_block_ratings, 1.0) / 90.0));
+  const int64_t cap = static_cast<int64_t>(std::sqrt(std::max<double>(avg_block_ratings, 1.0) / 150.0));
   g = std::min(g, cap);
   g = (g / 4) * 4;
   return static_cast<int32_t>(std::clamp<int64_t>(g, 4, 1024));
@@ -336,73 +336,123 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
       key[x] = {(cell << 40) | (static_cast<uint64_t>(il) << 16) | tie, x};
     }
     std::sort(key.begin(), key.end());
-    // Emit each cell run by run.  A user must not recur within kHazardWindow positions.  At a
-    // run boundary choose, among the cell's remaining item runs (longest first), one whose
-    // pending ratings offer a non-conflicting user; inside a run pick the first
-    // non-conflicting pending rating.  Only when nothing qualifies emit a no-op record.
-    // last[ul] = (cell, position) of the user's latest emission.
+    // Emit each cell as a sequence the kernel can run with a D-deep prefetch ring: every user
+    // and every item row recurs either at the next position (the kernel forwards it in
+    // registers: item runs and user runs) or at least kHazardWindow positions later (its
+    // store has been issued before the prefetch).  Greedy per position: continue the current
+    // item run, or the current user run when that user has more pending ratings than the
+    // item; otherwise start from the item with the most pending ratings whose row and some
+    // pending user row are both free; only when nothing qualifies emit a no-op record (zero
+    // user row, current item).  last_*[x] = (cell, position) of the row's latest emission.
     std::vector<FastRec>& out = outs[bx];
     std::vector<int64_t>& src = srcs[bx];
     std::vector<int32_t>& off = offs[bx];
-    out.reserve(len + len / 16 + 16);
-    if (rec_src) src.reserve(len + len / 16 + 16);
+    out.reserve(len + len / 8 + 16);
+    if (rec_src) src.reserve(len + len / 8 + 16);
     off.assign(GG + 1, 0);
-    std::vector<std::pair<int64_t, int64_t>> last(nu, {-1, 0});
-    struct Run { uint32_t irow; std::vector<int64_t> pend; size_t head = 0; };
-    std::vector<Run> runs;
-    std::vector<int32_t> alive;
+    std::vector<std::pair<int64_t, int64_t>> last_u(nu, {-1, 0}), last_i(ni, {-1, 0});
+    std::vector<std::pair<int64_t, int32_t>> uslot(nu, {-1, 0});
+    struct Ent { uint32_t ul, il; int32_t ug, ig; int64_t j; };
+    struct Grp { std::vector<int32_t> e; size_t head = 0; int32_t left = 0; uint32_t row = 0; };
+    std::vector<Ent> ents;
+    std::vector<Grp> igs, ugs;
+    std::vector<uint8_t> taken;
+    std::vector<int32_t> iorder;
     int64_t x = 0;
     for (int64_t c = 0; c < GG; ++c) {
       const int64_t cell_begin = static_cast<int64_t>(out.size());
-      runs.clear();
+      ents.clear();
+      igs.clear();
+      ugs.clear();
       while (x < len && static_cast<int64_t>(key[x].first >> 40) == c) {
-        const uint64_t il = (key[x].first >> 16) & 0xFFFFFFu;
-        Run rn;
-        rn.irow = static_cast<uint32_t>(ib + il);
-        while (x < len && (key[x].first >> 16) == ((static_cast<uint64_t>(c) << 24) | il)) rn.pend.push_back(key[x++].second);
-        runs.push_back(std::move(rn));
+        const int64_t j = s + key[x].second;
+        const uint32_t il = rb.irow[j] - static_cast<uint32_t>(ib), ul = rb.urow[j] - static_cast<uint32_t>(ub);
+        if (igs.empty() || ents.back().il != il) { igs.emplace_back(); igs.back().row = il; }
+        auto& us = uslot[ul];
+        if (us.first != c) { us = {c, static_cast<int32_t>(ugs.size())}; ugs.emplace_back(); }
+        const int32_t e = static_cast<int32_t>(ents.size());
+        ents.push_back(Ent{ul, il, us.second, static_cast<int32_t>(igs.size()) - 1, j});
+        igs.back().e.push_back(e);
+        ugs[us.second].e.push_back(e);
+        ++x;
       }
-      alive.resize(runs.size());
-      std::iota(alive.begin(), alive.end(), 0);
-      std::stable_sort(alive.begin(), alive.end(), [&](int32_t a2, int32_t b2) {
-        return runs[a2].pend.size() > runs[b2].pend.size();
+      const int32_t m = static_cast<int32_t>(ents.size());
+      taken.assign(m, 0);
+      for (auto& g2 : igs) g2.left = static_cast<int32_t>(g2.e.size());
+      for (auto& g2 : ugs) g2.left = static_cast<int32_t>(g2.e.size());
+      iorder.resize(igs.size());
+      std::iota(iorder.begin(), iorder.end(), 0);
+      std::stable_sort(iorder.begin(), iorder.end(), [&](int32_t a2, int32_t b2) {
+        return igs[a2].e.size() > igs[b2].e.size();
       });
-      auto candidate = [&](Run& rn, int64_t pos) -> size_t {  // index of a non-conflicting rating or npos
-        for (size_t y = rn.head; y < rn.pend.size() && y < rn.head + 4 * kHazardWindow; ++y) {
-          const auto& l = last[rb.urow[s + rn.pend[y]] - ub];
-          if (l.first != c || pos - l.second >= kHazardWindow) return y;
+      size_t iorder_head = 0;
+      int32_t prev_ug = -1, prev_ig = -1;
+      uint32_t prev_irow = 0;
+      int32_t left = m;
+      while (left > 0) {
+        const int64_t pos = static_cast<int64_t>(out.size()) - cell_begin;
+        auto ufree = [&](uint32_t ul) { return last_u[ul].first != c || pos - last_u[ul].second >= kHazardWindow; };
+        auto ifree = [&](uint32_t il) { return last_i[il].first != c || pos - last_i[il].second >= kHazardWindow; };
+        auto scan = [&](Grp& g2, auto ok) -> int32_t {
+          while (g2.head < g2.e.size() && taken[g2.e[g2.head]]) ++g2.head;
+          int seen = 0;
+          for (size_t y = g2.head; y < g2.e.size() && seen < 4 * kHazardWindow; ++y) {
+            const int32_t e = g2.e[y];
+            if (taken[e]) continue;
+            ++seen;
+            if (ok(ents[e])) return e;
+          }
+          return -1;
+        };
+        auto try_item = [&]() -> int32_t {  // continue the item run
+          if (prev_ig < 0 || igs[prev_ig].left == 0) return -1;
+          return scan(igs[prev_ig], [&](const Ent& en) { return en.ug == prev_ug || ufree(en.ul); });
+        };
+        auto try_user = [&]() -> int32_t {  // continue the user run
+          if (prev_ug < 0 || ugs[prev_ug].left == 0) return -1;
+          return scan(ugs[prev_ug], [&](const Ent& en) { return en.ig == prev_ig || ifree(en.il); });
+        };
+        const bool user_first = prev_ug >= 0 && prev_ig >= 0 && ugs[prev_ug].left > igs[prev_ig].left;
+        int32_t pick = user_first ? try_user() : try_item();
+        if (pick < 0) pick = user_first ? try_item() : try_user();
+        if (pick < 0) {  // fresh start: both rows free
+          while (iorder_head < iorder.size() && igs[iorder[iorder_head]].left == 0) ++iorder_head;
+          int tried = 0;
+          for (size_t z = iorder_head; z < iorder.size() && tried < 64; ++z) {
+            Grp& g2 = igs[iorder[z]];
+            if (g2.left == 0) continue;
+            ++tried;
+            if (!ifree(g2.row)) continue;
+            pick = scan(g2, [&](const Ent& en) { return ufree(en.ul); });
+            if (pick >= 0) break;
+          }
         }
-        return static_cast<size_t>(-1);
-      };
-      auto emit_pad = [&](uint32_t irow) {
-        out.push_back(FastRec{dummy_row * row_bytes, irow * row_bytes, 0.f, 0.f, 0.f, dummy_row, irow | kPadBit, 0});
-        if (rec_src) src.push_back(-1);
-        pads[bx]++;
-      };
-      uint32_t cur_irow = runs.empty() ? 0u : runs[alive[0]].irow;
-      while (!alive.empty()) {
-        int64_t pos = static_cast<int64_t>(out.size()) - cell_begin;
-        size_t ai = alive.size();
-        for (size_t z = 0; z < alive.size(); ++z)
-          if (candidate(runs[alive[z]], pos) != static_cast<size_t>(-1)) { ai = z; break; }
-        if (ai == alive.size()) { emit_pad(cur_irow); continue; }
-        Run& rn = runs[alive[ai]];
-        alive.erase(alive.begin() + ai);
-        cur_irow = rn.irow;
-        while (rn.head < rn.pend.size()) {
-          pos = static_cast<int64_t>(out.size()) - cell_begin;
-          const size_t pick = candidate(rn, pos);
-          if (pick == static_cast<size_t>(-1)) { emit_pad(cur_irow); continue; }
-          std::swap(rn.pend[rn.head], rn.pend[pick]);
-          const int64_t j = s + rn.pend[rn.head++];
-          const uint32_t urow = rb.urow[j];
-          last[urow - ub] = {c, pos};
-          out.push_back(FastRec{urow * row_bytes, rb.irow[j] * row_bytes, static_cast<float>(rb.r[j]),
-                                static_cast<float>(lambda / static_cast<double>(U.omega[urow])),
-                                static_cast<float>(lambda / static_cast<double>(I.omega[rb.irow[j]])), urow,
-                                rb.irow[j], 0});
-          if (rec_src) src.push_back(j);
+        if (pick < 0) {  // no-op record: zero user row, the current item (forwarded)
+          out.push_back(FastRec{dummy_row * row_bytes, prev_irow * row_bytes, 0.f, 0.f, 0.f, dummy_row,
+                                prev_irow | kPadBit, 0});
+          if (rec_src) src.push_back(-1);
+          pads[bx]++;
+          if (prev_ig >= 0) last_i[igs[prev_ig].row] = {c, pos};
+          prev_ug = -1;
+          continue;
         }
+        const Ent& en = ents[pick];
+        taken[pick] = 1;
+        --left;
+        igs[en.ig].left--;
+        ugs[en.ug].left--;
+        last_u[en.ul] = {c, pos};
+        last_i[en.il] = {c, pos};
+        prev_ug = en.ug;
+        prev_ig = en.ig;
+        const int64_t j = en.j;
+        const uint32_t urow = rb.urow[j];
+        prev_irow = rb.irow[j];
+        out.push_back(FastRec{urow * row_bytes, prev_irow * row_bytes, static_cast<float>(rb.r[j]),
+                              static_cast<float>(lambda / static_cast<double>(U.omega[urow])),
+                              static_cast<float>(lambda / static_cast<double>(I.omega[prev_irow])), urow, prev_irow,
+                              0});
+        if (rec_src) src.push_back(j);
       }
       off[c + 1] = static_cast<int32_t>(out.size());
     }

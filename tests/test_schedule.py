@@ -77,17 +77,22 @@ def test_fast_rotation_is_conflict_free(nb, G):
                 owner = {}
                 for x, c in zip(ids.tolist(), cell.tolist()):
                     assert owner.setdefault(x, c) == c
-    # every item group owns its items for the whole block; every cell is item-contiguous
+    # inside a cell every user and item row recurs either at the next position (forwarded in
+    # registers: user / item runs) or at least kHazardWindow = 8 positions later (the kernel's
+    # prefetch distance); item runs keep the item row in registers.  Padding records (the gaps)
+    # carry the zero user row and the preceding record's item, so they extend an item run.
     key = b.astype(np.int64) * G * G + t.astype(np.int64) * G + g
-    for c in np.unique(key)[:200]:
+    runs = 0
+    for c in np.unique(key)[:300]:
         m = np.where(key == c)[0]
-        items_in_order = d.i[m[np.argsort(p[m])]]
-        runs = [items_in_order[0]] + [x for a, x in zip(items_in_order, items_in_order[1:]) if x != a]
-        assert len(runs) == len(set(runs))
         pos = p[m]
         assert len(set(pos.tolist())) == len(m)  # distinct slots (gaps = no-op padding records)
-        # a user never reappears within the kernel's prefetch window (kHazardWindow = 8)
-        last = {}
-        for x, y in sorted(zip(pos.tolist(), d.u[m].tolist())):
-            assert y not in last or x - last[y] >= 8
-            last[y] = x
+        for side, ids in (("u", d.u[m]), ("i", d.i[m])):
+            last, prev = {}, -1
+            for x, y in sorted(zip(pos.tolist(), ids.tolist())):
+                run = side == "i" and last.get(y) == prev  # only padding since this item's last record
+                assert y not in last or x - last[y] == 1 or x - last[y] >= 8 or run, (side, y, last.get(y), x)
+                last[y] = prev = x
+        items_in_order = d.i[m[np.argsort(pos)]]
+        runs += int(np.sum(items_in_order[1:] == items_in_order[:-1]))
+    assert runs > 0

@@ -1,0 +1,40 @@
+#!/usr/bin/env python3
+"""Critical-path statistics of the fast-mode plan on a synthetic config (host only, no GPU).
+
+    python tools/plan_stats.py [config] [G ...]
+
+critical steps per epoch = sum over supersteps and sub-steps of the longest cell (records incl.
+padding) among the stratum's blocks; compare with the measured epoch time.
+"""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "large-scale-recommendation_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "oracle"))
+import numpy as np
+
+from mfhip import synth
+from test_schedule import fast_schedule
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "NFLX"
+Gs = [int(x) for x in sys.argv[2:]] or [96]
+nu, ni, nr, k, nb = synth.CONFIGS[cfg]
+d = synth.config(cfg)
+(tu, ti, tr), _ = d.split()
+for G in Gs:
+    t0 = time.time()
+    b, t, g, p = fast_schedule(tu, ti, nb, 0, G)
+    cell = (b.astype(np.int64) * G + t) * G + g
+    length = np.zeros(nb * nb * G * G, np.int64)
+    np.maximum.at(length, cell, p + 1)
+    L = length.reshape(nb, nb, G, G)  # [ub, ib, t, g]
+    crit = 0
+    for s in range(nb):
+        sub = np.stack([L[ub, (ub + s) % nb] for ub in range(nb)])  # [ub, t, g]
+        crit += int(sub.max(axis=(0, 2)).sum())
+    total = int(length.sum())
+    print(f"{cfg} G={G}: ratings={len(tu)} records={total} pads={total - len(tu)} critical_steps/epoch={crit} "
+          f"mean_cell={total / max(1, (length > 0).sum()):.1f} max_cell={length.max()} ({time.time() - t0:.1f}s)",
+          flush=True)
