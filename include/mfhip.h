@@ -59,6 +59,10 @@ extern "C" {
 #define MF_ONLINE_DELTA 1        /* SGDUpdater.delta + "vec + delta" (PS path)          */
 #define MF_ONLINE_SPARK_SWEEP 2  /* OfflineSpark.offlineDSGDUpdatesOnly order           */
 
+/* Fast-mode factor blocking (DSGDforMF.scala:531-533 is the reference's). */
+#define MF_BLOCKING_REFERENCE 0  /* new Random(id ^ seed).nextInt(numBlocks) (default)   */
+#define MF_BLOCKING_BALANCED 1   /* rating-count balanced blocks (faster; different RMSE) */
+
 /* Initialisers for ids first seen online (core/FactorInitializer.scala). */
 #define MF_INIT_PSEUDO_RANDOM 0  /* new Random(id), k x nextDouble   (:23-27)           */
 #define MF_INIT_SEEDED 1         /* new Random(id ^ seed), as DSGD init (DSGDforMF.scala:548) */
@@ -84,7 +88,10 @@ typedef struct mf_params {
   /* fast-mode tuning: waves per device for the rotation schedule (0 = auto);
      a negative value -G fixes G rotation groups per rating block */
   int32_t fast_waves;
-  int32_t reserved[7];
+  /* fast-mode blocking: MF_BLOCKING_REFERENCE (default) or MF_BLOCKING_BALANCED;
+     the deterministic mode always uses the reference's blocking */
+  int32_t fast_blocking;
+  int32_t reserved[6];
 } mf_params;
 
 /* Aggregated device statistics (timed with HIP events on the library's stream). */
@@ -188,12 +195,12 @@ int mf_learning_rate(int method, double lr, int32_t iteration, double lambda, do
    (order may be NULL = identity); rows are caller indices.
    mf_debug_fast_schedule: for every input rating, the rating block (ub*n+ib), rotation
    sub-step, item group and position inside its cell of the fast-mode plan with `groups`
-   groups per rating block. */
+   groups per rating block and MF_BLOCKING_* `blocking`. */
 int mf_debug_levels(const uint32_t* urow, const uint32_t* irow, const int32_t* order, int64_t n,
                     int32_t* level_out);
 int mf_debug_fast_schedule(const int32_t* users, const int32_t* items, int64_t n, int32_t n_blocks,
-                           int64_t seed, int32_t groups, int32_t* block_out, int32_t* substep_out,
-                           int32_t* group_out, int64_t* pos_out);
+                           int64_t seed, int32_t groups, int32_t blocking, int32_t* block_out,
+                           int32_t* substep_out, int32_t* group_out, int64_t* pos_out);
 
 #ifdef __cplusplus
 }

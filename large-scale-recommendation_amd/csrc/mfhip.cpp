@@ -135,6 +135,8 @@ void validate_params(const mf_params* p) {
   MF_REQUIRE(p->num_blocks >= 1, "num_blocks must be >= 1");
   MF_REQUIRE(p->mode == MF_MODE_DETERMINISTIC_F64 || p->mode == MF_MODE_FAST_F32, "unknown mode");
   MF_REQUIRE(p->lr_method >= MF_LR_DEFAULT && p->lr_method <= MF_LR_XU, "unknown lr_method");
+  MF_REQUIRE(p->fast_blocking == MF_BLOCKING_BALANCED || p->fast_blocking == MF_BLOCKING_REFERENCE,
+             "unknown fast_blocking");
 }
 
 void init_shard(Shard& s, int device, int index) {
@@ -305,8 +307,9 @@ void sync_all(mf_ctx* ctx) {
 // Model construction for a fit.
 void build_model(mf_ctx* ctx, const int32_t* u, const int32_t* i, int64_t n) {
   const bool seeded = ctx->P.has_seed != 0;
-  build_side(ctx->U, u, n, ctx->nb, ctx->P.seed, seeded);
-  build_side(ctx->I, i, n, ctx->nb, ctx->P.seed, seeded);
+  const Blocking bl = !ctx->f64 && ctx->P.fast_blocking == MF_BLOCKING_BALANCED ? Blocking::kBalanced : Blocking::kJvm;
+  build_side(ctx->U, u, n, ctx->nb, ctx->P.seed, seeded, bl);
+  build_side(ctx->I, i, n, ctx->nb, ctx->P.seed, seeded, bl);
   const int k = ctx->P.num_factors;
   for (int side = 0; side < 2; ++side) {
     SideLayout& S = side == kSideU ? ctx->U : ctx->I;
@@ -1286,14 +1289,15 @@ int mf_debug_levels(const uint32_t* urow, const uint32_t* irow, const int32_t* o
 }
 
 int mf_debug_fast_schedule(const int32_t* u, const int32_t* i, int64_t n, int32_t n_blocks, int64_t seed,
-                           int32_t groups, int32_t* block_out, int32_t* substep_out, int32_t* group_out,
-                           int64_t* pos_out) {
+                           int32_t groups, int32_t blocking, int32_t* block_out, int32_t* substep_out,
+                           int32_t* group_out, int64_t* pos_out) {
   return guarded([&] {
     MF_REQUIRE(n >= 0 && n_blocks >= 1 && groups >= 1, "bad argument");
     MF_REQUIRE(n == 0 || (u && i && block_out && substep_out && group_out && pos_out), "null argument");
     SideLayout U, I;
-    build_side(U, u, n, n_blocks, seed, true);
-    build_side(I, i, n, n_blocks, seed, true);
+    const Blocking bl = blocking == MF_BLOCKING_BALANCED ? Blocking::kBalanced : Blocking::kJvm;
+    build_side(U, u, n, n_blocks, seed, true, bl);
+    build_side(I, i, n, n_blocks, seed, true, bl);
     std::vector<double> r(n, 1.0);
     RatingBlocks rb;
     build_rating_blocks(rb, U, I, u, i, r.data(), n, 0, n_blocks, false, true);

@@ -47,7 +47,8 @@ bool dense_ok(int32_t mn, int32_t mx, int64_t n) {
 
 // initFactorBlockAndIndices (DSGDforMF.scala:513-588): distinct ids (:520), block per id
 // (:531-533), omega = rating count (:537-541), ids sorted within a block when seeded (:556).
-void build_side(SideLayout& s, const int32_t* ids, int64_t n, int32_t nb, int64_t seed, bool has_seed) {
+void build_side(SideLayout& s, const int32_t* ids, int64_t n, int32_t nb, int64_t seed, bool has_seed,
+                Blocking blocking) {
   s = SideLayout();
   s.n_blocks = nb;
   std::vector<int32_t> distinct, counts;
@@ -74,7 +75,28 @@ void build_side(SideLayout& s, const int32_t* ids, int64_t n, int32_t nb, int64_
   }
   const int64_t d = static_cast<int64_t>(distinct.size());
   std::vector<int32_t> blk(d);
-  if (has_seed) {
+  if (blocking == Blocking::kBalanced) {
+    std::vector<int64_t> order(d);
+    std::vector<uint64_t> tie(d);
+    for (int64_t x = 0; x < d; ++x) {
+      order[x] = x;
+      uint64_t h = static_cast<uint64_t>(static_cast<int64_t>(distinct[x]) ^ seed) * 0x9E3779B97F4A7C15ULL;
+      tie[x] = h ^ (h >> 29);
+    }
+    std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
+      return counts[a] != counts[b] ? counts[a] > counts[b] : tie[a] < tie[b];
+    });
+    using E = std::pair<int64_t, int32_t>;  // (load, block)
+    std::priority_queue<E, std::vector<E>, std::greater<E>> pq;
+    for (int32_t b = 0; b < nb; ++b) pq.emplace(0, b);
+    for (int64_t x : order) {
+      E e = pq.top();
+      pq.pop();
+      blk[x] = e.second;
+      e.first += counts[x];
+      pq.push(e);
+    }
+  } else if (has_seed) {
     parallel_for(d, [&](int64_t b, int64_t e, int) {
       for (int64_t x = b; x < e; ++x) {
         JavaRandom rng(static_cast<int64_t>(distinct[x]) ^ seed);

@@ -26,11 +26,22 @@ struct SideLayout {
   int64_t rows() const { return static_cast<int64_t>(row_id.size()); }
 };
 
+// How ids are assigned to factor blocks.
+//  kJvm:      the reference's new Random(id ^ seed).nextInt(n) (DSGDforMF.scala:531-533).  Its
+//             first draw varies slowly with the id, so runs of ~1.4k consecutive ids share a
+//             block and rating blocks come out unequal (NFLX, n=8: largest 1.8x the mean).
+//  kBalanced: fast-mode option: heaviest ids first into the least-loaded block (LPT over
+//             rating counts, ties by a hash of id ^ seed), so all n*n rating blocks are near
+//             equal and a superstep is not held up by one oversized block.  It changes which
+//             ratings share a stratum, and with it the trajectory: on the NFLX-shaped synthetic
+//             the held-out RMSE after 10 epochs is 0.690 against the reference blocking's 0.759.
+enum class Blocking { kJvm, kBalanced };
+
 // Builds the factor-block layout of one side from the rating column `ids`.
 // has_seed: block = new Random(id ^ seed).nextInt(n) and ids sorted in a block;
 // otherwise blocks come from an unseeded generator (the reference's scala.util.Random).
 void build_side(SideLayout& s, const int32_t* ids, int64_t n, int32_t n_blocks, int64_t seed,
-                bool has_seed);
+                bool has_seed, Blocking blocking = Blocking::kJvm);
 
 // Per-rating global rows (parallel lookup).
 void lookup_rows(const SideLayout& s, const int32_t* ids, int64_t n, std::vector<uint32_t>& rows);

@@ -26,6 +26,8 @@ MF_ERR_STATE = -7
 
 MODE_DETERMINISTIC_F64 = 0
 MODE_FAST_F32 = 1
+BLOCKING_REFERENCE = 0
+BLOCKING_BALANCED = 1
 SIDE_USER = 0
 SIDE_ITEM = 1
 ONLINE_NEXT_FACTORS = 0
@@ -63,7 +65,8 @@ class mf_params(C.Structure):
         ("online_learning_rate", C.c_double),
         ("online_init", C.c_int32),
         ("fast_waves", C.c_int32),
-        ("reserved", C.c_int32 * 7),
+        ("fast_blocking", C.c_int32),
+        ("reserved", C.c_int32 * 6),
     ]
 
 
@@ -146,8 +149,8 @@ def lib() -> C.CDLL:
         "mf_jvm_random_factors": (C.c_int, [C.c_int64, C.c_int32, _f64p]),
         "mf_learning_rate": (C.c_int, [C.c_int, C.c_double, C.c_int32, C.c_double, C.c_double, _f64p]),
         "mf_debug_levels": (C.c_int, [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), _i32p, C.c_int64, _i32p]),
-        "mf_debug_fast_schedule": (C.c_int, [_i32p, _i32p, C.c_int64, C.c_int32, C.c_int64, C.c_int32, _i32p, _i32p,
-                                             _i32p, _i64p]),
+        "mf_debug_fast_schedule": (C.c_int, [_i32p, _i32p, C.c_int64, C.c_int32, C.c_int64, C.c_int32, C.c_int32,
+                                             _i32p, _i32p, _i32p, _i64p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

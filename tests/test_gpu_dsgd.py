@@ -12,10 +12,12 @@ from mfhip import synth
 pytestmark = pytest.mark.gpu
 
 
-def params(k, iterations, nb, seed, mode=L.MODE_DETERMINISTIC_F64, lam=1.0, lr=0.001, fast_waves=0, has_seed=1):
+def params(k, iterations, nb, seed, mode=L.MODE_DETERMINISTIC_F64, lam=1.0, lr=0.001, fast_waves=0, has_seed=1,
+           blocking=L.BLOCKING_REFERENCE):
     p = L.default_params()
     p.num_factors, p.iterations, p.num_blocks, p.seed, p.mode = k, iterations, nb, seed, mode
     p.lambda_, p.learning_rate, p.fast_waves, p.has_seed = lam, lr, fast_waves, has_seed
+    p.fast_blocking = blocking
     return p
 
 
@@ -173,7 +175,8 @@ def test_fast_kernel_equals_its_schedule(k, nb, G):
     d = synth.generate(400, 120, 12000, seed=k)
     seed, lam, lr, iters = 3, 1.0, 0.002, 2
     uids, U, iids, I = fast_replay_reference(d, k, nb, seed, G, iters, lam, lr)
-    with mfhip.Context(params(k, iters, nb, seed, mode=L.MODE_FAST_F32, lam=lam, lr=lr, fast_waves=-G)) as ctx:
+    with mfhip.Context(params(k, iters, nb, seed, mode=L.MODE_FAST_F32, lam=lam, lr=lr, fast_waves=-G,
+                              blocking=L.BLOCKING_REFERENCE)) as ctx:
         ctx.fit(d.u, d.i, d.r)
         a_ids, a_u = ctx.factors(0)
         b_ids, a_i = ctx.factors(1)

@@ -49,11 +49,11 @@ def test_level_count_is_longest_row_chain_lower_bound():
     assert levels(np.arange(50), np.arange(50)).max() == 1
 
 
-def fast_schedule(u, i, nb, seed, G):
+def fast_schedule(u, i, nb, seed, G, blocking=L.BLOCKING_REFERENCE):
     n = len(u)
     b = np.empty(n, np.int32); t = np.empty(n, np.int32); g = np.empty(n, np.int32); p = np.empty(n, np.int64)
     L.check(L.lib().mf_debug_fast_schedule(L.ptr(L.as_i32(u), C.c_int32), L.ptr(L.as_i32(i), C.c_int32), n, nb,
-                                           seed, G, L.ptr(b, C.c_int32), L.ptr(t, C.c_int32), L.ptr(g, C.c_int32),
+                                           seed, G, blocking, L.ptr(b, C.c_int32), L.ptr(t, C.c_int32), L.ptr(g, C.c_int32),
                                            L.ptr(p, C.c_int64)))
     return b, t, g, p
 

@@ -20,20 +20,30 @@ from test_schedule import fast_schedule
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "NFLX"
 Gs = [int(x) for x in sys.argv[2:]] or [96]
+blocking = int(os.environ.get("BLOCKING", "0"))  # 0 reference (default), 1 balanced
 nu, ni, nr, k, nb = synth.CONFIGS[cfg]
 d = synth.config(cfg)
 (tu, ti, tr), _ = d.split()
 for G in Gs:
     t0 = time.time()
-    b, t, g, p = fast_schedule(tu, ti, nb, 0, G)
+    b, t, g, p = fast_schedule(tu, ti, nb, 0, G, blocking)
     cell = (b.astype(np.int64) * G + t) * G + g
     length = np.zeros(nb * nb * G * G, np.int64)
     np.maximum.at(length, cell, p + 1)
     L = length.reshape(nb, nb, G, G)  # [ub, ib, t, g]
-    crit = 0
+    # cells made of one item's ratings only (hot runs) and the rest
+    first_item = np.full(len(length), -1, np.int64)
+    np.maximum.at(first_item, cell, ti.astype(np.int64))
+    lo_item = np.full(len(length), np.iinfo(np.int64).max, np.int64)
+    np.minimum.at(lo_item, cell, ti.astype(np.int64))
+    single = ((first_item == lo_item) & (length > 32)).reshape(nb, nb, G, G)
+    crit = crit_rest = 0
     for s in range(nb):
         sub = np.stack([L[ub, (ub + s) % nb] for ub in range(nb)])  # [ub, t, g]
+        sng = np.stack([single[ub, (ub + s) % nb] for ub in range(nb)])
         crit += int(sub.max(axis=(0, 2)).sum())
+        crit_rest += int(np.where(sng, 0, sub).max(axis=(0, 2)).sum())
+    print(f"  single-item cells: {int(single.sum())}, critical steps without them: {crit_rest}")
     total = int(length.sum())
     print(f"{cfg} G={G}: ratings={len(tu)} records={total} pads={total - len(tu)} critical_steps/epoch={crit} "
           f"mean_cell={total / max(1, (length > 0).sum()):.1f} max_cell={length.max()} ({time.time() - t0:.1f}s)",
