@@ -195,12 +195,15 @@ int mf_learning_rate(int method, double lr, int32_t iteration, double lambda, do
    (order may be NULL = identity); rows are caller indices.
    mf_debug_fast_schedule: for every input rating, the rating block (ub*n+ib), rotation
    sub-step, item group and position inside its cell of the fast-mode plan with `groups`
-   groups per rating block and MF_BLOCKING_* `blocking`. */
+   groups per rating block, MF_BLOCKING_* `blocking` and hazard window `window` (0: 8). */
 int mf_debug_levels(const uint32_t* urow, const uint32_t* irow, const int32_t* order, int64_t n,
                     int32_t* level_out);
 int mf_debug_fast_schedule(const int32_t* users, const int32_t* items, int64_t n, int32_t n_blocks,
-                           int64_t seed, int32_t groups, int32_t blocking, int32_t* block_out,
+                           int64_t seed, int32_t groups, int32_t blocking, int32_t window, int32_t* block_out,
                            int32_t* substep_out, int32_t* group_out, int64_t* pos_out);
+/* The plan window (records between two uses of a row inside a cell unless adjacent) the fast
+   sweep uses at rank k: the prefetch distance of the kernel selected for k. */
+int mf_fast_plan_window(int32_t k, int32_t* window_out);
 
 #ifdef __cplusplus
 }

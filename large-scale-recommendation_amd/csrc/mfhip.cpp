@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -60,6 +61,10 @@ struct Shard {
   // fast mode
   DevBuf fast_recs, fast_cells, fast_blks;
   DevBuf fast_prog, fast_err;  // persistent sweep: progress words + timeout flag
+  DevBuf st_recs, st_waves;    // stream schedule (kernels_stream.hip)
+  std::vector<int64_t> st_sub_off;
+  std::vector<WaveDesc> st_waves_host;  // kept only when tracing
+  DevBuf st_trace;                      // MFHIP_WAVE_TRACE: {start, end} per wave
   // evaluation scratch
   DevBuf ev_u, ev_i, ev_r, ev_mult, ev_out, ev_part;
   // profiling
@@ -90,6 +95,7 @@ struct mf_ctx {
   uint32_t fast_dummy_u = 0, fast_dummy_i = 0;  // zeroed rows past the real ones (padding / idle prefetch)
   int32_t fast_prio_len = 1 << 30;  // cells at least this long run at raised priority
   bool fast_persistent = false;  // MFHIP_FAST_KERNEL=persistent selects the systolic single launch
+  bool fast_lean = false;         // one wave per cell, deep prefetch (kernels_lean.hip), k in {64, 128, 256}
   std::vector<int64_t> fast_rb_size;  // per rating block (fast mode)
   mf_stats stats{};
   bool profiling = false;
@@ -101,6 +107,19 @@ namespace mfhip {
 namespace {
 
 constexpr int kSideU = MF_SIDE_USER;
+
+enum class FastKernel { kLean, kCell, kPersistent };
+
+// Fast sweep kernel: MFHIP_FAST_KERNEL = cell (default, kernels_fast.hip) | persistent (same
+// file, one launch per superstep) | lean (kernels_lean.hip, k in {64, 128, 256}).
+FastKernel choose_fast_kernel(int k) {
+  const char* v = std::getenv("MFHIP_FAST_KERNEL");
+  const std::string want = v ? v : "";
+  if (want == "persistent") return FastKernel::kPersistent;
+  if (want == "lean" && lean_kernel_supports(k)) return FastKernel::kLean;
+  return FastKernel::kCell;
+}
+
 
 void set_error(const std::string& m) { g_last_error = m; }
 
@@ -286,6 +305,29 @@ void collect_profile(mf_ctx* ctx) {
   }
 }
 
+// MFHIP_WAVE_TRACE=<file>: per wave of the stream schedule "shard sm t wave steps cells start end"
+// (100 MHz clock) of the last time every sub-step ran.
+void dump_wave_trace(mf_ctx* ctx) {
+  const char* path = std::getenv("MFHIP_WAVE_TRACE");
+  if (!path) return;
+  FILE* f = nullptr;
+  for (auto& s : ctx->shards) {
+    if (!s.st_trace.get() || s.st_waves_host.empty()) continue;
+    DeviceGuard g(s.device);
+    std::vector<uint64_t> tr(s.st_waves_host.size() * 2);
+    MF_HIP(hipMemcpy(tr.data(), s.st_trace.get(), tr.size() * 8, hipMemcpyDeviceToHost));
+    if (!f) f = std::fopen(path, "w");
+    if (!f) return;
+    const int64_t G = ctx->G_fast;
+    for (size_t x = 0; x + 1 < s.st_sub_off.size(); ++x)
+      for (int64_t w = s.st_sub_off[x]; w < s.st_sub_off[x + 1]; ++w)
+        std::fprintf(f, "%d %lld %lld %lld %d %d %llu %llu\n", s.index, (long long)(x / G), (long long)(x % G),
+                     (long long)(w - s.st_sub_off[x]), s.st_waves_host[w].steps, s.st_waves_host[w].cells,
+                     (unsigned long long)tr[2 * w], (unsigned long long)tr[2 * w + 1]);
+  }
+  if (f) std::fclose(f);
+}
+
 void sync_all(mf_ctx* ctx) {
   for (auto& s : ctx->shards) {
     DeviceGuard g(s.device);
@@ -301,6 +343,7 @@ void sync_all(mf_ctx* ctx) {
     }
   }
   collect_profile(ctx);
+  dump_wave_trace(ctx);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -429,7 +472,18 @@ void fast_superstep(mf_ctx* ctx, Shard& s, int64_t superstep, double eta) {
     ups += ctx->fast_rb_size[static_cast<int64_t>(p) * n + q];
   }
   if (ups == 0) return;
-  if (ctx->fast_persistent) {
+  if (ctx->fast_lean) {
+    for (int32_t t = 0; t < ctx->G_fast; ++t) {
+      const int64_t x = smod * ctx->G_fast + t;
+      const int64_t w0 = s.st_sub_off[x], nw = s.st_sub_off[x + 1] - w0;
+      if (nw == 0) continue;
+      LaunchTimer tm(s, ctx->profiling);
+      launch_sweep_lean(s.stream, s.st_waves.as<WaveDesc>() + w0, static_cast<int>(nw), s.st_recs.as<StreamRec>(),
+                        s.uf.as<float>(), s.itf.as<float>(), s.uf.bytes(), s.itf.bytes(), ctx->P.num_factors,
+                        static_cast<float>(eta), s.st_trace.get() ? s.st_trace.as<uint64_t>() + 2 * w0 : nullptr);
+      ctx->stats.kernel_launches += 1;
+    }
+  } else if (ctx->fast_persistent) {
     MF_HIP(hipMemsetAsync(s.fast_prog.get(), 0, s.fast_prog.bytes(), s.stream));
     LaunchTimer tm(s, ctx->profiling);
     launch_fast_superstep(s.stream, blks, ctx->c, ctx->G_fast, s.fast_recs.as<FastRec>(), s.fast_cells.as<int32_t>(),
@@ -564,8 +618,12 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
     MF_REQUIRE(static_cast<uint64_t>(ctx->U.rows() + 2) * ctx->P.num_factors * 4 < (1ull << 32) &&
                    static_cast<uint64_t>(ctx->I.rows() + 1) * ctx->P.num_factors * 4 < (1ull << 32),
                "fast mode addresses each factor slab with 32-bit offsets (< 4 GiB)");
-    build_fast_plan(fp, ctx->rb, ctx->U, ctx->I, ctx->G_fast, ctx->P.num_factors, ctx->P.lambda,
-                    static_cast<uint64_t>(ctx->P.seed) * 0x9E3779B97F4A7C15ULL + 1, dummy);
+    const int k = ctx->P.num_factors;
+    const FastKernel fk = choose_fast_kernel(k);
+    ctx->fast_lean = fk == FastKernel::kLean;
+    build_fast_plan(fp, ctx->rb, ctx->U, ctx->I, ctx->G_fast, k, ctx->P.lambda,
+                    static_cast<uint64_t>(ctx->P.seed) * 0x9E3779B97F4A7C15ULL + 1, dummy, nullptr,
+                    ctx->fast_lean ? lean_ring_depth(k) : kHazardWindow);
     ctx->stats.pads = fp.pads;
     {  // priority threshold: 3x the mean non-empty cell length
       int64_t cells = 0, recs = 0;
@@ -590,6 +648,23 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
       const size_t row_bytes = static_cast<size_t>(ctx->P.num_factors) * ctx->es;
       MF_HIP(hipMemset(s.uf.as<char>() + static_cast<size_t>(dummy) * row_bytes, 0, 2 * row_bytes));
       MF_HIP(hipMemset(s.itf.as<char>() + static_cast<size_t>(ctx->fast_dummy_i) * row_bytes, 0, row_bytes));
+      if (ctx->fast_lean) {
+        LeanPlan sp;
+        build_lean_plan(sp, fp, ctx->nb, ctx->c, s.index, k);
+        s.st_recs.alloc(std::max<size_t>(sp.recs.size(), 1) * sizeof(StreamRec));
+        s.st_waves.alloc(std::max<size_t>(sp.waves.size(), 1) * sizeof(WaveDesc));
+        if (!sp.recs.empty())
+          MF_HIP(hipMemcpy(s.st_recs.get(), sp.recs.data(), sp.recs.size() * sizeof(StreamRec), hipMemcpyHostToDevice));
+        if (!sp.waves.empty())
+          MF_HIP(hipMemcpy(s.st_waves.get(), sp.waves.data(), sp.waves.size() * sizeof(WaveDesc), hipMemcpyHostToDevice));
+        s.st_sub_off = std::move(sp.sub_off);
+        if (std::getenv("MFHIP_WAVE_TRACE")) {
+          s.st_trace.alloc(std::max<size_t>(sp.waves.size(), 1) * 16);
+          MF_HIP(hipMemset(s.st_trace.get(), 0, std::max<size_t>(sp.waves.size(), 1) * 16));
+          s.st_waves_host = sp.waves;
+        }
+        continue;
+      }
       s.fast_recs.alloc(std::max<size_t>(fp.recs.size(), 1) * sizeof(FastRec));
       s.fast_cells.alloc(std::max<size_t>(fp.cell_off.size(), 1) * sizeof(int32_t));
       if (!fp.recs.empty())
@@ -869,7 +944,7 @@ mf_ctx* new_ctx(const mf_params* p) {
   ctx->P = *p;
   ctx->f64 = p->mode == MF_MODE_DETERMINISTIC_F64;
   ctx->es = ctx->f64 ? 8 : 4;
-  if (const char* v = std::getenv("MFHIP_FAST_KERNEL")) ctx->fast_persistent = std::string(v) == "persistent";
+  ctx->fast_persistent = choose_fast_kernel(p->num_factors) == FastKernel::kPersistent;
   return ctx;
 }
 
@@ -1289,8 +1364,8 @@ int mf_debug_levels(const uint32_t* urow, const uint32_t* irow, const int32_t* o
 }
 
 int mf_debug_fast_schedule(const int32_t* u, const int32_t* i, int64_t n, int32_t n_blocks, int64_t seed,
-                           int32_t groups, int32_t blocking, int32_t* block_out, int32_t* substep_out,
-                           int32_t* group_out, int64_t* pos_out) {
+                           int32_t groups, int32_t blocking, int32_t window, int32_t* block_out,
+                           int32_t* substep_out, int32_t* group_out, int64_t* pos_out) {
   return guarded([&] {
     MF_REQUIRE(n >= 0 && n_blocks >= 1 && groups >= 1, "bad argument");
     MF_REQUIRE(n == 0 || (u && i && block_out && substep_out && group_out && pos_out), "null argument");
@@ -1304,7 +1379,7 @@ int mf_debug_fast_schedule(const int32_t* u, const int32_t* i, int64_t n, int32_
     FastPlan fp;
     std::vector<int64_t> src;
     build_fast_plan(fp, rb, U, I, groups, 1, 1.0, static_cast<uint64_t>(seed) * 0x9E3779B97F4A7C15ULL + 1,
-                    static_cast<uint32_t>(U.rows()), &src);
+                    static_cast<uint32_t>(U.rows()), &src, window > 0 ? window : kHazardWindow);
     const int64_t nb2 = static_cast<int64_t>(n_blocks) * n_blocks;
     const int64_t GG = static_cast<int64_t>(groups) * groups;
     for (int64_t b = 0; b < nb2; ++b) {
@@ -1320,6 +1395,14 @@ int mf_debug_fast_schedule(const int32_t* u, const int32_t* i, int64_t n, int32_
           pos_out[j] = x - off[cidx];
         }
     }
+  });
+}
+
+int mf_fast_plan_window(int32_t k, int32_t* window_out) {
+  return guarded([&] {
+    MF_REQUIRE(window_out, "null");
+    const FastKernel fk = choose_fast_kernel(k);
+    *window_out = fk == FastKernel::kLean ? lean_ring_depth(k) : kHazardWindow;
   });
 }
 

@@ -318,7 +318,8 @@ inline uint32_t mix32(uint64_t x) {
 // of the user inside an item run.
 void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, const SideLayout& I,
                      int32_t G, int32_t k, double lambda, uint64_t order_seed, uint32_t dummy_row,
-                     std::vector<int64_t>* rec_src) {
+                     std::vector<int64_t>* rec_src, int32_t window) {
+  const int64_t kHazardWindow = window;  // shadows the default for this plan
   const uint32_t row_bytes = static_cast<uint32_t>(k) * 4u;
   const int32_t nb = rb.n_blocks;
   const int64_t nb2 = static_cast<int64_t>(nb) * nb;
@@ -496,6 +497,59 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
     std::copy(offs[bx].begin(), offs[bx].end(), fp.cell_off.begin() + fp.cell_base[b]);
     if (rec_src) std::copy(srcs[bx].begin(), srcs[bx].end(), rec_src->begin() + fp.rec_base[b]);
     std::vector<FastRec>().swap(outs[bx]);
+  });
+}
+
+// Lean schedule: every non-empty cell of a sub-step is one wave (longest first); records keep
+// the cell's order and encode the register forwarding as in build_stream_plan, with byte
+// offsets (row * k * 4) for the raw-buffer scalar offsets of kernels_lean.hip.
+void build_lean_plan(LeanPlan& lp, const FastPlan& fp, int32_t nb, int32_t c, int32_t shard, int32_t k) {
+  lp = LeanPlan();
+  const int32_t G = fp.G;
+  const int64_t nsub = static_cast<int64_t>(nb) * G;
+  const uint32_t rb = static_cast<uint32_t>(k) * 4u;
+  struct Cell { int32_t len; int64_t beg; };
+  std::vector<std::vector<Cell>> subs(nsub);
+  parallel_tasks(nsub, [&](int64_t x) {
+    const int32_t sm = static_cast<int32_t>(x / G), t = static_cast<int32_t>(x % G);
+    auto& cells = subs[x];
+    for (int32_t j = 0; j < c; ++j) {
+      const int32_t p = shard * c + j, q = (p + sm) % nb;
+      const int64_t b = static_cast<int64_t>(p) * nb + q;
+      if (fp.cell_base[b] < 0) continue;
+      const int32_t* off = fp.cell_off.data() + fp.cell_base[b];
+      for (int32_t g = 0; g < G; ++g) {
+        const int64_t cb = static_cast<int64_t>(t) * G + g;
+        const int32_t len = off[cb + 1] - off[cb];
+        if (len > 0) cells.push_back(Cell{len, fp.rec_base[b] + off[cb]});
+      }
+    }
+    std::stable_sort(cells.begin(), cells.end(), [](const Cell& a, const Cell& b2) { return a.len > b2.len; });
+  });
+  lp.sub_off.assign(nsub + 1, 0);
+  int64_t total = 0;
+  for (int64_t x = 0; x < nsub; ++x) {
+    lp.sub_off[x + 1] = lp.sub_off[x] + static_cast<int64_t>(subs[x].size());
+    for (const Cell& cl : subs[x]) {
+      lp.waves.push_back(WaveDesc{total, cl.len, 1});
+      total += cl.len;
+    }
+  }
+  lp.recs.resize(total);
+  parallel_tasks(nsub, [&](int64_t x) {
+    int64_t w = lp.sub_off[x];
+    for (const Cell& cl : subs[x]) {
+      StreamRec* out = lp.recs.data() + lp.waves[w++].base;
+      const FastRec* f = fp.recs.data() + cl.beg;
+      for (int64_t y = 0; y < cl.len; ++y) {
+        const uint32_t ur = f[y].u, ir = f[y].i & ~kPadBit;
+        const bool keep_u = y > 0 && f[y - 1].u == ur;
+        const bool keep_i = y > 0 && (f[y - 1].i & ~kPadBit) == ir;
+        const bool run_end = y + 1 == cl.len || (f[y + 1].i & ~kPadBit) != ir;
+        out[y] = StreamRec{keep_u ? kOffOOB : ur * rb, keep_i ? kOffOOB : ir * rb, ur * rb,
+                           run_end ? ir * rb : kOffOOB, f[y].r, f[y].ru, f[y].ri, 0u};
+      }
+    }
   });
 }
 

@@ -121,13 +121,44 @@ struct FastPlan {
   int64_t pads = 0;                    // padding records inserted
 };
 
+// ---------------------------------------------------------------------------------------
+// Per-cell sweep records (kernels_lean.hip): 32 B, the row fields name what to load and what
+// to store, so register forwarding is decided on the host.
+struct StreamRec {
+  uint32_t u_ld, i_ld, u_st, i_st;
+  float r, ru, ri;
+  uint32_t unused;
+};
+static_assert(sizeof(StreamRec) == 32, "StreamRec is two 16-B words");
+struct WaveDesc {
+  int64_t base;   // first record
+  int32_t steps;  // records
+  int32_t cells;
+};
+
+// ---------------------------------------------------------------------------------------
+// Fast mode, lean schedule (kernels_lean.hip): one wave per cell, k split over the 64 lanes,
+// user / item rows prefetched kLeanRing records ahead.  Records of a cell are contiguous;
+// row fields are byte offsets of the row in its slab, kOffOOB = no load / no store.
+constexpr uint32_t kOffOOB = 0xFFFFF000u;
+constexpr int kLeanRing = 32;       // k = 64, 128 (2 VMEM ops per step: vmcnt <= 63)
+constexpr int kLeanRingK256 = 16;   // k = 256 (VGPR budget)
+struct LeanPlan {
+  std::vector<StreamRec> recs;   // u_ld, i_ld, u_st, i_st as byte offsets
+  std::vector<WaveDesc> waves;   // one per non-empty cell, every sub-step (sm, t), sm-major
+  std::vector<int64_t> sub_off;  // nb*G + 1
+};
+void build_lean_plan(LeanPlan& lp, const FastPlan& fp, int32_t nb, int32_t c, int32_t shard, int32_t k);
+
 int32_t choose_groups(int64_t avg_block_ratings, int32_t blocks_per_device, int32_t fast_waves);
 
 // rec_src (optional): for every record, its position in the RatingBlocks arrays (-1: padding).
 // dummy_row: user row used by padding records (kept zero by the caller).  k: row length in
 // floats (record offsets are row * k * 4 and must stay below 4 GiB).
+// window: a row recurs inside a cell only at the next position or >= window positions later
+// (the kernel's prefetch distance; kHazardWindow for kernels_fast.hip).
 void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, const SideLayout& I,
                      int32_t G, int32_t k, double lambda, uint64_t order_seed, uint32_t dummy_row,
-                     std::vector<int64_t>* rec_src = nullptr);
+                     std::vector<int64_t>* rec_src = nullptr, int32_t window = kHazardWindow);
 
 }  // namespace mfhip

@@ -93,7 +93,7 @@ EXPORTS = [
     "mf_get_factors", "mf_set_factors", "mf_predict", "mf_rmse", "mf_empirical_risk",
     "mf_block_update", "mf_online_update", "mf_lookup", "mf_set_profiling", "mf_get_stats",
     "mf_reset_stats", "mf_jvm_shuffle", "mf_jvm_block_of", "mf_jvm_random_factors",
-    "mf_learning_rate", "mf_debug_levels", "mf_debug_fast_schedule",
+    "mf_learning_rate", "mf_debug_levels", "mf_debug_fast_schedule", "mf_fast_plan_window",
 ]
 
 _i32p = C.POINTER(C.c_int32)
@@ -150,7 +150,8 @@ def lib() -> C.CDLL:
         "mf_learning_rate": (C.c_int, [C.c_int, C.c_double, C.c_int32, C.c_double, C.c_double, _f64p]),
         "mf_debug_levels": (C.c_int, [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), _i32p, C.c_int64, _i32p]),
         "mf_debug_fast_schedule": (C.c_int, [_i32p, _i32p, C.c_int64, C.c_int32, C.c_int64, C.c_int32, C.c_int32,
-                                             _i32p, _i32p, _i32p, _i64p]),
+                                             C.c_int32, _i32p, _i32p, _i32p, _i64p]),
+        "mf_fast_plan_window": (C.c_int, [C.c_int32, _i32p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

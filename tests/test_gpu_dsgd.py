@@ -151,8 +151,8 @@ def test_edge_cases():
 
 def fast_replay_reference(d, k, nb, seed, G, iterations, lam, lr):
     """Serialise the fast plan (superstep, sub-step, group, position) and replay it in f64."""
-    from test_schedule import fast_schedule
-    b, t, g, p = fast_schedule(d.u, d.i, nb, seed, G)
+    from test_schedule import fast_plan_window, fast_schedule
+    b, t, g, p = fast_schedule(d.u, d.i, nb, seed, G, window=fast_plan_window(k))
     uids = np.unique(d.u); iids = np.unique(d.i)
     urow = np.searchsorted(uids, d.u).astype(np.int32)
     irow = np.searchsorted(iids, d.i).astype(np.int32)

@@ -49,19 +49,26 @@ def test_level_count_is_longest_row_chain_lower_bound():
     assert levels(np.arange(50), np.arange(50)).max() == 1
 
 
-def fast_schedule(u, i, nb, seed, G, blocking=L.BLOCKING_REFERENCE):
+def fast_plan_window(k):
+    w = C.c_int32(0)
+    L.check(L.lib().mf_fast_plan_window(k, C.byref(w)))
+    return w.value
+
+
+def fast_schedule(u, i, nb, seed, G, blocking=L.BLOCKING_REFERENCE, window=0):
     n = len(u)
     b = np.empty(n, np.int32); t = np.empty(n, np.int32); g = np.empty(n, np.int32); p = np.empty(n, np.int64)
     L.check(L.lib().mf_debug_fast_schedule(L.ptr(L.as_i32(u), C.c_int32), L.ptr(L.as_i32(i), C.c_int32), n, nb,
-                                           seed, G, blocking, L.ptr(b, C.c_int32), L.ptr(t, C.c_int32), L.ptr(g, C.c_int32),
+                                           seed, G, blocking, window, L.ptr(b, C.c_int32), L.ptr(t, C.c_int32), L.ptr(g, C.c_int32),
                                            L.ptr(p, C.c_int64)))
     return b, t, g, p
 
 
-@pytest.mark.parametrize("nb,G", [(1, 4), (3, 8), (4, 16)])
-def test_fast_rotation_is_conflict_free(nb, G):
+@pytest.mark.parametrize("nb,G,window", [(1, 4, 0), (3, 8, 0), (4, 16, 0), (3, 8, 32), (2, 4, 16)])
+def test_fast_rotation_is_conflict_free(nb, G, window):
     d = synth.generate(500, 200, 20000, seed=1)
-    b, t, g, p = fast_schedule(d.u, d.i, nb, 3, G)
+    b, t, g, p = fast_schedule(d.u, d.i, nb, 3, G, window=window)
+    win = window or 8
     # blocks follow DSGD blocking of the reference
     ub = np.array([mfhip.jvm.block_of(int(x), 3, nb) for x in d.u])
     ib = np.array([mfhip.jvm.block_of(int(x), 3, nb) for x in d.i])
@@ -78,8 +85,8 @@ def test_fast_rotation_is_conflict_free(nb, G):
                 for x, c in zip(ids.tolist(), cell.tolist()):
                     assert owner.setdefault(x, c) == c
     # inside a cell every user and item row recurs either at the next position (forwarded in
-    # registers: user / item runs) or at least kHazardWindow = 8 positions later (the kernel's
-    # prefetch distance); item runs keep the item row in registers.  Padding records (the gaps)
+    # registers: user / item runs) or at least `window` positions later (the kernel's prefetch
+    # distance: 8 for kernels_fast.hip, lean_ring_depth(k) for kernels_lean.hip); item runs keep the item row in registers.  Padding records (the gaps)
     # carry the zero user row and the preceding record's item, so they extend an item run.
     key = b.astype(np.int64) * G * G + t.astype(np.int64) * G + g
     runs = 0
@@ -91,7 +98,7 @@ def test_fast_rotation_is_conflict_free(nb, G):
             last, prev = {}, -1
             for x, y in sorted(zip(pos.tolist(), ids.tolist())):
                 run = side == "i" and last.get(y) == prev  # only padding since this item's last record
-                assert y not in last or x - last[y] == 1 or x - last[y] >= 8 or run, (side, y, last.get(y), x)
+                assert y not in last or x - last[y] == 1 or x - last[y] >= win or run, (side, y, last.get(y), x)
                 last[y] = prev = x
         items_in_order = d.i[m[np.argsort(pos)]]
         runs += int(np.sum(items_in_order[1:] == items_in_order[:-1]))
