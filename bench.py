@@ -168,7 +168,9 @@ def main():
     kernel_ms = D.reduce(st["kernel_ms"], "max")
     launches = st["kernel_launches"]
     alg_bytes_local = st["algorithmic_bytes"]
+    t0 = time.time()
     rmse, matched = ctx.rmse(eu, ei, er)
+    t_eval = time.time() - t0
 
     value = updates / elapsed
     bpu = 16 * k + 20 if a.mode == "fast" else 32 * k + 24
@@ -200,7 +202,7 @@ def main():
                        "parallelism": f"dsgd-ring{D.world}"},
             "rmse": round(rmse, 6), "rmse_epochs": a.warmup + a.steps, "rmse_matched": matched,
             "roofline": roof, "cpu_baseline": cpu,
-            "setup_s": {"generate": round(t_gen, 2), "prepare": round(t_prep, 2)},
+            "setup_s": {"generate": round(t_gen, 2), "prepare": round(t_prep, 2), "rmse_eval": round(t_eval, 3)},
         }
         print(json.dumps(out), flush=True)
     ctx.close()

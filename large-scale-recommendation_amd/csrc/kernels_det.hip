@@ -85,7 +85,13 @@ __global__ __launch_bounds__(256) void k_level(const DetEntry* __restrict__ ent,
   }
 }
 
-template <typename T, int KPL>
+// predictRating gathers, one pair per LANE: every lane sums its own pair's products in order
+// f = 0..k-1 (the F2jBLAS.ddot order, bit-exact in f64), so a wave runs 64 independent
+// k-long add chains instead of one readlane chain per pair.  Rows are staged through LDS in
+// chunks of CE = 128/sizeof(T) elements: CE consecutive lanes load one 128-B row chunk
+// (coalesced), then each lane reads its own pair's chunk back from a padded LDS row.
+// Bytes per pair: 2*k*sizeof(T) (HBM gather-bound).
+template <typename T>
 __global__ __launch_bounds__(256) void k_predict(const int32_t* __restrict__ urow,
                                                  const int32_t* __restrict__ irow, int64_t n,
                                                  const T* __restrict__ U, const T* __restrict__ I,
@@ -93,42 +99,58 @@ __global__ __launch_bounds__(256) void k_predict(const int32_t* __restrict__ uro
                                                  const double* __restrict__ r,
                                                  const int32_t* __restrict__ mult, double lambda,
                                                  double* __restrict__ partials) {
+  constexpr int CE = 128 / sizeof(T);  // elements per row chunk
+  constexpr int LPR = CE;               // lanes loading one row chunk (one element each)
+  constexpr int PPI = 64 / LPR;         // pairs covered by one load instruction
+  constexpr int STR = CE + 1;           // padded LDS row stride (elements): conflict-free reads
+  __shared__ T su[4][64 * STR], si[4][64 * STR];
   __shared__ double red[4][3];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t nwaves = static_cast<int64_t>(gridDim.x) * 4;
+  T* lu = su[wave];
+  T* li = si[wave];
   double sse = 0.0, cnt = 0.0, risk = 0.0;
-  for (int64_t j = static_cast<int64_t>(blockIdx.x) * 4 + wave; j < n; j += nwaves) {
-    const int32_t ur = urow[j], ir = irow[j];
-    if (ur < 0 || ir < 0) {
-      if (out && lane == 0) out[j] = 0.0;
-      continue;
+  const int64_t groups = (n + 63) / 64;
+  for (int64_t g = static_cast<int64_t>(blockIdx.x) * 4 + wave; g < groups; g += static_cast<int64_t>(gridDim.x) * 4) {
+    const int64_t j = g * 64 + lane;
+    const int32_t ur = j < n ? urow[j] : -1, ir = j < n ? irow[j] : -1;
+    const bool ok = ur >= 0 && ir >= 0;
+    double pq = 0.0, pp = 0.0, qq = 0.0;
+    for (int c0 = 0; c0 < k; c0 += CE) {
+      // stage: pair y of the group, element e of the chunk, loaded by lane (y % PPI) * LPR + e
+#pragma unroll 4
+      for (int y0 = 0; y0 < 64; y0 += PPI) {
+        const int y = y0 + lane / LPR, e = lane % LPR, f = c0 + e;
+        const int32_t uy = __shfl(ur, y), iy = __shfl(ir, y);
+        const bool v = uy >= 0 && iy >= 0 && f < k;
+        lu[y * STR + e] = v ? U[static_cast<int64_t>(uy) * k + f] : T(0);
+        li[y * STR + e] = v ? I[static_cast<int64_t>(iy) * k + f] : T(0);
+      }
+      const int lim = min(CE, k - c0);
+      for (int e = 0; e < lim; ++e) {
+        const double a = static_cast<double>(lu[lane * STR + e]), b = static_cast<double>(li[lane * STR + e]);
+        pq = pq + a * b;
+        if (mult) { pp = pp + a * a; qq = qq + b * b; }
+      }
     }
-    const T* p = U + static_cast<size_t>(ur) * k;
-    const T* q = I + static_cast<size_t>(ir) * k;
-    double pq[KPL], pp[KPL], qq[KPL];
-#pragma unroll
-    for (int c = 0; c < KPL; ++c) {
-      const int f = lane + 64 * c;
-      const double a = f < k ? static_cast<double>(p[f]) : 0.0;
-      const double b = f < k ? static_cast<double>(q[f]) : 0.0;
-      pq[c] = a * b;
-      pp[c] = a * a;
-      qq[c] = b * b;
-    }
-    const double pred = seq_dot<double, KPL>(pq, k);
-    if (out && lane == 0) out[j] = pred;
-    if (r) {
-      const double d = r[j] - pred;
+    if (j < n && out) out[j] = ok ? pq : 0.0;
+    if (ok && r) {
+      const double d = r[j] - pq;
       sse += d * d;
       cnt += 1.0;
       if (mult) {
-        const double term = d * d + lambda * (seq_dot<double, KPL>(pp, k) + seq_dot<double, KPL>(qq, k));
+        const double term = d * d + lambda * (pp + qq);
         for (int m = 0; m < mult[j]; ++m) risk += term;
       }
     }
   }
   if (!partials) return;
+  // fixed-order reduction: lanes in order, then the 4 waves
+  for (int l = 1; l < 64; l <<= 1) {
+    sse += __shfl_xor(sse, l);
+    cnt += __shfl_xor(cnt, l);
+    risk += __shfl_xor(risk, l);
+  }
   if (lane == 0) { red[wave][0] = sse; red[wave][1] = cnt; red[wave][2] = risk; }
   __syncthreads();
   if (threadIdx.x < 3) {
@@ -159,10 +181,7 @@ void predict_dispatch(hipStream_t st, const int32_t* ur, const int32_t* ir, int6
   const dim3 grid(static_cast<unsigned>(grid_blocks)), block(256);
   const T* u = static_cast<const T*>(U);
   const T* i = static_cast<const T*>(I);
-  if (k <= 64) hipLaunchKernelGGL((k_predict<T, 1>), grid, block, 0, st, ur, ir, n, u, i, k, out, r, mult, lambda, partials);
-  else if (k <= 128) hipLaunchKernelGGL((k_predict<T, 2>), grid, block, 0, st, ur, ir, n, u, i, k, out, r, mult, lambda, partials);
-  else if (k <= 256) hipLaunchKernelGGL((k_predict<T, 4>), grid, block, 0, st, ur, ir, n, u, i, k, out, r, mult, lambda, partials);
-  else hipLaunchKernelGGL((k_predict<T, 8>), grid, block, 0, st, ur, ir, n, u, i, k, out, r, mult, lambda, partials);
+  hipLaunchKernelGGL((k_predict<T>), grid, block, 0, st, ur, ir, n, u, i, k, out, r, mult, lambda, partials);
 }
 
 }  // namespace
@@ -180,7 +199,7 @@ void launch_level(hipStream_t st, const DetEntry* entries, int64_t n, void* U, v
 }
 
 int predict_grid(int64_t n) {
-  const int64_t g = (n + 3) / 4;
+  const int64_t g = (n + 255) / 256;  // 4 waves x 64 pairs per workgroup pass
   return static_cast<int>(g < 1 ? 1 : (g > 4096 ? 4096 : g));
 }
 
