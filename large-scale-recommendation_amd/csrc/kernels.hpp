@@ -51,6 +51,13 @@ int lean_ring_depth(int k);
 void launch_sweep_lean(hipStream_t st, const WaveDesc* waves, int nwaves, const StreamRec* recs, float* U, float* I,
                        uint64_t u_bytes, uint64_t i_bytes, int k, float eta, uint64_t* trace);
 
+// Fast-mode sweep, pair schedule (kernels_pair.hip): one launch per sub-step, one wave per
+// cell, two updates of one item per step (build_pair_plan).  k in {64, 128, 256}; the plan
+// window must be >= 2 * kPairRing.
+bool pair_kernel_supports(int k);
+void launch_sweep_pair(hipStream_t st, const WaveDesc* waves, int nwaves, const PairRec* recs, float* U, float* I,
+                       uint64_t u_bytes, uint64_t i_bytes, int k, float eta, uint64_t* trace);
+
 // Gather-dot over resolved pairs (row -1 = unknown id).  out[j] = p.q summed left to right in
 // f64 (predictRating's ddot).  When r != nullptr every workgroup writes partials[3*wg + c]:
 //   c=0: sum (r - p.q)^2, c=1: matched count, c=2: sum mult*((r-p.q)^2 + lambda*(p.p + q.q)).

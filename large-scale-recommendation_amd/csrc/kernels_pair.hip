@@ -1,0 +1,248 @@
+// kernels_pair.hip -- fast-mode DSGD sweep, two updates of one item per step (f32).
+//
+// Schedule: build_fast_plan's rotation (plan.cpp); sub-step t runs every cell (item group g,
+// user group (g+t) mod G) of the superstep's rating blocks at once, one wave per cell, longest
+// first (build_pair_plan).  Cells of a sub-step share no row: no atomics, no locks.
+//
+// A cell is a dependent chain through its item rows, and the hottest item's chain (29k
+// updates per NFLX superstep) sets the superstep's length.  One sequential SGD update costs a
+// 64-lane reduction on that chain.  Here a step applies two consecutive updates A, B of the
+// same item q (distinct users pA, pB) with ONE reduction round, using
+//   eA = rA - pA.q
+//   q1 = aA q + wA pA                               (wA = eta*eA, aA = 1 - eta*ri)
+//   eB = rB - pB.q1 = rB - (aA pB.q + wA pB.pA)
+// so the three dot products pA.q, pB.q, pB.pA are reduced together and only scalar work
+// separates them; the rows are then updated exactly as two sequential steps would:
+//   pA' = bA pA + wA q,  pB' = bB pB + wB q1,  q2 = aB q1 + wB pB   (DSGDforMF.scala:405-410).
+// The result equals the sequential order up to f32 rounding.  Pairs never span an item-run
+// boundary (build_pair_plan pads odd runs with a no-op B), so one pair loads at most one item
+// row and stores at most one.
+//
+// Memory: every step issues the same six vector-memory operations (user rows of A and B, item
+// row of A, their stores) with raw-buffer scalar offsets; a row that must not be touched gets
+// an offset past the slab (kOffOOB: the load returns zeros, the store is dropped), which is
+// also how forwarded rows and no-op records are expressed.  Rows of pair j+D are loaded after
+// the stores of pair j; the host keeps every row adjacent (forwarded in registers) or at
+// least 2D records apart inside a cell (plan window), so a prefetched row is always current.
+// 6 operations x D = 10 pairs stay under vmcnt's 63.
+// B_f32(k) = 16k + 20 algorithmic bytes per update.
+#include <hip/hip_runtime.h>
+
+#include "kernels.hpp"
+
+namespace mfhip {
+namespace {
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t rl(uint32_t v, int l) {
+  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), l));
+}
+__device__ __forceinline__ float rlf(float v, int l) { return __uint_as_float(rl(__float_as_uint(v), l)); }
+
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+// Three 64-lane sums at once (interleaved butterflies), uniform results.
+__device__ __forceinline__ void wave_sum3(float& x, float& y, float& z) {
+  x += dpp<0xB1>(x); y += dpp<0xB1>(y); z += dpp<0xB1>(z);
+  x += dpp<0x4E>(x); y += dpp<0x4E>(y); z += dpp<0x4E>(z);
+  x += dpp<0x141>(x); y += dpp<0x141>(y); z += dpp<0x141>(z);
+  x += dpp<0x140>(x); y += dpp<0x140>(y); z += dpp<0x140>(z);
+  asm("v_add_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+      "v_add_f32_dpp %1, %1, %1 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+      "v_add_f32_dpp %2, %2, %2 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+      "s_nop 0\n\t"
+      "v_add_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+      "v_add_f32_dpp %1, %1, %1 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+      "v_add_f32_dpp %2, %2, %2 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+      "s_nop 1"
+      : "+v"(x), "+v"(y), "+v"(z));
+  x = rlf(x, 63);
+  y = rlf(y, 63);
+  z = rlf(z, 63);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t raw_rsrc(const void* base, uint64_t bytes) {
+  const uint32_t n = bytes > 0xFFFFF000ull ? 0xFFFFF000u : static_cast<uint32_t>(bytes);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, n, 0x00020000);
+}
+
+// A lane holds floats [lane*KPL, (lane+1)*KPL) of a row, as NV float pairs.
+template <int KPL>
+struct Row {
+  static constexpr int NV = KPL == 1 ? 1 : KPL / 2;
+  f2 v[NV];
+};
+
+template <int KPL>
+__device__ __forceinline__ Row<KPL> ld(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t off) {
+  Row<KPL> r;
+  if constexpr (KPL == 1) {
+    r.v[0] = f2{__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, voff, off, 0)), 0.f};
+  } else if constexpr (KPL == 2) {
+    const auto x = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, off, 0);
+    r.v[0] = f2{__uint_as_float(x[0]), __uint_as_float(x[1])};
+  } else {
+#pragma unroll
+    for (int c = 0; c < KPL / 4; ++c) {
+      const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 16u * c, off, 0);
+      r.v[2 * c] = f2{__uint_as_float(x[0]), __uint_as_float(x[1])};
+      r.v[2 * c + 1] = f2{__uint_as_float(x[2]), __uint_as_float(x[3])};
+    }
+  }
+  return r;
+}
+
+template <int KPL>
+__device__ __forceinline__ void st(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t off, const Row<KPL>& r) {
+  if constexpr (KPL == 1) {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.v[0].x), rs, voff, off, 0);
+  } else if constexpr (KPL == 2) {
+    using u2 = uint32_t __attribute__((ext_vector_type(2)));
+    __builtin_amdgcn_raw_buffer_store_b64(u2{__float_as_uint(r.v[0].x), __float_as_uint(r.v[0].y)}, rs, voff, off, 0);
+  } else {
+#pragma unroll
+    for (int c = 0; c < KPL / 4; ++c)
+      __builtin_amdgcn_raw_buffer_store_b128(u4v{__float_as_uint(r.v[2 * c].x), __float_as_uint(r.v[2 * c].y),
+                                                 __float_as_uint(r.v[2 * c + 1].x), __float_as_uint(r.v[2 * c + 1].y)},
+                                             rs, voff + 16u * c, off, 0);
+  }
+}
+
+template <int KPL>
+__device__ __forceinline__ float dot_part(const Row<KPL>& a, const Row<KPL>& b) {
+  f2 acc = a.v[0] * b.v[0];
+#pragma unroll
+  for (int e = 1; e < Row<KPL>::NV; ++e) acc = a.v[e] * b.v[e] + acc;
+  return KPL == 1 ? acc.x : acc.x + acc.y;
+}
+
+// CH consecutive pair records of the cell, pair y in lane y (index clamped to the cell).
+struct Chunk {
+  uint32_t ua, ub, ia;     // loads: user rows of A and B, item row of A (byte offsets)
+  uint32_t sa, sb, si;     // stores: user rows of A and B, item row after B
+  uint32_t flags;          // kPairFwd* | kPairKeepQ | kPairNoop*
+  float era, erb;          // eta * r
+  float aa, ab, ba, bb;    // 1 - eta * ri, 1 - eta * ru
+};
+
+__device__ __forceinline__ void chunk_load(const u4v* __restrict__ R, int c, int npairs, int lane, float eta, Chunk& ch) {
+  const int64_t x = min(c * kPairChunk + lane, npairs - 1);
+  const u4v w0 = R[3 * x], w1 = R[3 * x + 1], w2 = R[3 * x + 2];
+  ch.ua = w0[0]; ch.ub = w0[1]; ch.ia = w0[2]; ch.sa = w0[3];
+  ch.sb = w1[0]; ch.si = w1[1]; ch.flags = w1[2];
+  ch.era = eta * __uint_as_float(w1[3]);
+  ch.erb = eta * __uint_as_float(w2[0]);
+  ch.ba = fmaf(-eta, __uint_as_float(w2[1]), 1.f);
+  ch.bb = fmaf(-eta, __uint_as_float(w2[2]), 1.f);
+  const float a = fmaf(-eta, __uint_as_float(w2[3]), 1.f);  // the pair's item
+  ch.aa = (w1[2] & kPairNoopA) ? 1.f : a;  // a no-op record leaves q unscaled
+  ch.ab = (w1[2] & kPairNoopB) ? 1.f : a;
+}
+
+template <int KPL, int D>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_sweep_pair(
+    const WaveDesc* __restrict__ waves, const u4v* __restrict__ recs, float* __restrict__ U, float* __restrict__ I,
+    uint64_t u_bytes, uint64_t i_bytes, float eta, uint64_t* __restrict__ trace) {
+  constexpr int NV = Row<KPL>::NV;
+  constexpr int CH = kPairChunk;
+  static_assert(CH % D == 0, "ring slots must repeat every chunk");
+  const int lane = threadIdx.x;
+  const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+  const WaveDesc d = waves[blockIdx.x];
+  const int npairs = d.steps;
+  const u4v* R = recs + 3 * d.base;
+  const uint32_t voff = static_cast<uint32_t>(lane) * KPL * 4u;
+  const __amdgpu_buffer_rsrc_t urs = raw_rsrc(U, u_bytes), irs = raw_rsrc(I, i_bytes);
+
+  Chunk C0, C1;  // current and next chunk
+  chunk_load(R, 0, npairs, lane, eta, C0);
+  chunk_load(R, 1, npairs, lane, eta, C1);
+  Row<KPL> PA[D], PB[D], QA[D];
+#define MF_PREFETCH(slot, CHK, YY)                                              \
+  do {                                                                          \
+    PA[slot] = ld<KPL>(urs, voff, rl(CHK.ua, (YY)));                            \
+    PB[slot] = ld<KPL>(urs, voff, rl(CHK.ub, (YY)));                            \
+    QA[slot] = ld<KPL>(irs, voff, rl(CHK.ia, (YY)));                            \
+  } while (0)
+#pragma unroll
+  for (int s = 0; s < D; ++s) MF_PREFETCH(s, C0, s);
+
+  Row<KPL> q, plA, plB;
+#pragma unroll
+  for (int e = 0; e < NV; ++e) q.v[e] = plA.v[e] = plB.v[e] = f2{0.f, 0.f};
+
+  for (int c = 0;; ++c) {
+#pragma unroll
+    for (int s = 0; s < CH; ++s) {
+      if (c * CH + s >= npairs) goto done;
+      const int slot = s % D;
+      const uint32_t fl = rl(C0.flags, s);
+      const float kfa = (fl & kPairFwdA) ? 1.f : 0.f, kfb = (fl & kPairFwdB) ? 1.f : 0.f;
+      const float kq = (fl & kPairKeepQ) ? 1.f : 0.f;
+      Row<KPL> pa, pb, qv;
+#pragma unroll
+      for (int e = 0; e < NV; ++e) {
+        pa.v[e] = kfb * plB.v[e] + (kfa * plA.v[e] + PA[slot].v[e]);  // loads of forwarded rows return 0
+        pb.v[e] = PB[slot].v[e];
+        qv.v[e] = kq * q.v[e] + QA[slot].v[e];
+      }
+      float c1 = dot_part<KPL>(pa, qv), c2 = dot_part<KPL>(pb, qv), g = dot_part<KPL>(pb, pa);
+      wave_sum3(c1, c2, g);
+      const float era = rlf(C0.era, s), erb = rlf(C0.erb, s);
+      const float aa = rlf(C0.aa, s), ab = rlf(C0.ab, s), ba = rlf(C0.ba, s), bb = rlf(C0.bb, s);
+      const float wa = fmaf(-eta, c1, era);
+      const float wb = fmaf(-eta, fmaf(wa, g, aa * c2), erb);
+#pragma unroll
+      for (int e = 0; e < NV; ++e) {
+        const f2 q0 = qv.v[e], a0 = pa.v[e], b0 = pb.v[e];
+        const f2 q1 = aa * q0 + wa * a0;
+        plA.v[e] = ba * a0 + wa * q0;
+        plB.v[e] = bb * b0 + wb * q1;
+        q.v[e] = ab * q1 + wb * b0;
+      }
+      st<KPL>(urs, voff, rl(C0.sa, s), plA);
+      st<KPL>(urs, voff, rl(C0.sb, s), plB);
+      st<KPL>(irs, voff, rl(C0.si, s), q);
+      // rows of pair j+D (after this pair's stores)
+      if (s + D < CH) MF_PREFETCH(slot, C0, s + D);
+      else MF_PREFETCH(slot, C1, s + D - CH);
+    }
+    C0 = C1;
+    chunk_load(R, c + 2, npairs, lane, eta, C1);
+  }
+done:
+#undef MF_PREFETCH
+  if (trace && lane == 0) {
+    trace[2 * blockIdx.x] = t_start;
+    trace[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+  }
+}
+
+template <int KPL>
+void dispatch(hipStream_t st, const WaveDesc* waves, int nwaves, const PairRec* recs, float* U, float* I,
+              uint64_t ub, uint64_t ib, float eta, uint64_t* trace) {
+  hipLaunchKernelGGL((k_sweep_pair<KPL, kPairRing>), dim3(static_cast<unsigned>(nwaves)), dim3(64), 0, st, waves,
+                     reinterpret_cast<const u4v*>(recs), U, I, ub, ib, eta, trace);
+}
+
+}  // namespace
+
+bool pair_kernel_supports(int k) { return k == 64 || k == 128 || k == 256; }
+
+void launch_sweep_pair(hipStream_t st, const WaveDesc* waves, int nwaves, const PairRec* recs, float* U, float* I,
+                       uint64_t u_bytes, uint64_t i_bytes, int k, float eta, uint64_t* trace) {
+  if (nwaves <= 0) return;
+  switch (k) {
+    case 64: dispatch<1>(st, waves, nwaves, recs, U, I, u_bytes, i_bytes, eta, trace); break;
+    case 128: dispatch<2>(st, waves, nwaves, recs, U, I, u_bytes, i_bytes, eta, trace); break;
+    case 256: dispatch<4>(st, waves, nwaves, recs, U, I, u_bytes, i_bytes, eta, trace); break;
+    default: break;
+  }
+}
+
+}  // namespace mfhip

@@ -96,6 +96,7 @@ struct mf_ctx {
   int32_t fast_prio_len = 1 << 30;  // cells at least this long run at raised priority
   bool fast_persistent = false;  // MFHIP_FAST_KERNEL=persistent selects the systolic single launch
   bool fast_lean = false;         // one wave per cell, deep prefetch (kernels_lean.hip), k in {64, 128, 256}
+  bool fast_pair = false;         // two updates per step (kernels_pair.hip), k in {64, 128, 256}
   std::vector<int64_t> fast_rb_size;  // per rating block (fast mode)
   mf_stats stats{};
   bool profiling = false;
@@ -108,7 +109,7 @@ namespace {
 
 constexpr int kSideU = MF_SIDE_USER;
 
-enum class FastKernel { kLean, kCell, kPersistent };
+enum class FastKernel { kPair, kLean, kCell, kPersistent };
 
 // Fast sweep kernel: MFHIP_FAST_KERNEL = cell (default, kernels_fast.hip) | persistent (same
 // file, one launch per superstep) | lean (kernels_lean.hip, k in {64, 128, 256}).
@@ -117,6 +118,7 @@ FastKernel choose_fast_kernel(int k) {
   const std::string want = v ? v : "";
   if (want == "persistent") return FastKernel::kPersistent;
   if (want == "lean" && lean_kernel_supports(k)) return FastKernel::kLean;
+  if (want == "pair" && pair_kernel_supports(k)) return FastKernel::kPair;
   return FastKernel::kCell;
 }
 
@@ -305,8 +307,8 @@ void collect_profile(mf_ctx* ctx) {
   }
 }
 
-// MFHIP_WAVE_TRACE=<file>: per wave of the stream schedule "shard sm t wave steps cells start end"
-// (100 MHz clock) of the last time every sub-step ran.
+// MFHIP_WAVE_TRACE=<file>: per wave of the per-cell schedules "shard sm t wave steps cells start
+// end" (100 MHz clock) of the last time every sub-step ran; written when the context is destroyed.
 void dump_wave_trace(mf_ctx* ctx) {
   const char* path = std::getenv("MFHIP_WAVE_TRACE");
   if (!path) return;
@@ -343,7 +345,6 @@ void sync_all(mf_ctx* ctx) {
     }
   }
   collect_profile(ctx);
-  dump_wave_trace(ctx);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -472,7 +473,18 @@ void fast_superstep(mf_ctx* ctx, Shard& s, int64_t superstep, double eta) {
     ups += ctx->fast_rb_size[static_cast<int64_t>(p) * n + q];
   }
   if (ups == 0) return;
-  if (ctx->fast_lean) {
+  if (ctx->fast_pair) {
+    for (int32_t t = 0; t < ctx->G_fast; ++t) {
+      const int64_t x = smod * ctx->G_fast + t;
+      const int64_t w0 = s.st_sub_off[x], nw = s.st_sub_off[x + 1] - w0;
+      if (nw == 0) continue;
+      LaunchTimer tm(s, ctx->profiling);
+      launch_sweep_pair(s.stream, s.st_waves.as<WaveDesc>() + w0, static_cast<int>(nw), s.st_recs.as<PairRec>(),
+                        s.uf.as<float>(), s.itf.as<float>(), s.uf.bytes(), s.itf.bytes(), ctx->P.num_factors,
+                        static_cast<float>(eta), s.st_trace.get() ? s.st_trace.as<uint64_t>() + 2 * w0 : nullptr);
+      ctx->stats.kernel_launches += 1;
+    }
+  } else if (ctx->fast_lean) {
     for (int32_t t = 0; t < ctx->G_fast; ++t) {
       const int64_t x = smod * ctx->G_fast + t;
       const int64_t w0 = s.st_sub_off[x], nw = s.st_sub_off[x + 1] - w0;
@@ -621,9 +633,10 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
     const int k = ctx->P.num_factors;
     const FastKernel fk = choose_fast_kernel(k);
     ctx->fast_lean = fk == FastKernel::kLean;
+    ctx->fast_pair = fk == FastKernel::kPair;
     build_fast_plan(fp, ctx->rb, ctx->U, ctx->I, ctx->G_fast, k, ctx->P.lambda,
                     static_cast<uint64_t>(ctx->P.seed) * 0x9E3779B97F4A7C15ULL + 1, dummy, nullptr,
-                    ctx->fast_lean ? lean_ring_depth(k) : kHazardWindow);
+                    ctx->fast_lean ? lean_ring_depth(k) : ctx->fast_pair ? 2 * kPairRing : kHazardWindow);
     ctx->stats.pads = fp.pads;
     {  // priority threshold: 3x the mean non-empty cell length
       int64_t cells = 0, recs = 0;
@@ -648,6 +661,24 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
       const size_t row_bytes = static_cast<size_t>(ctx->P.num_factors) * ctx->es;
       MF_HIP(hipMemset(s.uf.as<char>() + static_cast<size_t>(dummy) * row_bytes, 0, 2 * row_bytes));
       MF_HIP(hipMemset(s.itf.as<char>() + static_cast<size_t>(ctx->fast_dummy_i) * row_bytes, 0, row_bytes));
+      if (ctx->fast_pair) {
+        PairPlan pp;
+        build_pair_plan(pp, fp, ctx->nb, ctx->c, s.index, k);
+        ctx->stats.pads += pp.noop_halves - fp.pads;  // run padding on top of the planner's
+        s.st_recs.alloc(std::max<size_t>(pp.recs.size(), 1) * sizeof(PairRec));
+        s.st_waves.alloc(std::max<size_t>(pp.waves.size(), 1) * sizeof(WaveDesc));
+        if (!pp.recs.empty())
+          MF_HIP(hipMemcpy(s.st_recs.get(), pp.recs.data(), pp.recs.size() * sizeof(PairRec), hipMemcpyHostToDevice));
+        if (!pp.waves.empty())
+          MF_HIP(hipMemcpy(s.st_waves.get(), pp.waves.data(), pp.waves.size() * sizeof(WaveDesc), hipMemcpyHostToDevice));
+        s.st_sub_off = std::move(pp.sub_off);
+        if (std::getenv("MFHIP_WAVE_TRACE")) {
+          s.st_trace.alloc(std::max<size_t>(pp.waves.size(), 1) * 16);
+          MF_HIP(hipMemset(s.st_trace.get(), 0, std::max<size_t>(pp.waves.size(), 1) * 16));
+          s.st_waves_host = pp.waves;
+        }
+        continue;
+      }
       if (ctx->fast_lean) {
         LeanPlan sp;
         build_lean_plan(sp, fp, ctx->nb, ctx->c, s.index, k);
@@ -1056,6 +1087,11 @@ int mf_create_rank(const mf_params* p, int device_id, int nranks, int rank, cons
 int mf_destroy(mf_ctx* ctx) {
   return guarded([&] {
     if (!ctx) return;
+    for (auto& s : ctx->shards) {
+      DeviceGuard g(s.device);
+      (void)hipStreamSynchronize(s.stream);
+    }
+    dump_wave_trace(ctx);
     for (auto& s : ctx->shards) destroy_shard(s);
     if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
     delete ctx;
@@ -1402,7 +1438,7 @@ int mf_fast_plan_window(int32_t k, int32_t* window_out) {
   return guarded([&] {
     MF_REQUIRE(window_out, "null");
     const FastKernel fk = choose_fast_kernel(k);
-    *window_out = fk == FastKernel::kLean ? lean_ring_depth(k) : kHazardWindow;
+    *window_out = fk == FastKernel::kLean ? lean_ring_depth(k) : fk == FastKernel::kPair ? 2 * kPairRing : kHazardWindow;
   });
 }
 

@@ -500,15 +500,13 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
   });
 }
 
-// Lean schedule: every non-empty cell of a sub-step is one wave (longest first); records keep
-// the cell's order and encode the register forwarding as in build_stream_plan, with byte
-// offsets (row * k * 4) for the raw-buffer scalar offsets of kernels_lean.hip.
-void build_lean_plan(LeanPlan& lp, const FastPlan& fp, int32_t nb, int32_t c, int32_t shard, int32_t k) {
-  lp = LeanPlan();
+namespace {
+struct SubCell { int32_t len; int64_t beg; };
+// The non-empty cells of every sub-step (sm, t) of this shard's rating blocks, longest first.
+std::vector<std::vector<SubCell>> collect_subs(const FastPlan& fp, int32_t nb, int32_t c, int32_t shard) {
+  using Cell = SubCell;
   const int32_t G = fp.G;
   const int64_t nsub = static_cast<int64_t>(nb) * G;
-  const uint32_t rb = static_cast<uint32_t>(k) * 4u;
-  struct Cell { int32_t len; int64_t beg; };
   std::vector<std::vector<Cell>> subs(nsub);
   parallel_tasks(nsub, [&](int64_t x) {
     const int32_t sm = static_cast<int32_t>(x / G), t = static_cast<int32_t>(x % G);
@@ -526,6 +524,19 @@ void build_lean_plan(LeanPlan& lp, const FastPlan& fp, int32_t nb, int32_t c, in
     }
     std::stable_sort(cells.begin(), cells.end(), [](const Cell& a, const Cell& b2) { return a.len > b2.len; });
   });
+  return subs;
+}
+}  // namespace
+
+// Lean schedule: every non-empty cell of a sub-step is one wave (longest first); records keep
+// the cell's order and encode the register forwarding, with byte offsets (row * k * 4) for
+// the raw-buffer scalar offsets of kernels_lean.hip.
+void build_lean_plan(LeanPlan& lp, const FastPlan& fp, int32_t nb, int32_t c, int32_t shard, int32_t k) {
+  using Cell = SubCell;
+  lp = LeanPlan();
+  const int64_t nsub = static_cast<int64_t>(nb) * fp.G;
+  const uint32_t rb = static_cast<uint32_t>(k) * 4u;
+  const auto subs = collect_subs(fp, nb, c, shard);
   lp.sub_off.assign(nsub + 1, 0);
   int64_t total = 0;
   for (int64_t x = 0; x < nsub; ++x) {
@@ -551,6 +562,95 @@ void build_lean_plan(LeanPlan& lp, const FastPlan& fp, int32_t nb, int32_t c, in
       }
     }
   });
+}
+
+// Pair schedule (kernels_pair.hip): each cell's record sequence, in order, cut into steps of
+// two consecutive records A, B of one item run with distinct users.  A step with no partner
+// (odd run end, a user repeated inside the run) gets a no-op B.  Per step the record says
+// which rows to load (kOffOOB where the row is forwarded in registers or the record is a
+// no-op), which to store (the item row only where its run ends) and how A's user row is
+// forwarded: from the previous step's A or B when that was the record just before A.
+void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, int32_t shard, int32_t k) {
+  using Cell = SubCell;
+  pp = PairPlan();
+  const int64_t nsub = static_cast<int64_t>(nb) * fp.G;
+  const auto subs = collect_subs(fp, nb, c, shard);
+  auto item_of = [](const FastRec& f) { return f.i & ~kPadBit; };
+  auto is_pad = [](const FastRec& f) { return (f.i & kPadBit) != 0; };
+  // pass 1: pair counts per cell
+  std::vector<std::vector<int32_t>> npair(nsub);
+  auto count_pairs = [&](const FastRec* f, int64_t len) {
+    int32_t n = 0;
+    for (int64_t x = 0; x < len; ++n)
+      x += (x + 1 < len && item_of(f[x + 1]) == item_of(f[x]) && f[x + 1].u != f[x].u) ? 2 : 1;
+    return n;
+  };
+  parallel_tasks(nsub, [&](int64_t x) {
+    for (const Cell& cl : subs[x]) npair[x].push_back(count_pairs(fp.recs.data() + cl.beg, cl.len));
+  });
+  pp.sub_off.assign(nsub + 1, 0);
+  int64_t total = 0;
+  for (int64_t x = 0; x < nsub; ++x) {
+    pp.sub_off[x + 1] = pp.sub_off[x] + static_cast<int64_t>(subs[x].size());
+    for (size_t y = 0; y < subs[x].size(); ++y) {
+      pp.waves.push_back(WaveDesc{total, npair[x][y], 1});
+      total += npair[x][y];
+    }
+  }
+  pp.recs.resize(total);
+  std::vector<int64_t> noops(nsub, 0);
+  parallel_tasks(nsub, [&](int64_t sx) {
+    int64_t w = pp.sub_off[sx];
+    for (const Cell& cl : subs[sx]) {
+      PairRec* out = pp.recs.data() + pp.waves[w++].base;
+      const FastRec* f = fp.recs.data() + cl.beg;
+      const int64_t len = cl.len;
+      uint32_t last_u = kOffOOB;  // user offset of the record just before A (real records only)
+      uint32_t last_half = 0;     // kPairFwdA / kPairFwdB: the half that record was in
+      for (int64_t x = 0; x < len;) {
+        const FastRec& a = f[x];
+        const uint32_t item = item_of(a);
+        const bool has_b = x + 1 < len && item_of(f[x + 1]) == item && f[x + 1].u != a.u;
+        const int64_t nx = x + (has_b ? 2 : 1);
+        PairRec pr{};
+        uint32_t flags = 0;
+        const bool a_pad = is_pad(a);
+        const bool fwd = !a_pad && last_u == a.u_off;
+        if (fwd) flags |= last_half;
+        if (x > 0 && item_of(f[x - 1]) == item) flags |= kPairKeepQ;
+        pr.ua = (a_pad || fwd) ? kOffOOB : a.u_off;
+        pr.ia = (flags & kPairKeepQ) ? kOffOOB : a.i_off;
+        pr.sa = a_pad ? kOffOOB : a.u_off;
+        pr.ra = a.r;
+        pr.rua = a.ru;
+        pr.ri = a.ri;
+        if (a_pad) { flags |= kPairNoopA; noops[sx]++; }
+        if (has_b && !is_pad(f[x + 1])) {
+          const FastRec& b = f[x + 1];
+          pr.ub = pr.sb = b.u_off;
+          pr.rb = b.r;
+          pr.rub = b.ru;
+          pr.ri = b.ri;  // same item; also covers a padding A
+        } else {
+          pr.ub = pr.sb = kOffOOB;
+          flags |= kPairNoopB;
+          noops[sx]++;
+        }
+        pr.si = (nx >= len || item_of(f[nx]) != item) ? a.i_off : kOffOOB;
+        pr.flags = flags;
+        *out++ = pr;
+        if (has_b) {
+          last_u = is_pad(f[x + 1]) ? kOffOOB : f[x + 1].u_off;
+          last_half = kPairFwdB;
+        } else {
+          last_u = a_pad ? kOffOOB : a.u_off;
+          last_half = kPairFwdA;
+        }
+        x = nx;
+      }
+    }
+  });
+  for (int64_t x = 0; x < nsub; ++x) pp.noop_halves += noops[x];
 }
 
 }  // namespace mfhip

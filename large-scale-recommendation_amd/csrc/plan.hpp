@@ -150,6 +150,32 @@ struct LeanPlan {
 };
 void build_lean_plan(LeanPlan& lp, const FastPlan& fp, int32_t nb, int32_t c, int32_t shard, int32_t k);
 
+// ---------------------------------------------------------------------------------------
+// Fast mode, pair schedule (kernels_pair.hip): a step applies two consecutive updates A, B of
+// one item run; odd runs end with a no-op B.  Row fields are byte offsets, kOffOOB = no load
+// (the kernel forwards the row or the record is a no-op) / no store.
+constexpr int kPairRing = 10;   // pairs prefetched ahead: 6 VMEM ops per pair, vmcnt <= 63
+constexpr int kPairChunk = 60;  // pair records per register chunk (a multiple of kPairRing)
+constexpr uint32_t kPairFwdA = 1u;   // A's user row = previous pair's A result (registers)
+constexpr uint32_t kPairFwdB = 2u;   // A's user row = previous pair's B result
+constexpr uint32_t kPairKeepQ = 4u;  // A continues the item row held in registers
+constexpr uint32_t kPairNoopB = 8u;  // B is a no-op (run padding or planner padding)
+constexpr uint32_t kPairNoopA = 16u; // A is a no-op (planner padding)
+struct PairRec {
+  uint32_t ua, ub, ia, sa;  // loads: user A, user B, item (A starts its run); store user A
+  uint32_t sb, si, flags;   // store user B; store item after B (its run ends here)
+  float ra, rb, rua, rub, ri;
+};
+static_assert(sizeof(PairRec) == 48, "PairRec is three 16-B words");
+struct PairPlan {
+  std::vector<PairRec> recs;
+  std::vector<WaveDesc> waves;   // one per non-empty cell (steps = pairs), every (sm, t), sm-major
+  std::vector<int64_t> sub_off;  // nb*G + 1
+  int64_t noop_halves = 0;       // pair halves that are no-ops (run padding + planner padding)
+};
+// window: the plan's record window (>= 2*kPairRing).
+void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, int32_t shard, int32_t k);
+
 int32_t choose_groups(int64_t avg_block_ratings, int32_t blocks_per_device, int32_t fast_waves);
 
 // rec_src (optional): for every record, its position in the RatingBlocks arrays (-1: padding).
