@@ -204,6 +204,8 @@ int mf_debug_fast_schedule(const int32_t* users, const int32_t* items, int64_t n
 /* The plan window (records between two uses of a row inside a cell unless adjacent) the fast
    sweep uses at rank k: the prefetch distance of the kernel selected for k. */
 int mf_fast_plan_window(int32_t k, int32_t* window_out);
+/* Name of the fast-mode sweep kernel used at rank k (for profiles and bench reports). */
+const char* mf_fast_kernel_name(int32_t k);
 
 #ifdef __cplusplus
 }

@@ -43,20 +43,14 @@ void launch_fast_superstep(hipStream_t st, const FastBlk* blks, int nblk, int G,
                            uint64_t i_bytes, uint32_t dummy_u_off, uint32_t dummy_i_off, int32_t* progress,
                            int32_t* err);
 
-// Fast-mode sweep, lean schedule (kernels_lean.hip): one launch per sub-step, one wave per
-// cell (build_lean_plan).  u_bytes / i_bytes: slab sizes (byte offsets >= them are out of
-// range).  k in {64, 128, 256}; the plan window must be >= lean_ring_depth(k).
-bool lean_kernel_supports(int k);
-int lean_ring_depth(int k);
-void launch_sweep_lean(hipStream_t st, const WaveDesc* waves, int nwaves, const StreamRec* recs, float* U, float* I,
-                       uint64_t u_bytes, uint64_t i_bytes, int k, float eta, uint64_t* trace);
-
 // Fast-mode sweep, pair schedule (kernels_pair.hip): one launch per sub-step, one wave per
 // cell, two updates of one item per step (build_pair_plan).  k in {64, 128, 256}; the plan
 // window must be >= 2 * kPairRing.
 bool pair_kernel_supports(int k);
+// ev0 / ev1 (may be null): start / stop events recorded by the dispatch itself.
 void launch_sweep_pair(hipStream_t st, const WaveDesc* waves, int nwaves, const PairRec* recs, float* U, float* I,
-                       uint64_t u_bytes, uint64_t i_bytes, int k, float eta, uint64_t* trace);
+                       uint64_t u_bytes, uint64_t i_bytes, int k, float eta, uint64_t* trace, hipEvent_t ev0,
+                       hipEvent_t ev1);
 
 // Gather-dot over resolved pairs (row -1 = unknown id).  out[j] = p.q summed left to right in
 // f64 (predictRating's ddot).  When r != nullptr every workgroup writes partials[3*wg + c]:

@@ -14,18 +14,20 @@
 // so the three dot products pA.q, pB.q, pB.pA are reduced together and only scalar work
 // separates them; the rows are then updated exactly as two sequential steps would:
 //   pA' = bA pA + wA q,  pB' = bB pB + wB q1,  q2 = aB q1 + wB pB   (DSGDforMF.scala:405-410).
-// The result equals the sequential order up to f32 rounding.  Pairs never span an item-run
-// boundary (build_pair_plan pads odd runs with a no-op B), so one pair loads at most one item
-// row and stores at most one.
+// A "split" pair (B on another item qB: A's run ends, B's starts) is the same step with the
+// coupling switched off: eB = rB - pB.qB, pB' = bB pB + wB qB, qB' = aB qB + wB pB.  The
+// result equals the sequential order up to f32 rounding.
 //
-// Memory: every step issues the same six vector-memory operations (user rows of A and B, item
-// row of A, their stores) with raw-buffer scalar offsets; a row that must not be touched gets
-// an offset past the slab (kOffOOB: the load returns zeros, the store is dropped), which is
-// also how forwarded rows and no-op records are expressed.  Rows of pair j+D are loaded after
-// the stores of pair j; the host keeps every row adjacent (forwarded in registers) or at
-// least 2D records apart inside a cell (plan window), so a prefetched row is always current.
-// 6 operations x D = 10 pairs stay under vmcnt's 63.
+// Memory: every step issues the same eight vector-memory operations (user rows of A and B,
+// item rows of A and B, and their stores) with raw-buffer scalar offsets; a row that must not
+// be touched gets an offset past the slab (kOffOOB: the load returns zeros, the store is
+// dropped), which is also how forwarded rows and no-op records are expressed.  Rows of pair
+// j+D are loaded after the stores of pair j; the host keeps every row adjacent (forwarded in
+// registers) or at least 2D records apart inside a cell (plan window), so a prefetched row is
+// always current.  8 operations x D = 7 pairs stay under vmcnt's 63.  A cell that is a single
+// item run (hot items) takes a leaner loop with no item traffic at all.
 // B_f32(k) = 16k + 20 algorithmic bytes per update.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "kernels.hpp"
@@ -123,25 +125,27 @@ __device__ __forceinline__ float dot_part(const Row<KPL>& a, const Row<KPL>& b) 
 
 // CH consecutive pair records of the cell, pair y in lane y (index clamped to the cell).
 struct Chunk {
-  uint32_t ua, ub, ia;     // loads: user rows of A and B, item row of A (byte offsets)
-  uint32_t sa, sb, si;     // stores: user rows of A and B, item row after B
-  uint32_t flags;          // kPairFwd* | kPairKeepQ | kPairNoop*
-  float era, erb;          // eta * r
-  float aa, ab, ba, bb;    // 1 - eta * ri, 1 - eta * ru
+  uint32_t ua, ub, ia, ib;  // loads (byte offsets)
+  uint32_t sa, sb, sia, si; // stores
+  uint32_t flags;
+  float era, erb;           // eta * r
+  float aa, ab, ba, bb;     // 1 - eta * ri, 1 - eta * ru (1 for no-op records)
 };
 
 __device__ __forceinline__ void chunk_load(const u4v* __restrict__ R, int c, int npairs, int lane, float eta, Chunk& ch) {
   const int64_t x = min(c * kPairChunk + lane, npairs - 1);
-  const u4v w0 = R[3 * x], w1 = R[3 * x + 1], w2 = R[3 * x + 2];
-  ch.ua = w0[0]; ch.ub = w0[1]; ch.ia = w0[2]; ch.sa = w0[3];
-  ch.sb = w1[0]; ch.si = w1[1]; ch.flags = w1[2];
-  ch.era = eta * __uint_as_float(w1[3]);
-  ch.erb = eta * __uint_as_float(w2[0]);
-  ch.ba = fmaf(-eta, __uint_as_float(w2[1]), 1.f);
-  ch.bb = fmaf(-eta, __uint_as_float(w2[2]), 1.f);
-  const float a = fmaf(-eta, __uint_as_float(w2[3]), 1.f);  // the pair's item
-  ch.aa = (w1[2] & kPairNoopA) ? 1.f : a;  // a no-op record leaves q unscaled
-  ch.ab = (w1[2] & kPairNoopB) ? 1.f : a;
+  // records are read once: non-temporal, so they do not push factor rows out of L2 / MALL
+  const u4v w0 = __builtin_nontemporal_load(R + 4 * x), w1 = __builtin_nontemporal_load(R + 4 * x + 1);
+  const u4v w2 = __builtin_nontemporal_load(R + 4 * x + 2), w3 = __builtin_nontemporal_load(R + 4 * x + 3);
+  ch.ua = w0[0]; ch.ub = w0[1]; ch.ia = w0[2]; ch.ib = w0[3];
+  ch.sa = w1[0]; ch.sb = w1[1]; ch.sia = w1[2]; ch.si = w1[3];
+  ch.flags = w2[0];
+  ch.era = eta * __uint_as_float(w2[1]);
+  ch.erb = eta * __uint_as_float(w2[2]);
+  ch.ba = fmaf(-eta, __uint_as_float(w2[3]), 1.f);
+  ch.bb = fmaf(-eta, __uint_as_float(w3[0]), 1.f);
+  ch.aa = fmaf(-eta, __uint_as_float(w3[1]), 1.f);
+  ch.ab = fmaf(-eta, __uint_as_float(w3[2]), 1.f);
 }
 
 template <int KPL, int D>
@@ -155,92 +159,162 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
   const WaveDesc d = waves[blockIdx.x];
   const int npairs = d.steps;
-  const u4v* R = recs + 3 * d.base;
+  const u4v* R = recs + 4 * d.base;
   const uint32_t voff = static_cast<uint32_t>(lane) * KPL * 4u;
   const __amdgpu_buffer_rsrc_t urs = raw_rsrc(U, u_bytes), irs = raw_rsrc(I, i_bytes);
 
   Chunk C0, C1;  // current and next chunk
   chunk_load(R, 0, npairs, lane, eta, C0);
   chunk_load(R, 1, npairs, lane, eta, C1);
-  Row<KPL> PA[D], PB[D], QA[D];
-#define MF_PREFETCH(slot, CHK, YY)                                              \
-  do {                                                                          \
-    PA[slot] = ld<KPL>(urs, voff, rl(CHK.ua, (YY)));                            \
-    PB[slot] = ld<KPL>(urs, voff, rl(CHK.ub, (YY)));                            \
-    QA[slot] = ld<KPL>(irs, voff, rl(CHK.ia, (YY)));                            \
-  } while (0)
+  Row<KPL> plA, plB;  // the previous pair's updated user rows (forwarding)
 #pragma unroll
-  for (int s = 0; s < D; ++s) MF_PREFETCH(s, C0, s);
+  for (int e = 0; e < NV; ++e) plA.v[e] = plB.v[e] = f2{0.f, 0.f};
 
-  Row<KPL> q, plA, plB;
+  if (d.cells == kWaveSingleRun) {
+    // The cell is one item run (build_pair_plan): the item row stays in registers from the
+    // first pair to the last, so a pair moves no item row; B's user row is stored where it
+    // was loaded from (offset kept in an SGPR ring), A's may be forwarded from the previous
+    // pair (a user rating the item twice in a row).
+    const uint32_t item_off = rl(C0.ia, 0);
+    Row<KPL> q = ld<KPL>(irs, voff, item_off);
+    Row<KPL> RA[D], RB[D];
+    uint32_t ob[D];
 #pragma unroll
-  for (int e = 0; e < NV; ++e) q.v[e] = plA.v[e] = plB.v[e] = f2{0.f, 0.f};
-
-  for (int c = 0;; ++c) {
-#pragma unroll
-    for (int s = 0; s < CH; ++s) {
-      if (c * CH + s >= npairs) goto done;
-      const int slot = s % D;
-      const uint32_t fl = rl(C0.flags, s);
-      const float kfa = (fl & kPairFwdA) ? 1.f : 0.f, kfb = (fl & kPairFwdB) ? 1.f : 0.f;
-      const float kq = (fl & kPairKeepQ) ? 1.f : 0.f;
-      Row<KPL> pa, pb, qv;
-#pragma unroll
-      for (int e = 0; e < NV; ++e) {
-        pa.v[e] = kfb * plB.v[e] + (kfa * plA.v[e] + PA[slot].v[e]);  // loads of forwarded rows return 0
-        pb.v[e] = PB[slot].v[e];
-        qv.v[e] = kq * q.v[e] + QA[slot].v[e];
-      }
-      float c1 = dot_part<KPL>(pa, qv), c2 = dot_part<KPL>(pb, qv), g = dot_part<KPL>(pb, pa);
-      wave_sum3(c1, c2, g);
-      const float era = rlf(C0.era, s), erb = rlf(C0.erb, s);
-      const float aa = rlf(C0.aa, s), ab = rlf(C0.ab, s), ba = rlf(C0.ba, s), bb = rlf(C0.bb, s);
-      const float wa = fmaf(-eta, c1, era);
-      const float wb = fmaf(-eta, fmaf(wa, g, aa * c2), erb);
-#pragma unroll
-      for (int e = 0; e < NV; ++e) {
-        const f2 q0 = qv.v[e], a0 = pa.v[e], b0 = pb.v[e];
-        const f2 q1 = aa * q0 + wa * a0;
-        plA.v[e] = ba * a0 + wa * q0;
-        plB.v[e] = bb * b0 + wb * q1;
-        q.v[e] = ab * q1 + wb * b0;
-      }
-      st<KPL>(urs, voff, rl(C0.sa, s), plA);
-      st<KPL>(urs, voff, rl(C0.sb, s), plB);
-      st<KPL>(irs, voff, rl(C0.si, s), q);
-      // rows of pair j+D (after this pair's stores)
-      if (s + D < CH) MF_PREFETCH(slot, C0, s + D);
-      else MF_PREFETCH(slot, C1, s + D - CH);
+    for (int s = 0; s < D; ++s) {
+      ob[s] = rl(C0.ub, s);
+      RA[s] = ld<KPL>(urs, voff, rl(C0.ua, s));
+      RB[s] = ld<KPL>(urs, voff, ob[s]);
     }
-    C0 = C1;
-    chunk_load(R, c + 2, npairs, lane, eta, C1);
+    for (int c = 0;; ++c) {
+#pragma unroll
+      for (int s = 0; s < CH; ++s) {
+        if (c * CH + s >= npairs) goto run_done;
+        const int slot = s % D;
+        const uint32_t fl = rl(C0.flags, s);
+        const float kfa = (fl & kPairFwdA) ? 1.f : 0.f, kfb = (fl & kPairFwdB) ? 1.f : 0.f;
+        Row<KPL> pa;
+        const Row<KPL> pb = RB[slot];
+#pragma unroll
+        for (int e = 0; e < NV; ++e) pa.v[e] = kfb * plB.v[e] + (kfa * plA.v[e] + RA[slot].v[e]);
+        float c1 = dot_part<KPL>(pa, q), c2 = dot_part<KPL>(pb, q), g = dot_part<KPL>(pb, pa);
+        wave_sum3(c1, c2, g);
+        const float era = rlf(C0.era, s), erb = rlf(C0.erb, s);
+        const float aa = rlf(C0.aa, s), ab = rlf(C0.ab, s), ba = rlf(C0.ba, s), bb = rlf(C0.bb, s);
+        const float wa = fmaf(-eta, c1, era);
+        const float wb = fmaf(-eta, fmaf(wa, g, aa * c2), erb);
+#pragma unroll
+        for (int e = 0; e < NV; ++e) {
+          const f2 q0 = q.v[e], a0 = pa.v[e], b0 = pb.v[e];
+          const f2 q1 = aa * q0 + wa * a0;
+          plA.v[e] = ba * a0 + wa * q0;
+          plB.v[e] = bb * b0 + wb * q1;
+          q.v[e] = ab * q1 + wb * b0;
+        }
+        st<KPL>(urs, voff, rl(C0.sa, s), plA);
+        st<KPL>(urs, voff, ob[slot], plB);
+        uint32_t oa;
+        if (s + D < CH) { oa = rl(C0.ua, s + D); ob[slot] = rl(C0.ub, s + D); }
+        else { oa = rl(C1.ua, s + D - CH); ob[slot] = rl(C1.ub, s + D - CH); }
+        RA[slot] = ld<KPL>(urs, voff, oa);
+        RB[slot] = ld<KPL>(urs, voff, ob[slot]);
+      }
+      C0 = C1;
+      chunk_load(R, c + 2, npairs, lane, eta, C1);
+    }
+  run_done:
+    st<KPL>(irs, voff, item_off, q);
+    goto done;
+  }
+
+  {
+    Row<KPL> PA[D], PB[D], QA[D], QB[D];
+#define MF_PREFETCH(slot, CHK, YY)                                              \
+    do {                                                                        \
+      PA[slot] = ld<KPL>(urs, voff, rl(CHK.ua, (YY)));                          \
+      PB[slot] = ld<KPL>(urs, voff, rl(CHK.ub, (YY)));                          \
+      QA[slot] = ld<KPL>(irs, voff, rl(CHK.ia, (YY)));                          \
+      QB[slot] = ld<KPL>(irs, voff, rl(CHK.ib, (YY)));                          \
+    } while (0)
+#pragma unroll
+    for (int s = 0; s < D; ++s) MF_PREFETCH(s, C0, s);
+    Row<KPL> q;
+#pragma unroll
+    for (int e = 0; e < NV; ++e) q.v[e] = f2{0.f, 0.f};
+
+    for (int c = 0;; ++c) {
+#pragma unroll
+      for (int s = 0; s < CH; ++s) {
+        if (c * CH + s >= npairs) goto done;
+        const int slot = s % D;
+        const uint32_t fl = rl(C0.flags, s);
+        const float kfa = (fl & kPairFwdA) ? 1.f : 0.f, kfb = (fl & kPairFwdB) ? 1.f : 0.f;
+        const float kq = (fl & kPairKeepQ) ? 1.f : 0.f, sr = (fl & kPairSplit) ? 0.f : 1.f;
+        Row<KPL> pa, pb, qa, qbd;
+#pragma unroll
+        for (int e = 0; e < NV; ++e) {
+          pa.v[e] = kfb * plB.v[e] + (kfa * plA.v[e] + PA[slot].v[e]);  // loads of forwarded rows return 0
+          pb.v[e] = PB[slot].v[e];
+          qa.v[e] = kq * q.v[e] + QA[slot].v[e];
+          qbd.v[e] = sr * qa.v[e] + QB[slot].v[e];  // B's item before A's update: q (run) or qB (split)
+        }
+        float c1 = dot_part<KPL>(pa, qa), c2 = dot_part<KPL>(pb, qbd), g = dot_part<KPL>(pb, pa);
+        wave_sum3(c1, c2, g);
+        const float era = rlf(C0.era, s), erb = rlf(C0.erb, s);
+        const float aa = rlf(C0.aa, s), ab = rlf(C0.ab, s), ba = rlf(C0.ba, s), bb = rlf(C0.bb, s);
+        const float wa = fmaf(-eta, c1, era);
+        const float m = (fl & kPairSplit) ? 1.f : aa, gw = (fl & kPairSplit) ? 0.f : wa;
+        const float wb = fmaf(-eta, fmaf(gw, g, m * c2), erb);
+        Row<KPL> q1;
+#pragma unroll
+        for (int e = 0; e < NV; ++e) {
+          const f2 q0 = qa.v[e], a0 = pa.v[e], b0 = pb.v[e];
+          q1.v[e] = aa * q0 + wa * a0;
+          plA.v[e] = ba * a0 + wa * q0;
+          const f2 qb0 = sr * q1.v[e] + QB[slot].v[e];
+          plB.v[e] = bb * b0 + wb * qb0;
+          q.v[e] = ab * qb0 + wb * b0;
+        }
+        st<KPL>(urs, voff, rl(C0.sa, s), plA);
+        st<KPL>(urs, voff, rl(C0.sb, s), plB);
+        st<KPL>(irs, voff, rl(C0.sia, s), q1);
+        st<KPL>(irs, voff, rl(C0.si, s), q);
+        // rows of pair j+D (after this pair's stores)
+        if (s + D < CH) MF_PREFETCH(slot, C0, s + D);
+        else MF_PREFETCH(slot, C1, s + D - CH);
+      }
+      C0 = C1;
+      chunk_load(R, c + 2, npairs, lane, eta, C1);
+    }
+#undef MF_PREFETCH
   }
 done:
-#undef MF_PREFETCH
   if (trace && lane == 0) {
     trace[2 * blockIdx.x] = t_start;
     trace[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
   }
 }
 
+// ev0 / ev1 (may be null): timed by the dispatch packet itself (no extra stream commands).
 template <int KPL>
 void dispatch(hipStream_t st, const WaveDesc* waves, int nwaves, const PairRec* recs, float* U, float* I,
-              uint64_t ub, uint64_t ib, float eta, uint64_t* trace) {
-  hipLaunchKernelGGL((k_sweep_pair<KPL, kPairRing>), dim3(static_cast<unsigned>(nwaves)), dim3(64), 0, st, waves,
-                     reinterpret_cast<const u4v*>(recs), U, I, ub, ib, eta, trace);
+              uint64_t ub, uint64_t ib, float eta, uint64_t* trace, hipEvent_t ev0, hipEvent_t ev1) {
+  hipExtLaunchKernelGGL((k_sweep_pair<KPL, kPairRing>), dim3(static_cast<unsigned>(nwaves)), dim3(64), 0, st, ev0, ev1,
+                        0, waves, reinterpret_cast<const u4v*>(recs), U, I, ub, ib, eta, trace);
 }
 
 }  // namespace
 
 bool pair_kernel_supports(int k) { return k == 64 || k == 128 || k == 256; }
 
+
 void launch_sweep_pair(hipStream_t st, const WaveDesc* waves, int nwaves, const PairRec* recs, float* U, float* I,
-                       uint64_t u_bytes, uint64_t i_bytes, int k, float eta, uint64_t* trace) {
+                       uint64_t u_bytes, uint64_t i_bytes, int k, float eta, uint64_t* trace, hipEvent_t ev0,
+                       hipEvent_t ev1) {
   if (nwaves <= 0) return;
   switch (k) {
-    case 64: dispatch<1>(st, waves, nwaves, recs, U, I, u_bytes, i_bytes, eta, trace); break;
-    case 128: dispatch<2>(st, waves, nwaves, recs, U, I, u_bytes, i_bytes, eta, trace); break;
-    case 256: dispatch<4>(st, waves, nwaves, recs, U, I, u_bytes, i_bytes, eta, trace); break;
+    case 64: dispatch<1>(st, waves, nwaves, recs, U, I, u_bytes, i_bytes, eta, trace, ev0, ev1); break;
+    case 128: dispatch<2>(st, waves, nwaves, recs, U, I, u_bytes, i_bytes, eta, trace, ev0, ev1); break;
+    case 256: dispatch<4>(st, waves, nwaves, recs, U, I, u_bytes, i_bytes, eta, trace, ev0, ev1); break;
     default: break;
   }
 }

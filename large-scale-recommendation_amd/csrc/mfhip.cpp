@@ -95,7 +95,6 @@ struct mf_ctx {
   uint32_t fast_dummy_u = 0, fast_dummy_i = 0;  // zeroed rows past the real ones (padding / idle prefetch)
   int32_t fast_prio_len = 1 << 30;  // cells at least this long run at raised priority
   bool fast_persistent = false;  // MFHIP_FAST_KERNEL=persistent selects the systolic single launch
-  bool fast_lean = false;         // one wave per cell, deep prefetch (kernels_lean.hip), k in {64, 128, 256}
   bool fast_pair = false;         // two updates per step (kernels_pair.hip), k in {64, 128, 256}
   std::vector<int64_t> fast_rb_size;  // per rating block (fast mode)
   mf_stats stats{};
@@ -109,16 +108,17 @@ namespace {
 
 constexpr int kSideU = MF_SIDE_USER;
 
-enum class FastKernel { kPair, kLean, kCell, kPersistent };
+enum class FastKernel { kPair, kCell, kPersistent };
 
-// Fast sweep kernel: MFHIP_FAST_KERNEL = cell (default, kernels_fast.hip) | persistent (same
-// file, one launch per superstep) | lean (kernels_lean.hip, k in {64, 128, 256}).
+// Fast sweep kernel: pair (default where k is 64, 128 or 256; kernels_pair.hip) | cell (one
+// update per step, any k; kernels_fast.hip) | persistent (kernels_fast.hip, one launch per
+// superstep); MFHIP_FAST_KERNEL overrides.
 FastKernel choose_fast_kernel(int k) {
   const char* v = std::getenv("MFHIP_FAST_KERNEL");
   const std::string want = v ? v : "";
   if (want == "persistent") return FastKernel::kPersistent;
-  if (want == "lean" && lean_kernel_supports(k)) return FastKernel::kLean;
-  if (want == "pair" && pair_kernel_supports(k)) return FastKernel::kPair;
+  if (want == "cell") return FastKernel::kCell;
+  if (pair_kernel_supports(k)) return FastKernel::kPair;
   return FastKernel::kCell;
 }
 
@@ -266,11 +266,14 @@ void init_vectors(const int32_t* ids, int64_t n, int k, bool xor_seed, int64_t s
 
 // ---------------------------------------------------------------------------------------
 // profiling: a pair of HIP events around every sweep-kernel launch on the shard's stream.
+// ext = true: the launch records the pair itself (hipExtLaunchKernel start/stop events, part
+// of the dispatch packet, so timing adds no commands between kernels); start() / stop() give
+// the events, or null when profiling is off.
 struct LaunchTimer {
   Shard& s;
-  bool on;
+  bool on, ext;
   size_t slot = 0;
-  LaunchTimer(Shard& sh, bool enabled) : s(sh), on(enabled) {
+  LaunchTimer(Shard& sh, bool enabled, bool ext_events = false) : s(sh), on(enabled), ext(ext_events) {
     if (!on) return;
     if (s.ev_used + 2 > s.ev.size()) {
       for (int x = 0; x < 512; ++x) {
@@ -281,11 +284,13 @@ struct LaunchTimer {
     }
     slot = s.ev_used;
     s.ev_used += 2;
-    MF_HIP(hipEventRecord(s.ev[slot], s.stream));
+    if (!ext) MF_HIP(hipEventRecord(s.ev[slot], s.stream));
   }
+  hipEvent_t start() const { return on ? s.ev[slot] : nullptr; }
+  hipEvent_t stop() const { return on ? s.ev[slot + 1] : nullptr; }
   ~LaunchTimer() {
     if (on) {
-      (void)hipEventRecord(s.ev[slot + 1], s.stream);
+      if (!ext) (void)hipEventRecord(s.ev[slot + 1], s.stream);
       s.ev_launches++;
     }
   }
@@ -478,21 +483,11 @@ void fast_superstep(mf_ctx* ctx, Shard& s, int64_t superstep, double eta) {
       const int64_t x = smod * ctx->G_fast + t;
       const int64_t w0 = s.st_sub_off[x], nw = s.st_sub_off[x + 1] - w0;
       if (nw == 0) continue;
-      LaunchTimer tm(s, ctx->profiling);
+      LaunchTimer tm(s, ctx->profiling, true);
       launch_sweep_pair(s.stream, s.st_waves.as<WaveDesc>() + w0, static_cast<int>(nw), s.st_recs.as<PairRec>(),
                         s.uf.as<float>(), s.itf.as<float>(), s.uf.bytes(), s.itf.bytes(), ctx->P.num_factors,
-                        static_cast<float>(eta), s.st_trace.get() ? s.st_trace.as<uint64_t>() + 2 * w0 : nullptr);
-      ctx->stats.kernel_launches += 1;
-    }
-  } else if (ctx->fast_lean) {
-    for (int32_t t = 0; t < ctx->G_fast; ++t) {
-      const int64_t x = smod * ctx->G_fast + t;
-      const int64_t w0 = s.st_sub_off[x], nw = s.st_sub_off[x + 1] - w0;
-      if (nw == 0) continue;
-      LaunchTimer tm(s, ctx->profiling);
-      launch_sweep_lean(s.stream, s.st_waves.as<WaveDesc>() + w0, static_cast<int>(nw), s.st_recs.as<StreamRec>(),
-                        s.uf.as<float>(), s.itf.as<float>(), s.uf.bytes(), s.itf.bytes(), ctx->P.num_factors,
-                        static_cast<float>(eta), s.st_trace.get() ? s.st_trace.as<uint64_t>() + 2 * w0 : nullptr);
+                        static_cast<float>(eta), s.st_trace.get() ? s.st_trace.as<uint64_t>() + 2 * w0 : nullptr,
+                        tm.start(), tm.stop());
       ctx->stats.kernel_launches += 1;
     }
   } else if (ctx->fast_persistent) {
@@ -624,19 +619,19 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
   if (!ctx->f64) {
     const int64_t local = ctx->rb.start[nb2];
     const int64_t blocks_local = static_cast<int64_t>(hi - lo) * ctx->nb;
-    ctx->G_fast = choose_groups(local / std::max<int64_t>(blocks_local, 1), ctx->c, ctx->P.fast_waves);
+    const FastKernel fk = choose_fast_kernel(ctx->P.num_factors);
+    ctx->G_fast = choose_groups(local / std::max<int64_t>(blocks_local, 1), ctx->c, ctx->P.fast_waves,
+                                fk == FastKernel::kPair ? 86.0 : 150.0);
     FastPlan fp;
     const uint32_t dummy = static_cast<uint32_t>(ctx->U.rows());  // zeroed row used by padding records
     MF_REQUIRE(static_cast<uint64_t>(ctx->U.rows() + 2) * ctx->P.num_factors * 4 < (1ull << 32) &&
                    static_cast<uint64_t>(ctx->I.rows() + 1) * ctx->P.num_factors * 4 < (1ull << 32),
                "fast mode addresses each factor slab with 32-bit offsets (< 4 GiB)");
     const int k = ctx->P.num_factors;
-    const FastKernel fk = choose_fast_kernel(k);
-    ctx->fast_lean = fk == FastKernel::kLean;
     ctx->fast_pair = fk == FastKernel::kPair;
     build_fast_plan(fp, ctx->rb, ctx->U, ctx->I, ctx->G_fast, k, ctx->P.lambda,
                     static_cast<uint64_t>(ctx->P.seed) * 0x9E3779B97F4A7C15ULL + 1, dummy, nullptr,
-                    ctx->fast_lean ? lean_ring_depth(k) : ctx->fast_pair ? 2 * kPairRing : kHazardWindow);
+                    ctx->fast_pair ? 2 * kPairRing : kHazardWindow);
     ctx->stats.pads = fp.pads;
     {  // priority threshold: 3x the mean non-empty cell length
       int64_t cells = 0, recs = 0;
@@ -676,23 +671,6 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
           s.st_trace.alloc(std::max<size_t>(pp.waves.size(), 1) * 16);
           MF_HIP(hipMemset(s.st_trace.get(), 0, std::max<size_t>(pp.waves.size(), 1) * 16));
           s.st_waves_host = pp.waves;
-        }
-        continue;
-      }
-      if (ctx->fast_lean) {
-        LeanPlan sp;
-        build_lean_plan(sp, fp, ctx->nb, ctx->c, s.index, k);
-        s.st_recs.alloc(std::max<size_t>(sp.recs.size(), 1) * sizeof(StreamRec));
-        s.st_waves.alloc(std::max<size_t>(sp.waves.size(), 1) * sizeof(WaveDesc));
-        if (!sp.recs.empty())
-          MF_HIP(hipMemcpy(s.st_recs.get(), sp.recs.data(), sp.recs.size() * sizeof(StreamRec), hipMemcpyHostToDevice));
-        if (!sp.waves.empty())
-          MF_HIP(hipMemcpy(s.st_waves.get(), sp.waves.data(), sp.waves.size() * sizeof(WaveDesc), hipMemcpyHostToDevice));
-        s.st_sub_off = std::move(sp.sub_off);
-        if (std::getenv("MFHIP_WAVE_TRACE")) {
-          s.st_trace.alloc(std::max<size_t>(sp.waves.size(), 1) * 16);
-          MF_HIP(hipMemset(s.st_trace.get(), 0, std::max<size_t>(sp.waves.size(), 1) * 16));
-          s.st_waves_host = sp.waves;
         }
         continue;
       }
@@ -1434,11 +1412,19 @@ int mf_debug_fast_schedule(const int32_t* u, const int32_t* i, int64_t n, int32_
   });
 }
 
+const char* mf_fast_kernel_name(int32_t k) {
+  switch (choose_fast_kernel(k)) {
+    case FastKernel::kPair: return "k_sweep_pair";
+    case FastKernel::kPersistent: return "k_fast_superstep";
+    default: return "k_fast_substep";
+  }
+}
+
 int mf_fast_plan_window(int32_t k, int32_t* window_out) {
   return guarded([&] {
     MF_REQUIRE(window_out, "null");
     const FastKernel fk = choose_fast_kernel(k);
-    *window_out = fk == FastKernel::kLean ? lean_ring_depth(k) : fk == FastKernel::kPair ? 2 * kPairRing : kHazardWindow;
+    *window_out = fk == FastKernel::kPair ? 2 * kPairRing : kHazardWindow;
   });
 }
 

@@ -270,12 +270,13 @@ void build_level_plan(const std::vector<OrderedSeq>& seqs, LevelPlan& out) {
 // G trades launch/cell overhead and the record padding forced by heavy users (large G) against
 // cell imbalance (small G).  The per-superstep critical path is the sum over sub-steps of the
 // longest cell; on the NFLX-shaped synthetic it is minimal near ~150 ratings per average cell
-// (G = 96 for 1.4M-rating blocks), which this rule targets.
-int32_t choose_groups(int64_t avg_block_ratings, int32_t blocks_per_device, int32_t fast_waves) {
+// for the one-update-per-step kernel (G = 96 for 1.4M-rating blocks) and near ~86 for the pair
+// kernel (G = 128), the cell_target the caller passes.
+int32_t choose_groups(int64_t avg_block_ratings, int32_t blocks_per_device, int32_t fast_waves, double cell_target) {
   if (fast_waves < 0) return std::clamp(-fast_waves, 1, 4096);
   const int32_t waves = fast_waves > 0 ? fast_waves : 2048;
   int64_t g = waves / std::max(blocks_per_device, 1);
-  const int64_t cap = static_cast<int64_t>(std::sqrt(std::max<double>(avg_block_ratings, 1.0) / 150.0));
+  const int64_t cap = static_cast<int64_t>(std::sqrt(std::max<double>(avg_block_ratings, 1.0) / cell_target));
   g = std::min(g, cap);
   g = (g / 4) * 4;
   return static_cast<int32_t>(std::clamp<int64_t>(g, 4, 1024));
@@ -528,72 +529,35 @@ std::vector<std::vector<SubCell>> collect_subs(const FastPlan& fp, int32_t nb, i
 }
 }  // namespace
 
-// Lean schedule: every non-empty cell of a sub-step is one wave (longest first); records keep
-// the cell's order and encode the register forwarding, with byte offsets (row * k * 4) for
-// the raw-buffer scalar offsets of kernels_lean.hip.
-void build_lean_plan(LeanPlan& lp, const FastPlan& fp, int32_t nb, int32_t c, int32_t shard, int32_t k) {
-  using Cell = SubCell;
-  lp = LeanPlan();
-  const int64_t nsub = static_cast<int64_t>(nb) * fp.G;
-  const uint32_t rb = static_cast<uint32_t>(k) * 4u;
-  const auto subs = collect_subs(fp, nb, c, shard);
-  lp.sub_off.assign(nsub + 1, 0);
-  int64_t total = 0;
-  for (int64_t x = 0; x < nsub; ++x) {
-    lp.sub_off[x + 1] = lp.sub_off[x] + static_cast<int64_t>(subs[x].size());
-    for (const Cell& cl : subs[x]) {
-      lp.waves.push_back(WaveDesc{total, cl.len, 1});
-      total += cl.len;
-    }
-  }
-  lp.recs.resize(total);
-  parallel_tasks(nsub, [&](int64_t x) {
-    int64_t w = lp.sub_off[x];
-    for (const Cell& cl : subs[x]) {
-      StreamRec* out = lp.recs.data() + lp.waves[w++].base;
-      const FastRec* f = fp.recs.data() + cl.beg;
-      for (int64_t y = 0; y < cl.len; ++y) {
-        const uint32_t ur = f[y].u, ir = f[y].i & ~kPadBit;
-        const bool keep_u = y > 0 && f[y - 1].u == ur;
-        const bool keep_i = y > 0 && (f[y - 1].i & ~kPadBit) == ir;
-        const bool run_end = y + 1 == cl.len || (f[y + 1].i & ~kPadBit) != ir;
-        out[y] = StreamRec{keep_u ? kOffOOB : ur * rb, keep_i ? kOffOOB : ir * rb, ur * rb,
-                           run_end ? ir * rb : kOffOOB, f[y].r, f[y].ru, f[y].ri, 0u};
-      }
-    }
-  });
-}
-
 // Pair schedule (kernels_pair.hip): each cell's record sequence, in order, cut into steps of
-// two consecutive records A, B of one item run with distinct users.  A step with no partner
-// (odd run end, a user repeated inside the run) gets a no-op B.  Per step the record says
-// which rows to load (kOffOOB where the row is forwarded in registers or the record is a
-// no-op), which to store (the item row only where its run ends) and how A's user row is
-// forwarded: from the previous step's A or B when that was the record just before A.
+// two consecutive records A, B with distinct users (a no-op B where the next record repeats
+// A's user).  Per step the record names the rows to load (kOffOOB where a row is forwarded in
+// registers or the record is a no-op) and to store (an item row only where its run ends),
+// and how A's user row is forwarded: from the previous step's A or B when that was the
+// record just before A.
 void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, int32_t shard, int32_t k) {
+  (void)k;
   using Cell = SubCell;
   pp = PairPlan();
   const int64_t nsub = static_cast<int64_t>(nb) * fp.G;
   const auto subs = collect_subs(fp, nb, c, shard);
   auto item_of = [](const FastRec& f) { return f.i & ~kPadBit; };
   auto is_pad = [](const FastRec& f) { return (f.i & kPadBit) != 0; };
-  // pass 1: pair counts per cell
-  std::vector<std::vector<int32_t>> npair(nsub);
-  auto count_pairs = [&](const FastRec* f, int64_t len) {
+  auto pairs_of = [](const FastRec* f, int64_t len) {
     int32_t n = 0;
-    for (int64_t x = 0; x < len; ++n)
-      x += (x + 1 < len && item_of(f[x + 1]) == item_of(f[x]) && f[x + 1].u != f[x].u) ? 2 : 1;
+    for (int64_t x = 0; x < len; ++n) x += (x + 1 < len && f[x + 1].u != f[x].u) ? 2 : 1;
     return n;
   };
+  std::vector<std::vector<int32_t>> npair(nsub);
   parallel_tasks(nsub, [&](int64_t x) {
-    for (const Cell& cl : subs[x]) npair[x].push_back(count_pairs(fp.recs.data() + cl.beg, cl.len));
+    for (const Cell& cl : subs[x]) npair[x].push_back(pairs_of(fp.recs.data() + cl.beg, cl.len));
   });
   pp.sub_off.assign(nsub + 1, 0);
   int64_t total = 0;
   for (int64_t x = 0; x < nsub; ++x) {
     pp.sub_off[x + 1] = pp.sub_off[x] + static_cast<int64_t>(subs[x].size());
     for (size_t y = 0; y < subs[x].size(); ++y) {
-      pp.waves.push_back(WaveDesc{total, npair[x][y], 1});
+      pp.waves.push_back(WaveDesc{total, npair[x][y], kWaveGeneric});
       total += npair[x][y];
     }
   }
@@ -602,41 +566,52 @@ void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, in
   parallel_tasks(nsub, [&](int64_t sx) {
     int64_t w = pp.sub_off[sx];
     for (const Cell& cl : subs[sx]) {
-      PairRec* out = pp.recs.data() + pp.waves[w++].base;
+      const int64_t w_this = w++;
+      PairRec* const first = pp.recs.data() + pp.waves[w_this].base;
+      PairRec* out = first;
       const FastRec* f = fp.recs.data() + cl.beg;
       const int64_t len = cl.len;
       uint32_t last_u = kOffOOB;  // user offset of the record just before A (real records only)
       uint32_t last_half = 0;     // kPairFwdA / kPairFwdB: the half that record was in
       for (int64_t x = 0; x < len;) {
         const FastRec& a = f[x];
-        const uint32_t item = item_of(a);
-        const bool has_b = x + 1 < len && item_of(f[x + 1]) == item && f[x + 1].u != a.u;
+        const bool has_b = x + 1 < len && f[x + 1].u != a.u;
         const int64_t nx = x + (has_b ? 2 : 1);
         PairRec pr{};
         uint32_t flags = 0;
         const bool a_pad = is_pad(a);
-        const bool fwd = !a_pad && last_u == a.u_off;
-        if (fwd) flags |= last_half;
-        if (x > 0 && item_of(f[x - 1]) == item) flags |= kPairKeepQ;
-        pr.ua = (a_pad || fwd) ? kOffOOB : a.u_off;
+        if (!a_pad && last_u == a.u_off) flags |= last_half;
+        if (x > 0 && item_of(f[x - 1]) == item_of(a)) flags |= kPairKeepQ;
+        pr.ua = (a_pad || (flags & (kPairFwdA | kPairFwdB))) ? kOffOOB : a.u_off;
         pr.ia = (flags & kPairKeepQ) ? kOffOOB : a.i_off;
         pr.sa = a_pad ? kOffOOB : a.u_off;
         pr.ra = a.r;
         pr.rua = a.ru;
-        pr.ri = a.ri;
-        if (a_pad) { flags |= kPairNoopA; noops[sx]++; }
-        if (has_b && !is_pad(f[x + 1])) {
+        pr.ria = a.ri;
+        if (a_pad) noops[sx]++;
+        pr.ib = pr.ub = pr.sb = pr.sia = kOffOOB;
+        // the item row whose run may end after this step: B's if B exists, else A's
+        const FastRec* tail = &a;
+        if (has_b) {
           const FastRec& b = f[x + 1];
-          pr.ub = pr.sb = b.u_off;
-          pr.rb = b.r;
-          pr.rub = b.ru;
-          pr.ri = b.ri;  // same item; also covers a padding A
+          tail = &b;
+          if (item_of(b) != item_of(a)) {  // split: A's run ends at A, B starts a run
+            flags |= kPairSplit;
+            pr.sia = a.i_off;
+            pr.ib = b.i_off;
+          }
+          if (!is_pad(b)) {
+            pr.ub = pr.sb = b.u_off;
+            pr.rb = b.r;
+            pr.rub = b.ru;
+            pr.rib = b.ri;
+          } else {
+            noops[sx]++;
+          }
         } else {
-          pr.ub = pr.sb = kOffOOB;
-          flags |= kPairNoopB;
           noops[sx]++;
         }
-        pr.si = (nx >= len || item_of(f[nx]) != item) ? a.i_off : kOffOOB;
+        pr.si = (nx >= len || item_of(f[nx]) != item_of(*tail)) ? tail->i_off : kOffOOB;
         pr.flags = flags;
         *out++ = pr;
         if (has_b) {
@@ -648,6 +623,12 @@ void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, in
         }
         x = nx;
       }
+      // one item run (no split, every later pair keeps the item): the kernel's lean path
+      bool single = first[0].ia != kOffOOB && !(first[0].flags & (kPairKeepQ | kPairSplit));
+      for (const PairRec* r = first; single && r < out; ++r)
+        single = !(r->flags & kPairSplit) && (r == first || (r->flags & kPairKeepQ)) && r->ub == r->sb &&
+                 (r + 1 < out ? r->si == kOffOOB : r->si == first[0].ia);
+      if (single) pp.waves[w_this].cells = kWaveSingleRun;
     }
   });
   for (int64_t x = 0; x < nsub; ++x) pp.noop_halves += noops[x];

@@ -122,14 +122,8 @@ struct FastPlan {
 };
 
 // ---------------------------------------------------------------------------------------
-// Per-cell sweep records (kernels_lean.hip): 32 B, the row fields name what to load and what
-// to store, so register forwarding is decided on the host.
-struct StreamRec {
-  uint32_t u_ld, i_ld, u_st, i_st;
-  float r, ru, ri;
-  uint32_t unused;
-};
-static_assert(sizeof(StreamRec) == 32, "StreamRec is two 16-B words");
+// Per-cell sweep launch table (kernels_pair.hip): one wave per cell.
+constexpr uint32_t kOffOOB = 0xFFFFF000u;  // a row byte offset past any slab: load 0 / no store
 struct WaveDesc {
   int64_t base;   // first record
   int32_t steps;  // records
@@ -137,46 +131,38 @@ struct WaveDesc {
 };
 
 // ---------------------------------------------------------------------------------------
-// Fast mode, lean schedule (kernels_lean.hip): one wave per cell, k split over the 64 lanes,
-// user / item rows prefetched kLeanRing records ahead.  Records of a cell are contiguous;
-// row fields are byte offsets of the row in its slab, kOffOOB = no load / no store.
-constexpr uint32_t kOffOOB = 0xFFFFF000u;
-constexpr int kLeanRing = 32;       // k = 64, 128 (2 VMEM ops per step: vmcnt <= 63)
-constexpr int kLeanRingK256 = 16;   // k = 256 (VGPR budget)
-struct LeanPlan {
-  std::vector<StreamRec> recs;   // u_ld, i_ld, u_st, i_st as byte offsets
-  std::vector<WaveDesc> waves;   // one per non-empty cell, every sub-step (sm, t), sm-major
-  std::vector<int64_t> sub_off;  // nb*G + 1
-};
-void build_lean_plan(LeanPlan& lp, const FastPlan& fp, int32_t nb, int32_t c, int32_t shard, int32_t k);
-
-// ---------------------------------------------------------------------------------------
 // Fast mode, pair schedule (kernels_pair.hip): a step applies two consecutive updates A, B of
-// one item run; odd runs end with a no-op B.  Row fields are byte offsets, kOffOOB = no load
-// (the kernel forwards the row or the record is a no-op) / no store.
-constexpr int kPairRing = 10;   // pairs prefetched ahead: 6 VMEM ops per pair, vmcnt <= 63
-constexpr int kPairChunk = 60;  // pair records per register chunk (a multiple of kPairRing)
+// one cell with distinct users -- of the same item ("run" pair) or of two items ("split"
+// pair, A ends its item run, B starts one); a step whose B would repeat A's user gets a
+// no-op B.  Row fields are byte offsets, kOffOOB = no load (the row is forwarded in registers
+// or the record is a no-op) / no store.
+constexpr int kPairRing = 7;    // pairs prefetched ahead: 8 VMEM ops per pair, vmcnt <= 63
+constexpr int kPairChunk = 56;  // pair records per register chunk (a multiple of kPairRing)
 constexpr uint32_t kPairFwdA = 1u;   // A's user row = previous pair's A result (registers)
 constexpr uint32_t kPairFwdB = 2u;   // A's user row = previous pair's B result
 constexpr uint32_t kPairKeepQ = 4u;  // A continues the item row held in registers
-constexpr uint32_t kPairNoopB = 8u;  // B is a no-op (run padding or planner padding)
-constexpr uint32_t kPairNoopA = 16u; // A is a no-op (planner padding)
+constexpr uint32_t kPairSplit = 8u;  // B's item differs from A's (B starts a run)
+constexpr int32_t kWaveGeneric = 1;    // WaveDesc.cells: generic pair steps
+constexpr int32_t kWaveSingleRun = 2;  // the cell is one item run: no item traffic per pair
 struct PairRec {
-  uint32_t ua, ub, ia, sa;  // loads: user A, user B, item (A starts its run); store user A
-  uint32_t sb, si, flags;   // store user B; store item after B (its run ends here)
-  float ra, rb, rua, rub, ri;
+  uint32_t ua, ub, ia, ib;   // loads: users A and B; items of A (run start) and B (split)
+  uint32_t sa, sb, sia, si;  // stores: users A and B; A's item (split), the item after B (run end)
+  uint32_t flags;
+  float ra, rb, rua, rub, ria, rib;  // ratings and lambda/omega (0 for no-op records)
+  uint32_t pad_;
 };
-static_assert(sizeof(PairRec) == 48, "PairRec is three 16-B words");
+static_assert(sizeof(PairRec) == 64, "PairRec is four 16-B words");
 struct PairPlan {
   std::vector<PairRec> recs;
   std::vector<WaveDesc> waves;   // one per non-empty cell (steps = pairs), every (sm, t), sm-major
   std::vector<int64_t> sub_off;  // nb*G + 1
-  int64_t noop_halves = 0;       // pair halves that are no-ops (run padding + planner padding)
+  int64_t noop_halves = 0;       // pair halves that are no-ops (planner padding, repeated users)
 };
-// window: the plan's record window (>= 2*kPairRing).
+// The plan window must be >= 2 * kPairRing records.
 void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, int32_t shard, int32_t k);
 
-int32_t choose_groups(int64_t avg_block_ratings, int32_t blocks_per_device, int32_t fast_waves);
+int32_t choose_groups(int64_t avg_block_ratings, int32_t blocks_per_device, int32_t fast_waves,
+                      double cell_target = 150.0);
 
 // rec_src (optional): for every record, its position in the RatingBlocks arrays (-1: padding).
 // dummy_row: user row used by padding records (kept zero by the caller).  k: row length in

@@ -94,6 +94,7 @@ EXPORTS = [
     "mf_block_update", "mf_online_update", "mf_lookup", "mf_set_profiling", "mf_get_stats",
     "mf_reset_stats", "mf_jvm_shuffle", "mf_jvm_block_of", "mf_jvm_random_factors",
     "mf_learning_rate", "mf_debug_levels", "mf_debug_fast_schedule", "mf_fast_plan_window",
+    "mf_fast_kernel_name",
 ]
 
 _i32p = C.POINTER(C.c_int32)
@@ -152,6 +153,7 @@ def lib() -> C.CDLL:
         "mf_debug_fast_schedule": (C.c_int, [_i32p, _i32p, C.c_int64, C.c_int32, C.c_int64, C.c_int32, C.c_int32,
                                              C.c_int32, _i32p, _i32p, _i32p, _i64p]),
         "mf_fast_plan_window": (C.c_int, [C.c_int32, _i32p]),
+        "mf_fast_kernel_name": (C.c_char_p, [C.c_int32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
