@@ -621,7 +621,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
     const int64_t blocks_local = static_cast<int64_t>(hi - lo) * ctx->nb;
     const FastKernel fk = choose_fast_kernel(ctx->P.num_factors);
     ctx->G_fast = choose_groups(local / std::max<int64_t>(blocks_local, 1), ctx->c, ctx->P.fast_waves,
-                                fk == FastKernel::kPair ? 86.0 : 150.0);
+                                fk == FastKernel::kPair ? 40.0 : 150.0, fk == FastKernel::kPair ? 1024 : 2048);
     FastPlan fp;
     const uint32_t dummy = static_cast<uint32_t>(ctx->U.rows());  // zeroed row used by padding records
     MF_REQUIRE(static_cast<uint64_t>(ctx->U.rows() + 2) * ctx->P.num_factors * 4 < (1ull << 32) &&

@@ -270,11 +270,13 @@ void build_level_plan(const std::vector<OrderedSeq>& seqs, LevelPlan& out) {
 // G trades launch/cell overhead and the record padding forced by heavy users (large G) against
 // cell imbalance (small G).  The per-superstep critical path is the sum over sub-steps of the
 // longest cell; on the NFLX-shaped synthetic it is minimal near ~150 ratings per average cell
-// for the one-update-per-step kernel (G = 96 for 1.4M-rating blocks) and near ~86 for the pair
-// kernel (G = 128), the cell_target the caller passes.
-int32_t choose_groups(int64_t avg_block_ratings, int32_t blocks_per_device, int32_t fast_waves, double cell_target) {
+// for the one-update-per-step kernel (G = 96 for 1.4M-rating blocks).  The pair kernel does
+// best near 1024 waves per sub-step with cells of >= ~40 ratings (NFLX: G = 128; ML20M, 281k
+// ratings per block: G = 80), the cell_target / default_waves the caller passes.
+int32_t choose_groups(int64_t avg_block_ratings, int32_t blocks_per_device, int32_t fast_waves, double cell_target,
+                      int32_t default_waves) {
   if (fast_waves < 0) return std::clamp(-fast_waves, 1, 4096);
-  const int32_t waves = fast_waves > 0 ? fast_waves : 2048;
+  const int32_t waves = fast_waves > 0 ? fast_waves : default_waves;
   int64_t g = waves / std::max(blocks_per_device, 1);
   const int64_t cap = static_cast<int64_t>(std::sqrt(std::max<double>(avg_block_ratings, 1.0) / cell_target));
   g = std::min(g, cap);

@@ -162,7 +162,7 @@ struct PairPlan {
 void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, int32_t shard, int32_t k);
 
 int32_t choose_groups(int64_t avg_block_ratings, int32_t blocks_per_device, int32_t fast_waves,
-                      double cell_target = 150.0);
+                      double cell_target = 150.0, int32_t default_waves = 2048);
 
 // rec_src (optional): for every record, its position in the RatingBlocks arrays (-1: padding).
 // dummy_row: user row used by padding records (kept zero by the caller).  k: row length in
