@@ -145,6 +145,24 @@ int mf_get_factors(mf_ctx* ctx, int side, int32_t* ids_out, double* vecs_out, in
                    int64_t* written);
 /* Overwrite (or, in online use, insert) factor rows (checkpoint restore). */
 int mf_set_factors(mf_ctx* ctx, int side, const int32_t* ids, const double* vecs, int64_t n);
+/* The context's parameters (e.g. the rank k a caller sizes factor buffers with). */
+int mf_get_params(mf_ctx* ctx, mf_params* out);
+
+/* Input and snapshots.
+   mf_read_ratings: env.readCsvFile[(Int, Int, Double)](path) (DSGDforMF.scala:72) and MovieLens
+   u.data: one "user<d>item<d>rating[<d>...]" record per line, d = delim (',' is Flink's default,
+   '\t' u.data, 0 = any run of spaces / tabs / commas), the first skip_lines lines skipped, blank
+   lines ignored, extra fields ignored.  users == NULL: only *n_out = record count.  A line
+   that does not parse fails with MF_ERR_INVALID naming the line.
+   mf_save_model / mf_load_model: the TemporaryPath persistence of the fit (DSGDforMF.scala:291-296,
+   330-349) as one binary file: both factor sides (ids ascending, f64) and the superstep counter.
+   Loading sets the factors (mf_set_factors semantics) and returns the stored counter; to resume
+   a fit: mf_dsgd_prepare (same ratings), mf_load_model, mf_dsgd_set_superstep(counter),
+   mf_dsgd_run. */
+int mf_read_ratings(const char* path, char delim, int32_t skip_lines, int32_t* users, int32_t* items,
+                    double* ratings, int64_t cap, int64_t* n_out);
+int mf_save_model(mf_ctx* ctx, const char* path);
+int mf_load_model(mf_ctx* ctx, const char* path, int64_t* superstep_out);
 
 /* predictRating (MatrixFactorization.scala:239-274): inner-join semantics via found[]. */
 int mf_predict(mf_ctx* ctx, const int32_t* users, const int32_t* items, int64_t n, double* out,

@@ -23,6 +23,26 @@ struct Error : std::runtime_error {
 
 [[noreturn]] inline void fail(int code, const std::string& msg) { throw Error(code, msg); }
 
+// The C ABI's error convention: run f, map exceptions to an MF_ERR_* status and keep the
+// message for mf_last_error() (thread-local, defined in mfhip.cpp).
+extern thread_local std::string g_last_error;
+template <typename F>
+int guarded(F&& f) {
+  try {
+    f();
+    return MF_OK;
+  } catch (const Error& e) {
+    g_last_error = e.what();
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    g_last_error = "host allocation failed";
+    return MF_ERR_CAPACITY;
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return MF_ERR_INVALID;
+  }
+}
+
 #define MF_HIP(call)                                                                        \
   do {                                                                                      \
     hipError_t _e = (call);                                                                 \

@@ -123,24 +123,6 @@ FastKernel choose_fast_kernel(int k) {
 }
 
 
-void set_error(const std::string& m) { g_last_error = m; }
-
-template <typename F>
-int guarded(F&& f) {
-  try {
-    f();
-    return MF_OK;
-  } catch (const Error& e) {
-    set_error(e.what());
-    return e.code;
-  } catch (const std::bad_alloc&) {
-    set_error("host allocation failed");
-    return MF_ERR_CAPACITY;
-  } catch (const std::exception& e) {
-    set_error(e.what());
-    return MF_ERR_INVALID;
-  }
-}
 
 double bytes_per_update(const mf_ctx* ctx) {
   const double k = ctx->P.num_factors;
@@ -1174,11 +1156,27 @@ int mf_set_factors(mf_ctx* ctx, int side, const int32_t* ids, const double* vecs
     std::vector<int32_t> rows(n);
     for (int64_t j = 0; j < n; ++j) rows[j] = online_row(ctx, S, ids[j], fresh);
     const int k = ctx->P.num_factors;
+    sync_all(ctx);
     for (auto& s : ctx->shards) {
-      sync_all(ctx);
       ensure_rows(ctx, s, side, std::max<int64_t>(S.rows(), 1));
-      for (int64_t j = 0; j < n; ++j) upload_rows(ctx, s, side, rows[j], vecs + static_cast<size_t>(j) * k, 1);
+      if (n < 64) {
+        for (int64_t j = 0; j < n; ++j) upload_rows(ctx, s, side, rows[j], vecs + static_cast<size_t>(j) * k, 1);
+        continue;
+      }
+      // many rows: patch a host copy of the slab and upload it once
+      std::vector<double> all(static_cast<size_t>(S.rows()) * k);
+      download_rows(ctx, s, side, 0, S.rows(), all.data());
+      for (int64_t j = 0; j < n; ++j)
+        std::memcpy(all.data() + static_cast<size_t>(rows[j]) * k, vecs + static_cast<size_t>(j) * k, k * sizeof(double));
+      upload_rows(ctx, s, side, 0, all.data(), S.rows());
     }
+  });
+}
+
+int mf_get_params(mf_ctx* ctx, mf_params* out) {
+  return guarded([&] {
+    MF_REQUIRE(ctx && out, "null argument");
+    *out = ctx->P;
   });
 }
 

@@ -12,11 +12,12 @@ from .core import (FactorInitializer, FactorInitializerDescriptor, Factors, Fact
                    RandomFactorInitializerDescriptor, Rating, SGDUpdater, UserUpdate)
 from .dsgd import DSGDforMF, LearningRateMethod
 from .online import OnlineMF
+from .ratings_io import read_ratings
 
 __all__ = [
     "MFError", "MFNoDeviceError", "device_count", "version", "Context", "block_update", "DSGDforMF",
     "LearningRateMethod", "OnlineMF", "Rating", "FactorVector", "Factors", "FactorUpdater", "SGDUpdater",
     "MockFactorUpdater", "FactorInitializer", "FactorInitializerDescriptor", "PseudoRandomFactorInitializer",
     "PseudoRandomFactorInitializerDescriptor", "RandomFactorInitializer", "RandomFactorInitializerDescriptor",
-    "UserUpdate", "ItemUpdate",
+    "UserUpdate", "ItemUpdate", "read_ratings",
 ]

@@ -94,7 +94,7 @@ EXPORTS = [
     "mf_block_update", "mf_online_update", "mf_lookup", "mf_set_profiling", "mf_get_stats",
     "mf_reset_stats", "mf_jvm_shuffle", "mf_jvm_block_of", "mf_jvm_random_factors",
     "mf_learning_rate", "mf_debug_levels", "mf_debug_fast_schedule", "mf_fast_plan_window",
-    "mf_fast_kernel_name",
+    "mf_fast_kernel_name", "mf_get_params", "mf_read_ratings", "mf_save_model", "mf_load_model",
 ]
 
 _i32p = C.POINTER(C.c_int32)
@@ -154,6 +154,10 @@ def lib() -> C.CDLL:
                                              C.c_int32, _i32p, _i32p, _i32p, _i64p]),
         "mf_fast_plan_window": (C.c_int, [C.c_int32, _i32p]),
         "mf_fast_kernel_name": (C.c_char_p, [C.c_int32]),
+        "mf_get_params": (C.c_int, [C.c_void_p, C.POINTER(mf_params)]),
+        "mf_read_ratings": (C.c_int, [C.c_char_p, C.c_char, C.c_int32, _i32p, _i32p, _f64p, C.c_int64, _i64p]),
+        "mf_save_model": (C.c_int, [C.c_void_p, C.c_char_p]),
+        "mf_load_model": (C.c_int, [C.c_void_p, C.c_char_p, _i64p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -139,7 +139,18 @@ class Context:
                                        flavour, num_partitions, C.byref(tu), C.byref(ti)))
         return tu.value, ti.value
 
-    # -- stats -----------------------------------------------------------------
+    # -- snapshots (TemporaryPath persistence, DSGDforMF.scala:291-296, 330-349) --
+    def save(self, path: str) -> None:
+        check(L.lib().mf_save_model(self._h, path.encode()))
+
+    def load(self, path: str) -> int:
+        """Set both factor sides from a snapshot; returns the stored superstep counter (to resume
+        a fit: prepare(same ratings), load(path), set_superstep(counter), run(...))."""
+        step = C.c_int64(0)
+        check(L.lib().mf_load_model(self._h, path.encode(), C.byref(step)))
+        return step.value
+
+        # -- stats -----------------------------------------------------------------
     def set_profiling(self, on: bool) -> None:
         check(L.lib().mf_set_profiling(self._h, 1 if on else 0))
 

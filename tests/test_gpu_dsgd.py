@@ -118,6 +118,32 @@ def test_staged_run_and_resume_equal_one_shot():
             assert np.array_equal(ctx2.factors(side)[1], m.factors(side)[1])
 
 
+def test_snapshot_file_resume_bit_exact(tmp_path):
+    """mf_save_model / mf_load_model (TemporaryPath persistence, DSGDforMF.scala:291-296, 330-349):
+    4 supersteps, snapshot to disk, a fresh context resumes and finishes == the oracle's one-shot fit;
+    with more than 64 rows per side the load takes the bulk-upload path."""
+    d = synth.generate(300, 150, 8000, seed=2)
+    m = coracle.dsgd_fit(d.u, d.i, d.r, k=16, iterations=3, n_blocks=3, seed=4)
+    snap = str(tmp_path / "model.mfsnap")
+    with mfhip.Context(params(16, 3, 3, 4)) as ctx:
+        ctx.prepare(d.u, d.i, d.r)
+        ctx.run(4)
+        ctx.save(snap)
+    with mfhip.Context(params(16, 3, 3, 4)) as ctx2:
+        ctx2.prepare(d.u, d.i, d.r)
+        step = ctx2.load(snap)
+        assert step == 4
+        ctx2.superstep = step
+        ctx2.run(5)
+        for side in (0, 1):
+            ids, vecs = ctx2.factors(side)
+            rids, rvecs = m.factors(side)
+            assert np.array_equal(ids, rids) and np.array_equal(vecs, rvecs)
+    with mfhip.Context(params(8, 1, 1, 0)) as bad:
+        with pytest.raises(mfhip.MFError, match="rank"):
+            bad.load(snap)
+
+
 def test_block_update_exact():
     rng = np.random.default_rng(8)
     nu, ni, k, n = 30, 20, 12, 400
