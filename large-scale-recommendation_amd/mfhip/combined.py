@@ -1,0 +1,84 @@
+"""Combined offline + online model.
+
+Mirrors OnlineSpark.buildModelCombineOffline (sp/OnlineSpark.scala:26-162) on GPU-resident
+factors: every micro-batch either
+  * updates the model online -- one OfflineSpark.offlineDSGDUpdatesOnly sweep of the batch over
+    num_partitions partitions (sp/OfflineSpark.scala:91-207, iterations = 1; MF_ONLINE_SPARK_SWEEP)
+    -- and emits the touched user and item vectors (UpdateSeparatedHashMap.updates, :33-67), or,
+  * every `offline_every`-th batch, refits from scratch on the whole rating history --
+    OfflineSpark.offlineDSGD with empty initial factors and `iterations` sweeps (:68-89) -- and
+    emits every vector.
+The counters follow the reference (decrement, fire at <= 0, reset).  Every `checkpoint_every`-th
+batch the model is written as an mf_save_model snapshot when `snapshot_dir` is given: the
+localCheckpoint of the reference (:93-99) cuts RDD lineage; here it is a restartable file.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Optional, Tuple
+
+import numpy as np
+
+from . import _lib as L
+from .context import Context
+
+
+class OnlineOfflineSpark:
+    def __init__(self, num_factors: int, learning_rate: float = 0.01, num_partitions: int = 4,
+                 offline_every: int = 10, checkpoint_every: int = 10, iterations: int = 10,
+                 init: str = "pseudo_random", seed: int = 0, mode: str = "deterministic",
+                 snapshot_dir: Optional[str] = None):
+        self.k = num_factors
+        self.P = num_partitions
+        self.offline_every = offline_every
+        self.checkpoint_every = checkpoint_every
+        self.iterations = iterations
+        self.snapshot_dir = snapshot_dir
+        self._offline_cnt = offline_every
+        self._checkpoint_cnt = checkpoint_every
+        self._batches = 0
+        p = L.default_params()
+        p.num_factors = num_factors
+        p.online_learning_rate = learning_rate
+        p.online_init = L.INIT_SEEDED if init == "seeded" else L.INIT_PSEUDO_RANDOM
+        p.seed = seed
+        p.mode = L.MODE_FAST_F32 if mode == "fast" else L.MODE_DETERMINISTIC_F64
+        self._params = p
+        self.ctx = Context(p)
+        self._hist = ([], [], [])  # ratings history (OnlineSpark.scala:71), as array chunks
+
+    def close(self) -> None:
+        self.ctx.close()
+
+    def process(self, u, i, r) -> Tuple[Dict[int, np.ndarray], Dict[int, np.ndarray], bool]:
+        """One micro-batch; returns (user updates, item updates, whether it was an offline refit)."""
+        u = np.ascontiguousarray(u, np.int32)
+        i = np.ascontiguousarray(i, np.int32)
+        r = np.ascontiguousarray(r, np.float64)
+        self._batches += 1
+        self._checkpoint_cnt -= 1
+        checkpoint = self._checkpoint_cnt <= 0
+        if checkpoint:
+            self._checkpoint_cnt = self.checkpoint_every
+        self._offline_cnt -= 1
+        offline = self._offline_cnt <= 0
+        if offline:
+            self._offline_cnt = self.offline_every
+        for dst, src in zip(self._hist, (u, i, r)):
+            dst.append(src)
+        if not offline:
+            self.ctx.online_update(u, i, r, L.ONLINE_SPARK_SWEEP, self.P)
+            users, items = np.unique(u), np.unique(i)
+        else:
+            hu, hi, hr = (np.concatenate(x) for x in self._hist)
+            fresh = Context(self._params)
+            for _ in range(self.iterations):
+                fresh.online_update(hu, hi, hr, L.ONLINE_SPARK_SWEEP, self.P)
+            self.ctx.close()
+            self.ctx = fresh
+            users, items = np.unique(hu), np.unique(hi)
+        uv, _ = self.ctx.lookup(L.SIDE_USER, users)
+        iv, _ = self.ctx.lookup(L.SIDE_ITEM, items)
+        if checkpoint and self.snapshot_dir:
+            self.ctx.save(os.path.join(self.snapshot_dir, f"model_{self._batches:06d}.mfsnap"))
+        return ({int(a): v for a, v in zip(users, uv)}, {int(a): v for a, v in zip(items, iv)}, offline)

@@ -1,4 +1,6 @@
 """Online micro-batch path on the GPU vs the oracle (SGDUpdater arithmetic, bit-exact in f64)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -70,3 +72,36 @@ def test_online_on_top_of_offline_model():
     ids, vecs = ctx.factors(1)
     assert np.array_equal(vecs, np.array([items[x] for x in ids.tolist()]))
     ctx.close()
+
+
+@pytest.mark.gpu
+def test_combined_offline_online_matches_oracle(tmp_path):
+    """OnlineSpark.buildModelCombineOffline (sp/OnlineSpark.scala:26-162): online Spark sweeps per
+    micro-batch, a from-scratch offlineDSGD over the whole history every offline_every-th batch;
+    bit-exact against the oracle's composition of the same sweeps, snapshots written on schedule."""
+    from mfhip import synth
+    from mfhip.combined import OnlineOfflineSpark
+    d = synth.generate(120, 60, 1800, seed=9)
+    batches = [(d.u[x:x + 200], d.i[x:x + 200], d.r[x:x + 200]) for x in range(0, 1800, 200)]
+    k, lr, P, every, iters = 6, 0.01, 3, 4, 3
+    m = OnlineOfflineSpark(k, lr, num_partitions=P, offline_every=every, checkpoint_every=5, iterations=iters,
+                           snapshot_dir=str(tmp_path))
+    users, items, hist = {}, {}, []
+    for b, (u, i, r) in enumerate(batches, start=1):
+        rs = list(zip(u.tolist(), i.tolist(), r.tolist()))
+        hist += rs
+        uu, iu, offline = m.process(u, i, r)
+        assert offline == (b % every == 0)
+        if offline:
+            users, items = {}, {}
+            O.spark_sweep(hist, users, items, k, lr, P, iters)
+            assert set(uu) == set(users) and set(iu) == set(items)
+        else:
+            O.spark_sweep(rs, users, items, k, lr, P, 1)
+            assert set(uu) == set(u.tolist()) and set(iu) == set(i.tolist())
+        for x, v in uu.items():
+            assert np.array_equal(v, np.array(users[x])), (b, "user", x)
+        for x, v in iu.items():
+            assert np.array_equal(v, np.array(items[x])), (b, "item", x)
+    assert sorted(os.listdir(tmp_path)) == ["model_000005.mfsnap"]
+    m.close()
