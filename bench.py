@@ -128,6 +128,7 @@ def main():
     data = synth.generate(max(1, int(nu * a.scale)), max(1, int(ni * a.scale)), max(1, int(nr * a.scale)))
     (tu, ti, tr), (eu, ei, er) = data.split()
     t_gen = time.time() - t0
+    print(f"[bench] rank {D.rank}: generated {len(tr)} training ratings in {t_gen:.1f} s", file=sys.stderr, flush=True)
 
     p = L.default_params()
     p.num_factors, p.num_blocks, p.seed, p.has_seed = k, nb, 0, 1
@@ -145,6 +146,7 @@ def main():
     ctx.prepare(tu, ti, tr)
     ctx.sync()
     t_prep = time.time() - t0
+    print(f"[bench] rank {D.rank}: prepared (blocking, plan, H2D) in {t_prep:.1f} s", file=sys.stderr, flush=True)
 
     ctx.run(a.warmup * nb)
     ctx.sync()
