@@ -191,7 +191,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
         if (c * CH + s >= npairs) goto run_done;
         const int slot = s % D;
         const uint32_t fl = rl(C0.flags, s);
-        const float kfa = (fl & kPairFwdA) ? 1.f : 0.f, kfb = (fl & kPairFwdB) ? 1.f : 0.f;
+        const float kfa = static_cast<float>(fl & 0xFFu), kfb = static_cast<float>((fl >> 8) & 0xFFu);
         Row<KPL> pa;
         const Row<KPL> pb = RB[slot];
 #pragma unroll
@@ -247,8 +247,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
         if (c * CH + s >= npairs) goto done;
         const int slot = s % D;
         const uint32_t fl = rl(C0.flags, s);
-        const float kfa = (fl & kPairFwdA) ? 1.f : 0.f, kfb = (fl & kPairFwdB) ? 1.f : 0.f;
-        const float kq = (fl & kPairKeepQ) ? 1.f : 0.f, sr = (fl & kPairSplit) ? 0.f : 1.f;
+        // byte flags -> float coefficients (v_cvt_f32_ubyteN): forwarding, keep q, split
+        const float kfa = static_cast<float>(fl & 0xFFu), kfb = static_cast<float>((fl >> 8) & 0xFFu);
+        const float kq = static_cast<float>((fl >> 16) & 0xFFu), sp = static_cast<float>(fl >> 24);
+        const float sr = 1.f - sp;
         Row<KPL> pa, pb, qa, qbd;
 #pragma unroll
         for (int e = 0; e < NV; ++e) {
@@ -262,7 +264,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
         const float era = rlf(C0.era, s), erb = rlf(C0.erb, s);
         const float aa = rlf(C0.aa, s), ab = rlf(C0.ab, s), ba = rlf(C0.ba, s), bb = rlf(C0.bb, s);
         const float wa = fmaf(-eta, c1, era);
-        const float m = (fl & kPairSplit) ? 1.f : aa, gw = (fl & kPairSplit) ? 0.f : wa;
+        const float m = fmaf(sr, aa - 1.f, 1.f), gw = sr * wa;  // split: no coupling to A's update
         const float wb = fmaf(-eta, fmaf(gw, g, m * c2), erb);
         Row<KPL> q1;
 #pragma unroll

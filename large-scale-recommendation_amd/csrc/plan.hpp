@@ -138,10 +138,12 @@ struct WaveDesc {
 // or the record is a no-op) / no store.
 constexpr int kPairRing = 7;    // pairs prefetched ahead: 8 VMEM ops per pair, vmcnt <= 63
 constexpr int kPairChunk = 56;  // pair records per register chunk (a multiple of kPairRing)
-constexpr uint32_t kPairFwdA = 1u;   // A's user row = previous pair's A result (registers)
-constexpr uint32_t kPairFwdB = 2u;   // A's user row = previous pair's B result
-constexpr uint32_t kPairKeepQ = 4u;  // A continues the item row held in registers
-constexpr uint32_t kPairSplit = 8u;  // B's item differs from A's (B starts a run)
+// Flags are one byte each (0 or 1), so the kernel turns each into a float coefficient with a
+// single v_cvt_f32_ubyteN.
+constexpr uint32_t kPairFwdA = 1u << 0;    // A's user row = previous pair's A result (registers)
+constexpr uint32_t kPairFwdB = 1u << 8;    // A's user row = previous pair's B result
+constexpr uint32_t kPairKeepQ = 1u << 16;  // A continues the item row held in registers
+constexpr uint32_t kPairSplit = 1u << 24;  // B's item differs from A's (B starts a run)
 constexpr int32_t kWaveGeneric = 1;    // WaveDesc.cells: generic pair steps
 constexpr int32_t kWaveSingleRun = 2;  // the cell is one item run: no item traffic per pair
 struct PairRec {
