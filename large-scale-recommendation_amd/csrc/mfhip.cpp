@@ -14,6 +14,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -586,17 +587,32 @@ void reset_item_loc(mf_ctx* ctx) {
       }
 }
 
+// MFHIP_TIMING=1: host phases of prepare on stderr.
+struct PhaseClock {
+  bool on = std::getenv("MFHIP_TIMING") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void lap(const char* what) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[mfhip] %-28s %8.3f s\n", what, std::chrono::duration<double>(now - t).count());
+    t = now;
+  }
+};
+
 void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, int64_t n) {
   MF_REQUIRE(n >= 0, "negative rating count");
   MF_REQUIRE(n == 0 || (u && i && r), "null rating arrays");
   sync_all(ctx);
+  PhaseClock clk;
   ctx->nb = std::max(1, ctx->P.num_blocks);
   MF_REQUIRE(ctx->nb % ctx->G == 0, "num_blocks must be a multiple of the device count");
   ctx->c = ctx->nb / ctx->G;
   build_model(ctx, u, i, n);
+  clk.lap("blocking + factor init + H2D");
   int32_t lo = 0, hi = ctx->nb;
   if (ctx->rank_mode) { lo = ctx->shards[0].index * ctx->c; hi = lo + ctx->c; }
   build_rating_blocks(ctx->rb, ctx->U, ctx->I, u, i, r, n, lo, hi, ctx->f64 && ctx->P.has_seed);
+  clk.lap("rating blocks");
   const int64_t nb2 = static_cast<int64_t>(ctx->nb) * ctx->nb;
   if (!ctx->f64) {
     const int64_t local = ctx->rb.start[nb2];
@@ -615,6 +631,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
                     static_cast<uint64_t>(ctx->P.seed) * 0x9E3779B97F4A7C15ULL + 1, dummy, nullptr,
                     ctx->fast_pair ? 2 * kPairRing : kHazardWindow);
     ctx->stats.pads = fp.pads;
+    clk.lap("cell plan");
     {  // priority threshold: 3x the mean non-empty cell length
       int64_t cells = 0, recs = 0;
       for (int64_t b = 0; b < nb2; ++b)
@@ -649,6 +666,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
         if (!pp.waves.empty())
           MF_HIP(hipMemcpy(s.st_waves.get(), pp.waves.data(), pp.waves.size() * sizeof(WaveDesc), hipMemcpyHostToDevice));
         s.st_sub_off = std::move(pp.sub_off);
+        clk.lap("pair plan + H2D");
         if (std::getenv("MFHIP_WAVE_TRACE")) {
           s.st_trace.alloc(std::max<size_t>(pp.waves.size(), 1) * 16);
           MF_HIP(hipMemset(s.st_trace.get(), 0, std::max<size_t>(pp.waves.size(), 1) * 16));
