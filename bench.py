@@ -85,9 +85,9 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def pmc_traffic(a, k, groups):
+def pmc_traffic(a, k, groups, kernel):
     """HBM bytes per launch of the dominant kernel from a committed rocprofv3 --pmc summary
-    (tools/pmc_summary.py) of the same workload, or (None, None)."""
+    (tools/pmc_summary.py) of the same workload and kernel, or (None, None)."""
     import glob
     paths = [a.traffic_json] if a.traffic_json else sorted(
         glob.glob(os.path.join(ROOT, "profiles", f"r*_traffic_{a.config}_{a.mode}.json")))
@@ -95,7 +95,7 @@ def pmc_traffic(a, k, groups):
         if not path or not os.path.exists(path):
             continue
         rec = json.load(open(path))
-        if rec.get("rank") == k and rec.get("groups") in (groups, 0) and a.scale == 1.0:
+        if rec.get("rank") == k and rec.get("groups") in (groups, 0) and rec.get("kernel") == kernel and a.scale == 1.0:
             return rec["bytes_per_launch"], os.path.relpath(path, ROOT)
     return None, None
 
@@ -191,8 +191,8 @@ def main():
     if st_p["kernel_ms"] > 0:
         launches = st_p["kernel_launches"]
         achieved = st_p["algorithmic_bytes"] / (st_p["kernel_ms"] / 1e3) / 1e9  # GB/s, this rank's sweep kernel
-        traffic, traffic_src = pmc_traffic(a, k, st["groups"])
         kname = L.lib().mf_fast_kernel_name(k).decode() if a.mode == "fast" else "k_level"
+        traffic, traffic_src = pmc_traffic(a, k, st["groups"], kname)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kname,
                 "bytes_per_update": bpu, "avg_launch_us": round(st_p["kernel_ms"] * 1e3 / max(launches, 1), 2),

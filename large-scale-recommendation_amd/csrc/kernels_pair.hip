@@ -48,24 +48,27 @@ __device__ __forceinline__ float dpp(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
 }
 
-// Three 64-lane sums at once (interleaved butterflies), uniform results.
+__device__ __forceinline__ float u2f(uint32_t v) { return __uint_as_float(v); }
+__device__ __forceinline__ uint32_t f2u(float v) { return __float_as_uint(v); }
+
+// Three 64-lane sums at once, uniform results.  gfx950's half swaps fold the three values into
+// one register first (v_permlane32_swap: x | y halves; v_permlane16_swap: rows of x, z, y, z),
+// so only one 16-lane butterfly remains: 10 VALU operations instead of 18 interleaved DPP adds
+// (measured equal per step: a swap costs ~14 cycles against ~4.6 for an interleaved DPP add).
 __device__ __forceinline__ void wave_sum3(float& x, float& y, float& z) {
-  x += dpp<0xB1>(x); y += dpp<0xB1>(y); z += dpp<0xB1>(z);
-  x += dpp<0x4E>(x); y += dpp<0x4E>(y); z += dpp<0x4E>(z);
-  x += dpp<0x141>(x); y += dpp<0x141>(y); z += dpp<0x141>(z);
-  x += dpp<0x140>(x); y += dpp<0x140>(y); z += dpp<0x140>(z);
-  asm("v_add_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
-      "v_add_f32_dpp %1, %1, %1 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
-      "v_add_f32_dpp %2, %2, %2 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
-      "s_nop 0\n\t"
-      "v_add_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
-      "v_add_f32_dpp %1, %1, %1 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
-      "v_add_f32_dpp %2, %2, %2 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
-      "s_nop 1"
-      : "+v"(x), "+v"(y), "+v"(z));
-  x = rlf(x, 63);
-  y = rlf(y, 63);
-  z = rlf(z, 63);
+  const auto xy = __builtin_amdgcn_permlane32_swap(f2u(x), f2u(y), false, false);  // [x_lo y_lo], [x_hi y_hi]
+  const auto zz = __builtin_amdgcn_permlane32_swap(f2u(z), f2u(z), false, false);  // [z_lo z_lo], [z_hi z_hi]
+  const float v = u2f(xy[0]) + u2f(xy[1]);  // lanes 0-31: x halves summed, 32-63: y
+  const float w = u2f(zz[0]) + u2f(zz[1]);  // z halves summed (both halves)
+  const auto vw = __builtin_amdgcn_permlane16_swap(f2u(v), f2u(w), false, false);
+  float s = u2f(vw[0]) + u2f(vw[1]);  // row 0: x, row 1: z, row 2: y, row 3: z (16-lane partials)
+  s += dpp<0xB1>(s);
+  s += dpp<0x4E>(s);
+  s += dpp<0x141>(s);
+  s += dpp<0x140>(s);
+  x = rlf(s, 0);
+  z = rlf(s, 16);
+  y = rlf(s, 32);
 }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t raw_rsrc(const void* base, uint64_t bytes) {
@@ -80,18 +83,23 @@ struct Row {
   f2 v[NV];
 };
 
-template <int KPL>
+// Cache policy of a row access: 0 = plain; kSC1 = sc1 (L1 bypass on loads, write-through and
+// dropped from the XCD's L2 on stores), used for user rows handed between waves of the
+// systolic sweep (MI355X_MICROARCH.md, inter-workgroup visibility, valid forms).
+constexpr int kSC1 = 16;
+
+template <int KPL, int POL = 0>
 __device__ __forceinline__ Row<KPL> ld(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t off) {
   Row<KPL> r;
   if constexpr (KPL == 1) {
-    r.v[0] = f2{__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, voff, off, 0)), 0.f};
+    r.v[0] = f2{__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, voff, off, POL)), 0.f};
   } else if constexpr (KPL == 2) {
-    const auto x = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, off, 0);
+    const auto x = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, off, POL);
     r.v[0] = f2{__uint_as_float(x[0]), __uint_as_float(x[1])};
   } else {
 #pragma unroll
     for (int c = 0; c < KPL / 4; ++c) {
-      const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 16u * c, off, 0);
+      const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 16u * c, off, POL);
       r.v[2 * c] = f2{__uint_as_float(x[0]), __uint_as_float(x[1])};
       r.v[2 * c + 1] = f2{__uint_as_float(x[2]), __uint_as_float(x[3])};
     }
@@ -99,19 +107,19 @@ __device__ __forceinline__ Row<KPL> ld(__amdgpu_buffer_rsrc_t rs, uint32_t voff,
   return r;
 }
 
-template <int KPL>
+template <int KPL, int POL = 0>
 __device__ __forceinline__ void st(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t off, const Row<KPL>& r) {
   if constexpr (KPL == 1) {
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.v[0].x), rs, voff, off, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.v[0].x), rs, voff, off, POL);
   } else if constexpr (KPL == 2) {
     using u2 = uint32_t __attribute__((ext_vector_type(2)));
-    __builtin_amdgcn_raw_buffer_store_b64(u2{__float_as_uint(r.v[0].x), __float_as_uint(r.v[0].y)}, rs, voff, off, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(u2{__float_as_uint(r.v[0].x), __float_as_uint(r.v[0].y)}, rs, voff, off, POL);
   } else {
 #pragma unroll
     for (int c = 0; c < KPL / 4; ++c)
       __builtin_amdgcn_raw_buffer_store_b128(u4v{__float_as_uint(r.v[2 * c].x), __float_as_uint(r.v[2 * c].y),
                                                  __float_as_uint(r.v[2 * c + 1].x), __float_as_uint(r.v[2 * c + 1].y)},
-                                             rs, voff + 16u * c, off, 0);
+                                             rs, voff + 16u * c, off, POL);
   }
 }
 
@@ -132,40 +140,55 @@ struct Chunk {
   float aa, ab, ba, bb;     // 1 - eta * ri, 1 - eta * ru (1 for no-op records)
 };
 
-__device__ __forceinline__ void chunk_load(const u4v* __restrict__ R, int c, int npairs, int lane, float eta, Chunk& ch) {
+// A chunk's records as loaded (raw words, one pair per lane).  The next chunk is loaded a whole
+// chunk ahead and only converted (eta folded in) when it becomes current, so nothing reads a
+// just-loaded register at the chunk boundary and the factor-row ring keeps running across it
+// (converting at load time made every chunk boundary wait for its own record loads).
+// s_waitcnt vmcnt(0) the compiler can see (gfx9 encoding: expcnt 7, lgkmcnt 15).  Issued once
+// after a wave's initial prefetch: otherwise the loop header inherits the preheader's "just
+// loaded" ring rows and the compiler drains the ring at EVERY chunk boundary (vmcnt(0) in the
+// header, i.e. once per 56 pairs).
+__device__ __forceinline__ void drain_vmem() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
+struct ChunkRaw {
+  u4v w0, w1, w2, w3;
+};
+
+__device__ __forceinline__ ChunkRaw chunk_load(const u4v* __restrict__ R, int c, int npairs, int lane) {
   const int64_t x = min(c * kPairChunk + lane, npairs - 1);
   // records are read once: non-temporal, so they do not push factor rows out of L2 / MALL
-  const u4v w0 = __builtin_nontemporal_load(R + 4 * x), w1 = __builtin_nontemporal_load(R + 4 * x + 1);
-  const u4v w2 = __builtin_nontemporal_load(R + 4 * x + 2), w3 = __builtin_nontemporal_load(R + 4 * x + 3);
-  ch.ua = w0[0]; ch.ub = w0[1]; ch.ia = w0[2]; ch.ib = w0[3];
-  ch.sa = w1[0]; ch.sb = w1[1]; ch.sia = w1[2]; ch.si = w1[3];
-  ch.flags = w2[0];
-  ch.era = eta * __uint_as_float(w2[1]);
-  ch.erb = eta * __uint_as_float(w2[2]);
-  ch.ba = fmaf(-eta, __uint_as_float(w2[3]), 1.f);
-  ch.bb = fmaf(-eta, __uint_as_float(w3[0]), 1.f);
-  ch.aa = fmaf(-eta, __uint_as_float(w3[1]), 1.f);
-  ch.ab = fmaf(-eta, __uint_as_float(w3[2]), 1.f);
+  return ChunkRaw{__builtin_nontemporal_load(R + 4 * x), __builtin_nontemporal_load(R + 4 * x + 1),
+                  __builtin_nontemporal_load(R + 4 * x + 2), __builtin_nontemporal_load(R + 4 * x + 3)};
 }
 
-template <int KPL, int D>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_sweep_pair(
-    const WaveDesc* __restrict__ waves, const u4v* __restrict__ recs, float* __restrict__ U, float* __restrict__ I,
-    uint64_t u_bytes, uint64_t i_bytes, float eta, uint64_t* __restrict__ trace) {
+__device__ __forceinline__ Chunk chunk_convert(const ChunkRaw& r, float eta) {
+  Chunk ch;
+  ch.ua = r.w0[0]; ch.ub = r.w0[1]; ch.ia = r.w0[2]; ch.ib = r.w0[3];
+  ch.sa = r.w1[0]; ch.sb = r.w1[1]; ch.sia = r.w1[2]; ch.si = r.w1[3];
+  ch.flags = r.w2[0];
+  ch.era = eta * __uint_as_float(r.w2[1]);
+  ch.erb = eta * __uint_as_float(r.w2[2]);
+  ch.ba = fmaf(-eta, __uint_as_float(r.w2[3]), 1.f);
+  ch.bb = fmaf(-eta, __uint_as_float(r.w3[0]), 1.f);
+  ch.aa = fmaf(-eta, __uint_as_float(r.w3[1]), 1.f);
+  ch.ab = fmaf(-eta, __uint_as_float(r.w3[2]), 1.f);
+  return ch;
+}
+
+// One cell (WaveDesc d) of the pair schedule, swept by the calling wave.  UP = cache policy of
+// the user-row loads and stores.
+template <int KPL, int D, int UP>
+__device__ __forceinline__ void pair_cell(const WaveDesc d, const u4v* __restrict__ recs, __amdgpu_buffer_rsrc_t urs,
+                                          __amdgpu_buffer_rsrc_t irs, float eta, int lane) {
   constexpr int NV = Row<KPL>::NV;
   constexpr int CH = kPairChunk;
   static_assert(CH % D == 0, "ring slots must repeat every chunk");
-  const int lane = threadIdx.x;
-  const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-  const WaveDesc d = waves[blockIdx.x];
   const int npairs = d.steps;
   const u4v* R = recs + 4 * d.base;
   const uint32_t voff = static_cast<uint32_t>(lane) * KPL * 4u;
-  const __amdgpu_buffer_rsrc_t urs = raw_rsrc(U, u_bytes), irs = raw_rsrc(I, i_bytes);
 
-  Chunk C0, C1;  // current and next chunk
-  chunk_load(R, 0, npairs, lane, eta, C0);
-  chunk_load(R, 1, npairs, lane, eta, C1);
+  Chunk C0 = chunk_convert(chunk_load(R, 0, npairs, lane), eta);  // current chunk
+  ChunkRaw C1 = chunk_load(R, 1, npairs, lane);                     // next chunk, as loaded
   Row<KPL> plA, plB;  // the previous pair's updated user rows (forwarding)
 #pragma unroll
   for (int e = 0; e < NV; ++e) plA.v[e] = plB.v[e] = f2{0.f, 0.f};
@@ -177,19 +200,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     // pair (a user rating the item twice in a row).
     const uint32_t item_off = rl(C0.ia, 0);
     Row<KPL> q = ld<KPL>(irs, voff, item_off);
-    Row<KPL> RA[D], RB[D];
-    uint32_t ob[D];
+    constexpr int DS = kPairRingSingle;  // 4 VMEM ops per pair: a deeper ring than the generic path
+    Row<KPL> RA[DS], RB[DS];
+    uint32_t ob[DS];
 #pragma unroll
-    for (int s = 0; s < D; ++s) {
+    for (int s = 0; s < DS; ++s) {
       ob[s] = rl(C0.ub, s);
-      RA[s] = ld<KPL>(urs, voff, rl(C0.ua, s));
-      RB[s] = ld<KPL>(urs, voff, ob[s]);
+      RA[s] = ld<KPL, UP>(urs, voff, rl(C0.ua, s));
+      RB[s] = ld<KPL, UP>(urs, voff, ob[s]);
     }
+    drain_vmem();
     for (int c = 0;; ++c) {
 #pragma unroll
       for (int s = 0; s < CH; ++s) {
         if (c * CH + s >= npairs) goto run_done;
-        const int slot = s % D;
+        const int slot = s % DS;
         const uint32_t fl = rl(C0.flags, s);
         const float kfa = static_cast<float>(fl & 0xFFu), kfb = static_cast<float>((fl >> 8) & 0xFFu);
         Row<KPL> pa;
@@ -210,33 +235,34 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
           plB.v[e] = bb * b0 + wb * q1;
           q.v[e] = ab * q1 + wb * b0;
         }
-        st<KPL>(urs, voff, rl(C0.sa, s), plA);
-        st<KPL>(urs, voff, ob[slot], plB);
+        st<KPL, UP>(urs, voff, rl(C0.sa, s), plA);
+        st<KPL, UP>(urs, voff, ob[slot], plB);
         uint32_t oa;
-        if (s + D < CH) { oa = rl(C0.ua, s + D); ob[slot] = rl(C0.ub, s + D); }
-        else { oa = rl(C1.ua, s + D - CH); ob[slot] = rl(C1.ub, s + D - CH); }
-        RA[slot] = ld<KPL>(urs, voff, oa);
-        RB[slot] = ld<KPL>(urs, voff, ob[slot]);
+        if (s + DS < CH) { oa = rl(C0.ua, s + DS); ob[slot] = rl(C0.ub, s + DS); }
+        else { oa = rl(C1.w0[0], s + DS - CH); ob[slot] = rl(C1.w0[1], s + DS - CH); }
+        RA[slot] = ld<KPL, UP>(urs, voff, oa);
+        RB[slot] = ld<KPL, UP>(urs, voff, ob[slot]);
       }
-      C0 = C1;
-      chunk_load(R, c + 2, npairs, lane, eta, C1);
+      C0 = chunk_convert(C1, eta);
+      C1 = chunk_load(R, c + 2, npairs, lane);
     }
   run_done:
     st<KPL>(irs, voff, item_off, q);
-    goto done;
+    return;
   }
 
   {
     Row<KPL> PA[D], PB[D], QA[D], QB[D];
-#define MF_PREFETCH(slot, CHK, YY)                                              \
+#define MF_PREFETCH(slot, UA, UB, IA, IB, YY)                                   \
     do {                                                                        \
-      PA[slot] = ld<KPL>(urs, voff, rl(CHK.ua, (YY)));                          \
-      PB[slot] = ld<KPL>(urs, voff, rl(CHK.ub, (YY)));                          \
-      QA[slot] = ld<KPL>(irs, voff, rl(CHK.ia, (YY)));                          \
-      QB[slot] = ld<KPL>(irs, voff, rl(CHK.ib, (YY)));                          \
+      PA[slot] = ld<KPL, UP>(urs, voff, rl(UA, (YY)));                              \
+      PB[slot] = ld<KPL, UP>(urs, voff, rl(UB, (YY)));                              \
+      QA[slot] = ld<KPL>(irs, voff, rl(IA, (YY)));                              \
+      QB[slot] = ld<KPL>(irs, voff, rl(IB, (YY)));                              \
     } while (0)
 #pragma unroll
-    for (int s = 0; s < D; ++s) MF_PREFETCH(s, C0, s);
+    for (int s = 0; s < D; ++s) MF_PREFETCH(s, C0.ua, C0.ub, C0.ia, C0.ib, s);
+    drain_vmem();
     Row<KPL> q;
 #pragma unroll
     for (int e = 0; e < NV; ++e) q.v[e] = f2{0.f, 0.f};
@@ -244,7 +270,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     for (int c = 0;; ++c) {
 #pragma unroll
       for (int s = 0; s < CH; ++s) {
-        if (c * CH + s >= npairs) goto done;
+        if (c * CH + s >= npairs) return;
         const int slot = s % D;
         const uint32_t fl = rl(C0.flags, s);
         // byte flags -> float coefficients (v_cvt_f32_ubyteN): forwarding, keep q, split
@@ -276,23 +302,87 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
           plB.v[e] = bb * b0 + wb * qb0;
           q.v[e] = ab * qb0 + wb * b0;
         }
-        st<KPL>(urs, voff, rl(C0.sa, s), plA);
-        st<KPL>(urs, voff, rl(C0.sb, s), plB);
+        st<KPL, UP>(urs, voff, rl(C0.sa, s), plA);
+        st<KPL, UP>(urs, voff, rl(C0.sb, s), plB);
         st<KPL>(irs, voff, rl(C0.sia, s), q1);
         st<KPL>(irs, voff, rl(C0.si, s), q);
         // rows of pair j+D (after this pair's stores)
-        if (s + D < CH) MF_PREFETCH(slot, C0, s + D);
-        else MF_PREFETCH(slot, C1, s + D - CH);
+        if (s + D < CH) MF_PREFETCH(slot, C0.ua, C0.ub, C0.ia, C0.ib, s + D);
+        else MF_PREFETCH(slot, C1.w0[0], C1.w0[1], C1.w0[2], C1.w0[3], s + D - CH);
       }
-      C0 = C1;
-      chunk_load(R, c + 2, npairs, lane, eta, C1);
+      C0 = chunk_convert(C1, eta);
+      C1 = chunk_load(R, c + 2, npairs, lane);
     }
 #undef MF_PREFETCH
   }
-done:
-  if (trace && lane == 0) {
+}
+
+// One launch per sub-step: wave = cell (waves[] of the sub-step, longest first).
+template <int KPL, int D>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_sweep_pair(
+    const WaveDesc* __restrict__ waves, const u4v* __restrict__ recs, float* __restrict__ U, float* __restrict__ I,
+    uint64_t u_bytes, uint64_t i_bytes, float eta, uint64_t* __restrict__ trace) {
+  const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+  pair_cell<KPL, D, 0>(waves[blockIdx.x], recs, raw_rsrc(U, u_bytes), raw_rsrc(I, i_bytes), eta, threadIdx.x);
+  if (trace && threadIdx.x == 0) {
     trace[2 * blockIdx.x] = t_start;
     trace[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+  }
+}
+
+// One persistent launch per superstep (systolic rotation).  Wave (j, g) sweeps the G cells of
+// item group g of local rating block j in sub-step order; before cell t it waits until wave
+// (j, g+1) has finished cell t-1, the only earlier user of user group (g+t) mod G in this
+// superstep (item group g is this wave's alone).  So a sub-step is no longer a grid-wide
+// barrier: each cell starts when its two predecessors are done, and a long cell delays only
+// the waves downstream of it.  Hand-off (MI355X_MICROARCH.md, valid forms, row 1): every
+// user-row store and load is sc1, the wave drains its stores (vmcnt(0)), then lane 0 stores
+// the progress word (agent-scope relaxed atomic = sc1 store); the consumer polls it with
+// agent-scope relaxed loads (sc1).  Progress words are monotonic across launches (base), so
+// they are never reset.  Every wave must be resident at once (the host checks occupancy); a
+// poll that exceeds ~1 s sets err[0] and the wave gives up (the host then fails loudly).
+template <int KPL, int D>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_sweep_pair_sys(
+    const WaveDesc* __restrict__ sys, int G, int nw, const u4v* __restrict__ recs, float* __restrict__ U,
+    float* __restrict__ I, uint64_t u_bytes, uint64_t i_bytes, float eta, int32_t* __restrict__ prog, uint32_t base,
+    int32_t* __restrict__ err, uint64_t* __restrict__ trace) {
+  const int lane = threadIdx.x;
+  // blocks b and b+8 share an XCD: give each XCD a contiguous range of (j, g), so most
+  // hand-offs (g+1 -> g) stay inside one L2 (speed only; correctness does not depend on it)
+  const int b = static_cast<int>(blockIdx.x);
+  const int L = (nw % 8 == 0) ? (b % 8) * (nw / 8) + b / 8 : b;
+  const int j = L / G, g = L % G;
+  const WaveDesc* my = sys + static_cast<int64_t>(L) * G;
+  int32_t* my_prog = prog + static_cast<int64_t>(L) * kProgStride;
+  int32_t* nb_prog = prog + static_cast<int64_t>(j * G + (g + 1 == G ? 0 : g + 1)) * kProgStride;
+  const __amdgpu_buffer_rsrc_t urs = raw_rsrc(U, u_bytes), irs = raw_rsrc(I, i_bytes);
+  for (int t = 0; t < G; ++t) {
+    const WaveDesc d = my[t];
+    if (t > 0 && G > 1) {
+      const uint32_t want = base + static_cast<uint32_t>(t);
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      for (;;) {
+        const uint32_t v = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(nb_prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+        if (static_cast<int32_t>(v - want) >= 0) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {  // 100 MHz clock: ~1 s
+          if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          return;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    const uint64_t c_start = __builtin_amdgcn_s_memrealtime();
+    if (d.steps > 0) pair_cell<KPL, D, kSC1>(d, recs, urs, irs, eta, lane);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): every user-row store of this wave has landed
+    if (lane == 0)
+      __hip_atomic_store(my_prog, static_cast<int32_t>(base + static_cast<uint32_t>(t) + 1u), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    if (trace && lane == 0) {
+      uint64_t* tr = trace + 2 * (static_cast<int64_t>(L) * G + t);
+      tr[0] = c_start;
+      tr[1] = __builtin_amdgcn_s_memrealtime();
+    }
   }
 }
 
@@ -304,9 +394,48 @@ void dispatch(hipStream_t st, const WaveDesc* waves, int nwaves, const PairRec* 
                         0, waves, reinterpret_cast<const u4v*>(recs), U, I, ub, ib, eta, trace);
 }
 
+template <int KPL>
+void dispatch_sys(hipStream_t st, const WaveDesc* sys, int G, int nw, const PairRec* recs, float* U, float* I,
+                  uint64_t ub, uint64_t ib, float eta, int32_t* prog, uint32_t base, int32_t* err, uint64_t* trace,
+                  hipEvent_t ev0, hipEvent_t ev1) {
+  hipExtLaunchKernelGGL((k_sweep_pair_sys<KPL, kPairRing>), dim3(static_cast<unsigned>(nw)), dim3(64), 0, st, ev0, ev1,
+                        0, sys, G, nw, reinterpret_cast<const u4v*>(recs), U, I, ub, ib, eta, prog, base, err, trace);
+}
+
+template <int KPL>
+int sys_capacity() {
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sweep_pair_sys<KPL, kPairRing>, 64, 0) != hipSuccess)
+    return 0;
+  return cus * per_cu;
+}
+
 }  // namespace
 
 bool pair_kernel_supports(int k) { return k == 64 || k == 128 || k == 256; }
+
+int sweep_pair_sys_capacity(int k) {
+  switch (k) {
+    case 64: return sys_capacity<1>();
+    case 128: return sys_capacity<2>();
+    case 256: return sys_capacity<4>();
+    default: return 0;
+  }
+}
+
+void launch_sweep_pair_sys(hipStream_t st, const WaveDesc* sys, int G, int nw, const PairRec* recs, float* U, float* I,
+                           uint64_t u_bytes, uint64_t i_bytes, int k, float eta, int32_t* prog, uint32_t base,
+                           int32_t* err, uint64_t* trace, hipEvent_t ev0, hipEvent_t ev1) {
+  if (nw <= 0) return;
+  switch (k) {
+    case 64: dispatch_sys<1>(st, sys, G, nw, recs, U, I, u_bytes, i_bytes, eta, prog, base, err, trace, ev0, ev1); break;
+    case 128: dispatch_sys<2>(st, sys, G, nw, recs, U, I, u_bytes, i_bytes, eta, prog, base, err, trace, ev0, ev1); break;
+    case 256: dispatch_sys<4>(st, sys, G, nw, recs, U, I, u_bytes, i_bytes, eta, prog, base, err, trace, ev0, ev1); break;
+    default: break;
+  }
+}
 
 
 void launch_sweep_pair(hipStream_t st, const WaveDesc* waves, int nwaves, const PairRec* recs, float* U, float* I,

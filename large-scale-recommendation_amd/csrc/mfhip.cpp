@@ -65,6 +65,9 @@ struct Shard {
   DevBuf st_recs, st_waves;    // stream schedule (kernels_stream.hip)
   std::vector<int64_t> st_sub_off;
   std::vector<WaveDesc> st_waves_host;  // kept only when tracing
+  DevBuf st_sys;                        // systolic pair table (PairPlan::sys)
+  std::vector<WaveDesc> st_sys_host;    // kept only when tracing
+  uint32_t sys_base = 0;                // progress-word base of the next systolic launch
   DevBuf st_trace;                      // MFHIP_WAVE_TRACE: {start, end} per wave
   // evaluation scratch
   DevBuf ev_u, ev_i, ev_r, ev_mult, ev_out, ev_part;
@@ -97,6 +100,7 @@ struct mf_ctx {
   int32_t fast_prio_len = 1 << 30;  // cells at least this long run at raised priority
   bool fast_persistent = false;  // MFHIP_FAST_KERNEL=persistent selects the systolic single launch
   bool fast_pair = false;         // two updates per step (kernels_pair.hip), k in {64, 128, 256}
+  bool fast_sys = false;          // pair cells as one systolic launch per superstep (k_sweep_pair_sys)
   std::vector<int64_t> fast_rb_size;  // per rating block (fast mode)
   mf_stats stats{};
   bool profiling = false;
@@ -114,6 +118,13 @@ enum class FastKernel { kPair, kCell, kPersistent };
 // Fast sweep kernel: pair (default where k is 64, 128 or 256; kernels_pair.hip) | cell (one
 // update per step, any k; kernels_fast.hip) | persistent (kernels_fast.hip, one launch per
 // superstep); MFHIP_FAST_KERNEL overrides.
+// Pair cells as one systolic launch per superstep (default; MFHIP_PAIR_SYS=0: one launch per
+// sub-step).  Falls back to per-sub-step launches when a superstep's waves cannot all be resident.
+bool want_pair_sys() {
+  const char* v = std::getenv("MFHIP_PAIR_SYS");
+  return v ? std::string(v) != "0" : true;
+}
+
 FastKernel choose_fast_kernel(int k) {
   const char* v = std::getenv("MFHIP_FAST_KERNEL");
   const std::string want = v ? v : "";
@@ -302,6 +313,21 @@ void dump_wave_trace(mf_ctx* ctx) {
   if (!path) return;
   FILE* f = nullptr;
   for (auto& s : ctx->shards) {
+    if (s.st_trace.get() && !s.st_sys_host.empty()) {  // systolic: one row per cell, wave = j*G + g
+      DeviceGuard g(s.device);
+      std::vector<uint64_t> tr(s.st_sys_host.size() * 2);
+      MF_HIP(hipMemcpy(tr.data(), s.st_trace.get(), tr.size() * 8, hipMemcpyDeviceToHost));
+      if (!f) f = std::fopen(path, "w");
+      if (!f) return;
+      const int64_t G = ctx->G_fast, per = static_cast<int64_t>(ctx->c) * G * G;
+      for (int64_t x = 0; x < static_cast<int64_t>(s.st_sys_host.size()); ++x) {
+        const int64_t sm = x / per, L = (x % per) / G, t = x % G;
+        std::fprintf(f, "%d %lld %lld %lld %d %d %llu %llu\n", s.index, (long long)sm, (long long)t, (long long)L,
+                     s.st_sys_host[x].steps, s.st_sys_host[x].cells, (unsigned long long)tr[2 * x],
+                     (unsigned long long)tr[2 * x + 1]);
+      }
+      continue;
+    }
     if (!s.st_trace.get() || s.st_waves_host.empty()) continue;
     DeviceGuard g(s.device);
     std::vector<uint64_t> tr(s.st_waves_host.size() * 2);
@@ -328,7 +354,7 @@ void sync_all(mf_ctx* ctx) {
       if (err) {
         MF_HIP(hipMemset(s.fast_err.get(), 0, sizeof(err)));
         fail(MF_ERR_TIMEOUT, "fast sweep: a wave waited > 1 s for its neighbour (workgroups not co-resident?); "
-                             "set MFHIP_FAST_KERNEL=substep");
+                             "set MFHIP_PAIR_SYS=0 (or MFHIP_FAST_KERNEL=cell)");
       }
     }
   }
@@ -461,7 +487,18 @@ void fast_superstep(mf_ctx* ctx, Shard& s, int64_t superstep, double eta) {
     ups += ctx->fast_rb_size[static_cast<int64_t>(p) * n + q];
   }
   if (ups == 0) return;
-  if (ctx->fast_pair) {
+  if (ctx->fast_pair && ctx->fast_sys) {
+    const int32_t G = ctx->G_fast;
+    const int64_t per = static_cast<int64_t>(ctx->c) * G * G;
+    LaunchTimer tm(s, ctx->profiling, true);
+    launch_sweep_pair_sys(s.stream, s.st_sys.as<WaveDesc>() + smod * per, G, ctx->c * G, s.st_recs.as<PairRec>(),
+                          s.uf.as<float>(), s.itf.as<float>(), s.uf.bytes(), s.itf.bytes(), ctx->P.num_factors,
+                          static_cast<float>(eta), s.fast_prog.as<int32_t>(), s.sys_base, s.fast_err.as<int32_t>(),
+                          s.st_trace.get() ? s.st_trace.as<uint64_t>() + 2 * smod * per : nullptr, tm.start(),
+                          tm.stop());
+    s.sys_base += static_cast<uint32_t>(G);
+    ctx->stats.kernel_launches += 1;
+  } else if (ctx->fast_pair) {
     for (int32_t t = 0; t < ctx->G_fast; ++t) {
       const int64_t x = smod * ctx->G_fast + t;
       const int64_t w0 = s.st_sub_off[x], nw = s.st_sub_off[x + 1] - w0;
@@ -627,6 +664,15 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
                "fast mode addresses each factor slab with 32-bit offsets (< 4 GiB)");
     const int k = ctx->P.num_factors;
     ctx->fast_pair = fk == FastKernel::kPair;
+    ctx->fast_sys = false;
+    if (ctx->fast_pair && want_pair_sys()) {  // every wave of a superstep must be resident at once
+      bool fits = true;
+      for (auto& s : ctx->shards) {
+        DeviceGuard g(s.device);
+        fits = fits && static_cast<int64_t>(ctx->c) * ctx->G_fast <= sweep_pair_sys_capacity(k);
+      }
+      ctx->fast_sys = fits;
+    }
     build_fast_plan(fp, ctx->rb, ctx->U, ctx->I, ctx->G_fast, k, ctx->P.lambda,
                     static_cast<uint64_t>(ctx->P.seed) * 0x9E3779B97F4A7C15ULL + 1, dummy, nullptr,
                     ctx->fast_pair ? 2 * kPairRing : kHazardWindow);
@@ -666,11 +712,23 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
         if (!pp.waves.empty())
           MF_HIP(hipMemcpy(s.st_waves.get(), pp.waves.data(), pp.waves.size() * sizeof(WaveDesc), hipMemcpyHostToDevice));
         s.st_sub_off = std::move(pp.sub_off);
+        s.st_sys_host.clear();
+        s.sys_base = 0;
+        if (ctx->fast_sys) {
+          s.st_sys.alloc(pp.sys.size() * sizeof(WaveDesc));
+          MF_HIP(hipMemcpy(s.st_sys.get(), pp.sys.data(), pp.sys.size() * sizeof(WaveDesc), hipMemcpyHostToDevice));
+          s.fast_prog.alloc(static_cast<size_t>(ctx->c) * ctx->G_fast * kProgStride * sizeof(int32_t));
+          MF_HIP(hipMemset(s.fast_prog.get(), 0, s.fast_prog.bytes()));
+          s.fast_err.alloc(16);
+          MF_HIP(hipMemset(s.fast_err.get(), 0, 16));
+        }
         clk.lap("pair plan + H2D");
         if (std::getenv("MFHIP_WAVE_TRACE")) {
-          s.st_trace.alloc(std::max<size_t>(pp.waves.size(), 1) * 16);
-          MF_HIP(hipMemset(s.st_trace.get(), 0, std::max<size_t>(pp.waves.size(), 1) * 16));
-          s.st_waves_host = pp.waves;
+          const size_t n = ctx->fast_sys ? pp.sys.size() : pp.waves.size();
+          s.st_trace.alloc(std::max<size_t>(n, 1) * 16);
+          MF_HIP(hipMemset(s.st_trace.get(), 0, std::max<size_t>(n, 1) * 16));
+          if (ctx->fast_sys) s.st_sys_host = pp.sys;
+          else s.st_waves_host = pp.waves;
         }
         continue;
       }
@@ -1430,7 +1488,7 @@ int mf_debug_fast_schedule(const int32_t* u, const int32_t* i, int64_t n, int32_
 
 const char* mf_fast_kernel_name(int32_t k) {
   switch (choose_fast_kernel(k)) {
-    case FastKernel::kPair: return "k_sweep_pair";
+    case FastKernel::kPair: return want_pair_sys() ? "k_sweep_pair_sys" : "k_sweep_pair";
     case FastKernel::kPersistent: return "k_fast_superstep";
     default: return "k_fast_substep";
   }

@@ -2,6 +2,7 @@
 #include "plan.hpp"
 
 #include <algorithm>
+#include <unordered_map>
 #include <atomic>
 #include <cmath>
 #include <numeric>
@@ -504,7 +505,7 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
 }
 
 namespace {
-struct SubCell { int32_t len; int64_t beg; };
+struct SubCell { int32_t len; int64_t beg; int32_t j, g; };
 // The non-empty cells of every sub-step (sm, t) of this shard's rating blocks, longest first.
 std::vector<std::vector<SubCell>> collect_subs(const FastPlan& fp, int32_t nb, int32_t c, int32_t shard) {
   using Cell = SubCell;
@@ -522,7 +523,7 @@ std::vector<std::vector<SubCell>> collect_subs(const FastPlan& fp, int32_t nb, i
       for (int32_t g = 0; g < G; ++g) {
         const int64_t cb = static_cast<int64_t>(t) * G + g;
         const int32_t len = off[cb + 1] - off[cb];
-        if (len > 0) cells.push_back(Cell{len, fp.rec_base[b] + off[cb]});
+        if (len > 0) cells.push_back(Cell{len, fp.rec_base[b] + off[cb], j, g});
       }
     }
     std::stable_sort(cells.begin(), cells.end(), [](const Cell& a, const Cell& b2) { return a.len > b2.len; });
@@ -630,10 +631,32 @@ void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, in
       for (const PairRec* r = first; single && r < out; ++r)
         single = !(r->flags & kPairSplit) && (r == first || (r->flags & kPairKeepQ)) && r->ub == r->sb &&
                  (r + 1 < out ? r->si == kOffOOB : r->si == first[0].ia);
+      // the lean path prefetches kPairRingSingle pairs ahead: a user row it loads must have
+      // been stored by an earlier pair at least that far back
+      if (single) {
+        std::unordered_map<uint32_t, int64_t> stored;
+        for (const PairRec* r = first; single && r < out; ++r) {
+          const int64_t j = r - first;
+          for (uint32_t off : {r->ua, r->ub}) {
+            if (off == kOffOOB) continue;
+            const auto it = stored.find(off);
+            if (it != stored.end() && j - it->second < kPairRingSingle) single = false;
+          }
+          if (r->sa != kOffOOB) stored[r->sa] = j;
+          if (r->sb != kOffOOB) stored[r->sb] = j;
+        }
+      }
       if (single) pp.waves[w_this].cells = kWaveSingleRun;
     }
   });
   for (int64_t x = 0; x < nsub; ++x) pp.noop_halves += noops[x];
+  const int64_t G = fp.G;
+  pp.sys.assign(static_cast<size_t>(nb) * c * G * G, WaveDesc{0, 0, kWaveGeneric});
+  for (int64_t x = 0; x < nsub; ++x) {
+    const int64_t sm = x / G, t = x % G;
+    int64_t w = pp.sub_off[x];
+    for (const Cell& cl : subs[x]) pp.sys[((sm * c + cl.j) * G + cl.g) * G + t] = pp.waves[w++];
+  }
 }
 
 }  // namespace mfhip

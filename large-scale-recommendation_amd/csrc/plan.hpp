@@ -138,6 +138,12 @@ struct WaveDesc {
 // or the record is a no-op) / no store.
 constexpr int kPairRing = 7;    // pairs prefetched ahead: 8 VMEM ops per pair, vmcnt <= 63
 constexpr int kPairChunk = 56;  // pair records per register chunk (a multiple of kPairRing)
+// Single-run waves (one item run, kWaveSingleRun) move only user rows (4 VMEM ops per pair) and
+// could run a ring twice as deep; 14 measured no faster than 7 (the step is not load-latency
+// bound), so they share kPairRing.  build_pair_plan checks that every user row such a wave
+// loads was last stored at least kPairRingSingle pairs earlier (or is forwarded in registers).
+constexpr int kPairRingSingle = kPairRing;
+static_assert(kPairChunk % kPairRing == 0 && kPairChunk % kPairRingSingle == 0, "ring slots must repeat every chunk");
 // Flags are one byte each (0 or 1), so the kernel turns each into a float coefficient with a
 // single v_cvt_f32_ubyteN.
 constexpr uint32_t kPairFwdA = 1u << 0;    // A's user row = previous pair's A result (registers)
@@ -158,6 +164,9 @@ struct PairPlan {
   std::vector<PairRec> recs;
   std::vector<WaveDesc> waves;   // one per non-empty cell (steps = pairs), every (sm, t), sm-major
   std::vector<int64_t> sub_off;  // nb*G + 1
+  // Systolic table (k_sweep_pair_sys): the cell of every (sm, local block j, item group g,
+  // sub-step t) at [((sm*c + j)*G + g)*G + t]; steps = 0 for an empty cell.
+  std::vector<WaveDesc> sys;
   int64_t noop_halves = 0;       // pair halves that are no-ops (planner padding, repeated users)
 };
 // The plan window must be >= 2 * kPairRing records.

@@ -261,3 +261,41 @@ def test_profiling_stats():
     assert st["updates"] == 50000 and st["supersteps"] == 2
     assert st["kernel_launches"] > 0 and st["kernel_ms"] > 0
     assert st["algorithmic_bytes"] == 50000 * (16 * 128 + 20)
+
+
+@pytest.mark.parametrize("k,nb,G,hot,n", [(64, 2, 8, False, 12000), (128, 3, 4, True, 12000), (256, 1, 8, True, 12000),
+                                          (64, 4, 0, False, 1_000_000), (128, 8, 0, True, 400_000)])
+def test_systolic_sweep_equals_substep_launches(monkeypatch, k, nb, G, hot, n):
+    """k_sweep_pair_sys (one launch per superstep, neighbour hand-offs through progress words and
+    sc1 user-row traffic) runs exactly the cells of the per-sub-step launches in the same order:
+    factors must be bitwise equal.  A stale user row read across a hand-off would break this."""
+    if hot:
+        d = hot_item_data(k)
+        if n > 20000:  # scale up: many users, one very hot item among a Zipf tail
+            big = synth.generate(n // 20, 2000, n, seed=k)
+            hu = np.arange(0, n // 20, 2, dtype=np.int32)
+            d.u = np.concatenate([big.u, hu])
+            d.i = np.concatenate([big.i, np.full(len(hu), 7, np.int32)])
+            d.r = np.concatenate([big.r, np.ones(len(hu))])
+    else:
+        d = synth.generate(max(400, n // 50), max(120, n // 300), n, seed=k)
+    outs = []
+    for sys_on in ("0", "1"):
+        monkeypatch.setenv("MFHIP_PAIR_SYS", sys_on)
+        with mfhip.Context(params(k, 2, nb, 3, mode=L.MODE_FAST_F32, fast_waves=-G if G else 0,
+                                  blocking=L.BLOCKING_REFERENCE)) as ctx:
+            ctx.fit(d.u, d.i, d.r)
+            outs.append((ctx.factors(0)[1], ctx.factors(1)[1], ctx.stats()["kernel_launches"]))
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+    assert outs[1][2] < outs[0][2]  # the systolic path really ran (one launch per superstep)
+
+
+def test_systolic_multi_shard_matches_single(monkeypatch):
+    monkeypatch.setenv("MFHIP_PAIR_SYS", "1")
+    d = synth.generate(2000, 500, 60000, seed=9)
+    outs = []
+    for devs in ([0], [0, 0]):
+        with mfhip.Context(params(64, 2, 4, 1, mode=L.MODE_FAST_F32, fast_waves=-8), devices=devs) as ctx:
+            ctx.fit(d.u, d.i, d.r)
+            outs.append((ctx.factors(0)[1], ctx.factors(1)[1]))
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])

@@ -16,8 +16,13 @@ import csv
 import json
 
 
+def kernel_match(name, kernel):
+    """rocprof kernel names are demangled signatures: match the template name exactly."""
+    return f"{kernel}<" in name or name.split("(")[0].endswith(kernel)
+
+
 def counter(path, kernel):
-    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path)) if kernel in r["Kernel_Name"]]
+    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path)) if kernel_match(r["Kernel_Name"], kernel)]
     return len(vals), (sum(vals) / len(vals) if vals else 0.0)
 
 
@@ -33,7 +38,7 @@ def main():
     ap.add_argument("--groups", type=int, default=0)
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
-    st = [r for r in csv.DictReader(open(a.stats)) if a.kernel in r["Name"]]
+    st = [r for r in csv.DictReader(open(a.stats)) if kernel_match(r["Name"], a.kernel)]
     assert st, f"kernel {a.kernel} not in {a.stats}"
     nf, fetch_kib = counter(a.fetch, a.kernel)
     nw, write_kib = counter(a.write, a.kernel)

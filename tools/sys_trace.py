@@ -1,0 +1,38 @@
+#!/usr/bin/env python3
+"""Summarise an MFHIP_WAVE_TRACE dump of the systolic pair sweep (rows: shard sm t wave steps kind
+start end, one per cell, 100 MHz): per-kind cell cost fit, the gaps between a wave's consecutive
+cells (neighbour wait + hand-off), and each superstep's span."""
+import sys
+
+import numpy as np
+
+a = np.loadtxt(sys.argv[1], dtype=np.int64)
+a = a[a[:, 6] > 0]
+dur = (a[:, 7] - a[:, 6]) * 10.0
+for kind in (1, 2):
+    m = (a[:, 5] == kind) & (a[:, 4] > 0)
+    if m.sum() < 10:
+        continue
+    A = np.stack([np.ones(m.sum()), a[m, 4]], 1)
+    coef, *_ = np.linalg.lstsq(A, dur[m], rcond=None)
+    print(f"kind {kind}: cells {m.sum()}, fixed {coef[0]:.0f} ns, per pair {coef[1]:.1f} ns, median pairs {np.median(a[m, 4]):.0f}")
+e = a[a[:, 4] == 0]
+print(f"empty cells {len(e)}, median duration {np.median((e[:, 7] - e[:, 6]) * 10.0) if len(e) else 0:.0f} ns")
+order = np.lexsort((a[:, 2], a[:, 3], a[:, 1], a[:, 0]))
+b = a[order]
+same = (b[1:, 0] == b[:-1, 0]) & (b[1:, 1] == b[:-1, 1]) & (b[1:, 3] == b[:-1, 3])
+gap = (b[1:, 6] - b[:-1, 7])[same] * 10.0
+print(f"gap between a wave's cells: median {np.median(gap):.0f} ns, p10 {np.percentile(gap, 10):.0f}, "
+      f"p90 {np.percentile(gap, 90):.0f}, mean {gap.mean():.0f}")
+tot = 0.0
+for sm in np.unique(a[:, 1]):
+    w = a[a[:, 1] == sm]
+    span = (w[:, 7].max() - w[:, 6].min()) * 10.0
+    busy = np.zeros(0)
+    tot += span
+    waves = np.unique(w[:, 3])
+    per_wave = [((w[w[:, 3] == x, 7] - w[w[:, 3] == x, 6]) * 10.0).sum() for x in waves]
+    xm = waves[int(np.argmax(per_wave))]
+    print(f"superstep {sm}: span {span / 1e3:.0f} us, busiest wave {xm} busy {max(per_wave) / 1e3:.0f} us "
+          f"({int(w[w[:, 3] == xm, 4].sum())} pairs), median wave busy {np.median(per_wave) / 1e3:.0f} us")
+print(f"sum of superstep spans {tot / 1e6:.2f} ms")
