@@ -213,7 +213,9 @@ int mf_learning_rate(int method, double lr, int32_t iteration, double lambda, do
    (order may be NULL = identity); rows are caller indices.
    mf_debug_fast_schedule: for every input rating, the rating block (ub*n+ib), rotation
    sub-step, item group and position inside its cell of the fast-mode plan with `groups`
-   groups per rating block, MF_BLOCKING_* `blocking` and hazard window `window` (0: 8). */
+   groups per rating block (groups < 0: the systolic sweep's per-block choice for a budget of
+   -groups waves per superstep, as mf_dsgd_prepare makes it with MFHIP_SYS_WAVES=-groups),
+   MF_BLOCKING_* `blocking` and hazard window `window` (0: 8). */
 int mf_debug_levels(const uint32_t* urow, const uint32_t* irow, const int32_t* order, int64_t n,
                     int32_t* level_out);
 int mf_debug_fast_schedule(const int32_t* users, const int32_t* items, int64_t n, int32_t n_blocks,

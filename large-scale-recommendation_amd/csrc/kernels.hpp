@@ -51,15 +51,16 @@ bool pair_kernel_supports(int k);
 void launch_sweep_pair(hipStream_t st, const WaveDesc* waves, int nwaves, const PairRec* recs, float* U, float* I,
                        uint64_t u_bytes, uint64_t i_bytes, int k, float eta, uint64_t* trace, hipEvent_t ev0,
                        hipEvent_t ev1);
-// Systolic variant, one launch per superstep: sys = PairPlan::sys of this superstep ([c][G][G]),
-// nw = c*G waves, all of which must be resident at once (nw <= sweep_pair_sys_capacity(k)).
-// prog: nw*kProgStride int32 progress words, monotonic across launches (this launch writes
-// base+1 .. base+G); err[0] is set when a wave gave up waiting.  trace (may be null): per cell
-// {start, end} at [2*(L*G + t)].
+// Systolic variant, one launch per superstep: sw = this superstep's PairPlan::sys_waves (nw of
+// them, all of which must be resident at once: nw <= sweep_pair_sys_capacity(k)), sys =
+// PairPlan::sys.  prog: nw*kProgStride int32 progress words, monotonic across launches (this
+// launch writes base+1 .. base+G_j and must advance base by more than the largest G_j);
+// err[0] is set when a wave gave up waiting.  trace (may be null): per cell {start, end} at
+// [2*(cell index in sys)].
 int sweep_pair_sys_capacity(int k);
-void launch_sweep_pair_sys(hipStream_t st, const WaveDesc* sys, int G, int nw, const PairRec* recs, float* U, float* I,
-                           uint64_t u_bytes, uint64_t i_bytes, int k, float eta, int32_t* prog, uint32_t base,
-                           int32_t* err, uint64_t* trace, hipEvent_t ev0, hipEvent_t ev1);
+void launch_sweep_pair_sys(hipStream_t st, const SysWave* sw, const WaveDesc* sys, int nw, const PairRec* recs,
+                           float* U, float* I, uint64_t u_bytes, uint64_t i_bytes, int k, float eta, int32_t* prog,
+                           uint32_t base, int32_t* err, uint64_t* trace, hipEvent_t ev0, hipEvent_t ev1);
 
 // Gather-dot over resolved pairs (row -1 = unknown id).  out[j] = p.q summed left to right in
 // f64 (predictRating's ddot).  When r != nullptr every workgroup writes partials[3*wg + c]:

@@ -330,10 +330,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   }
 }
 
-// One persistent launch per superstep (systolic rotation).  Wave (j, g) sweeps the G cells of
+// One persistent launch per superstep (systolic rotation).  Wave (j, g) sweeps the G_j cells of
 // item group g of local rating block j in sub-step order; before cell t it waits until wave
-// (j, g+1) has finished cell t-1, the only earlier user of user group (g+t) mod G in this
-// superstep (item group g is this wave's alone).  So a sub-step is no longer a grid-wide
+// (j, g+1) has finished cell t-1, the only earlier user of user group (g+t) mod G_j in this
+// superstep (item group g is this wave's alone).  Rating blocks are independent grids, each
+// with its own G_j (choose_block_groups).  So a sub-step is no longer a grid-wide
 // barrier: each cell starts when its two predecessors are done, and a long cell delays only
 // the waves downstream of it.  Hand-off (MI355X_MICROARCH.md, valid forms, row 1): every
 // user-row store and load is sc1, the wave drains its stores (vmcnt(0)), then lane 0 stores
@@ -343,22 +344,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
 // poll that exceeds ~1 s sets err[0] and the wave gives up (the host then fails loudly).
 template <int KPL, int D>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_sweep_pair_sys(
-    const WaveDesc* __restrict__ sys, int G, int nw, const u4v* __restrict__ recs, float* __restrict__ U,
-    float* __restrict__ I, uint64_t u_bytes, uint64_t i_bytes, float eta, int32_t* __restrict__ prog, uint32_t base,
-    int32_t* __restrict__ err, uint64_t* __restrict__ trace) {
+    const SysWave* __restrict__ sw, const WaveDesc* __restrict__ sys, int nw, const u4v* __restrict__ recs,
+    float* __restrict__ U, float* __restrict__ I, uint64_t u_bytes, uint64_t i_bytes, float eta,
+    int32_t* __restrict__ prog, uint32_t base, int32_t* __restrict__ err, uint64_t* __restrict__ trace) {
   const int lane = threadIdx.x;
-  // blocks b and b+8 share an XCD: give each XCD a contiguous range of (j, g), so most
-  // hand-offs (g+1 -> g) stay inside one L2 (speed only; correctness does not depend on it)
+  // blocks b and b+8 share an XCD: give each XCD a contiguous range of waves, so most hand-offs
+  // (g+1 -> g) stay inside one L2 (speed only; correctness does not depend on it)
   const int b = static_cast<int>(blockIdx.x);
   const int L = (nw % 8 == 0) ? (b % 8) * (nw / 8) + b / 8 : b;
-  const int j = L / G, g = L % G;
-  const WaveDesc* my = sys + static_cast<int64_t>(L) * G;
+  const SysWave w = sw[L];
+  const WaveDesc* my = sys + w.cell0;
   int32_t* my_prog = prog + static_cast<int64_t>(L) * kProgStride;
-  int32_t* nb_prog = prog + static_cast<int64_t>(j * G + (g + 1 == G ? 0 : g + 1)) * kProgStride;
+  int32_t* nb_prog = prog + static_cast<int64_t>(w.nbr) * kProgStride;
   const __amdgpu_buffer_rsrc_t urs = raw_rsrc(U, u_bytes), irs = raw_rsrc(I, i_bytes);
-  for (int t = 0; t < G; ++t) {
+  for (int t = 0; t < w.G; ++t) {
     const WaveDesc d = my[t];
-    if (t > 0 && G > 1) {
+    if (t > 0 && w.G > 1) {
       const uint32_t want = base + static_cast<uint32_t>(t);
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       for (;;) {
@@ -379,7 +380,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
       __hip_atomic_store(my_prog, static_cast<int32_t>(base + static_cast<uint32_t>(t) + 1u), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
     if (trace && lane == 0) {
-      uint64_t* tr = trace + 2 * (static_cast<int64_t>(L) * G + t);
+      uint64_t* tr = trace + 2 * (w.cell0 + t);
       tr[0] = c_start;
       tr[1] = __builtin_amdgcn_s_memrealtime();
     }
@@ -395,11 +396,11 @@ void dispatch(hipStream_t st, const WaveDesc* waves, int nwaves, const PairRec* 
 }
 
 template <int KPL>
-void dispatch_sys(hipStream_t st, const WaveDesc* sys, int G, int nw, const PairRec* recs, float* U, float* I,
-                  uint64_t ub, uint64_t ib, float eta, int32_t* prog, uint32_t base, int32_t* err, uint64_t* trace,
-                  hipEvent_t ev0, hipEvent_t ev1) {
+void dispatch_sys(hipStream_t st, const SysWave* sw, const WaveDesc* sys, int nw, const PairRec* recs, float* U,
+                  float* I, uint64_t ub, uint64_t ib, float eta, int32_t* prog, uint32_t base, int32_t* err,
+                  uint64_t* trace, hipEvent_t ev0, hipEvent_t ev1) {
   hipExtLaunchKernelGGL((k_sweep_pair_sys<KPL, kPairRing>), dim3(static_cast<unsigned>(nw)), dim3(64), 0, st, ev0, ev1,
-                        0, sys, G, nw, reinterpret_cast<const u4v*>(recs), U, I, ub, ib, eta, prog, base, err, trace);
+                        0, sw, sys, nw, reinterpret_cast<const u4v*>(recs), U, I, ub, ib, eta, prog, base, err, trace);
 }
 
 template <int KPL>
@@ -425,18 +426,17 @@ int sweep_pair_sys_capacity(int k) {
   }
 }
 
-void launch_sweep_pair_sys(hipStream_t st, const WaveDesc* sys, int G, int nw, const PairRec* recs, float* U, float* I,
-                           uint64_t u_bytes, uint64_t i_bytes, int k, float eta, int32_t* prog, uint32_t base,
-                           int32_t* err, uint64_t* trace, hipEvent_t ev0, hipEvent_t ev1) {
+void launch_sweep_pair_sys(hipStream_t st, const SysWave* sw, const WaveDesc* sys, int nw, const PairRec* recs,
+                           float* U, float* I, uint64_t u_bytes, uint64_t i_bytes, int k, float eta, int32_t* prog,
+                           uint32_t base, int32_t* err, uint64_t* trace, hipEvent_t ev0, hipEvent_t ev1) {
   if (nw <= 0) return;
   switch (k) {
-    case 64: dispatch_sys<1>(st, sys, G, nw, recs, U, I, u_bytes, i_bytes, eta, prog, base, err, trace, ev0, ev1); break;
-    case 128: dispatch_sys<2>(st, sys, G, nw, recs, U, I, u_bytes, i_bytes, eta, prog, base, err, trace, ev0, ev1); break;
-    case 256: dispatch_sys<4>(st, sys, G, nw, recs, U, I, u_bytes, i_bytes, eta, prog, base, err, trace, ev0, ev1); break;
+    case 64: dispatch_sys<1>(st, sw, sys, nw, recs, U, I, u_bytes, i_bytes, eta, prog, base, err, trace, ev0, ev1); break;
+    case 128: dispatch_sys<2>(st, sw, sys, nw, recs, U, I, u_bytes, i_bytes, eta, prog, base, err, trace, ev0, ev1); break;
+    case 256: dispatch_sys<4>(st, sw, sys, nw, recs, U, I, u_bytes, i_bytes, eta, prog, base, err, trace, ev0, ev1); break;
     default: break;
   }
 }
-
 
 void launch_sweep_pair(hipStream_t st, const WaveDesc* waves, int nwaves, const PairRec* recs, float* U, float* I,
                        uint64_t u_bytes, uint64_t i_bytes, int k, float eta, uint64_t* trace, hipEvent_t ev0,

@@ -65,9 +65,12 @@ struct Shard {
   DevBuf st_recs, st_waves;    // stream schedule (kernels_stream.hip)
   std::vector<int64_t> st_sub_off;
   std::vector<WaveDesc> st_waves_host;  // kept only when tracing
-  DevBuf st_sys;                        // systolic pair table (PairPlan::sys)
+  DevBuf st_sys, st_sysw;               // systolic pair tables (PairPlan::sys, sys_waves)
+  std::vector<int64_t> st_sys_off;      // PairPlan::sys_off
   std::vector<WaveDesc> st_sys_host;    // kept only when tracing
+  std::vector<SysWave> st_sysw_host;    // kept only when tracing
   uint32_t sys_base = 0;                // progress-word base of the next systolic launch
+  uint32_t sys_step = 1;                // base advance per launch (> the largest G_j)
   DevBuf st_trace;                      // MFHIP_WAVE_TRACE: {start, end} per wave
   // evaluation scratch
   DevBuf ev_u, ev_i, ev_r, ev_mult, ev_out, ev_part;
@@ -313,19 +316,22 @@ void dump_wave_trace(mf_ctx* ctx) {
   if (!path) return;
   FILE* f = nullptr;
   for (auto& s : ctx->shards) {
-    if (s.st_trace.get() && !s.st_sys_host.empty()) {  // systolic: one row per cell, wave = j*G + g
+    if (s.st_trace.get() && !s.st_sys_host.empty()) {  // systolic: one row per cell, wave = index in superstep
       DeviceGuard g(s.device);
       std::vector<uint64_t> tr(s.st_sys_host.size() * 2);
       MF_HIP(hipMemcpy(tr.data(), s.st_trace.get(), tr.size() * 8, hipMemcpyDeviceToHost));
       if (!f) f = std::fopen(path, "w");
       if (!f) return;
-      const int64_t G = ctx->G_fast, per = static_cast<int64_t>(ctx->c) * G * G;
-      for (int64_t x = 0; x < static_cast<int64_t>(s.st_sys_host.size()); ++x) {
-        const int64_t sm = x / per, L = (x % per) / G, t = x % G;
-        std::fprintf(f, "%d %lld %lld %lld %d %d %llu %llu\n", s.index, (long long)sm, (long long)t, (long long)L,
-                     s.st_sys_host[x].steps, s.st_sys_host[x].cells, (unsigned long long)tr[2 * x],
-                     (unsigned long long)tr[2 * x + 1]);
-      }
+      for (int32_t sm = 0; sm < ctx->nb; ++sm)
+        for (int64_t w = s.st_sys_off[sm]; w < s.st_sys_off[sm + 1]; ++w) {
+          const SysWave& sw = s.st_sysw_host[w];
+          for (int32_t t = 0; t < sw.G; ++t) {
+            const int64_t x = sw.cell0 + t;
+            std::fprintf(f, "%d %d %d %lld %d %d %llu %llu\n", s.index, sm, t, (long long)(w - s.st_sys_off[sm]),
+                         s.st_sys_host[x].steps, s.st_sys_host[x].cells, (unsigned long long)tr[2 * x],
+                         (unsigned long long)tr[2 * x + 1]);
+          }
+        }
       continue;
     }
     if (!s.st_trace.get() || s.st_waves_host.empty()) continue;
@@ -488,16 +494,17 @@ void fast_superstep(mf_ctx* ctx, Shard& s, int64_t superstep, double eta) {
   }
   if (ups == 0) return;
   if (ctx->fast_pair && ctx->fast_sys) {
-    const int32_t G = ctx->G_fast;
-    const int64_t per = static_cast<int64_t>(ctx->c) * G * G;
-    LaunchTimer tm(s, ctx->profiling, true);
-    launch_sweep_pair_sys(s.stream, s.st_sys.as<WaveDesc>() + smod * per, G, ctx->c * G, s.st_recs.as<PairRec>(),
-                          s.uf.as<float>(), s.itf.as<float>(), s.uf.bytes(), s.itf.bytes(), ctx->P.num_factors,
-                          static_cast<float>(eta), s.fast_prog.as<int32_t>(), s.sys_base, s.fast_err.as<int32_t>(),
-                          s.st_trace.get() ? s.st_trace.as<uint64_t>() + 2 * smod * per : nullptr, tm.start(),
-                          tm.stop());
-    s.sys_base += static_cast<uint32_t>(G);
-    ctx->stats.kernel_launches += 1;
+    const int64_t w0 = s.st_sys_off[smod], nw = s.st_sys_off[smod + 1] - w0;
+    if (nw > 0) {
+      LaunchTimer tm(s, ctx->profiling, true);
+      launch_sweep_pair_sys(s.stream, s.st_sysw.as<SysWave>() + w0, s.st_sys.as<WaveDesc>(), static_cast<int>(nw),
+                            s.st_recs.as<PairRec>(), s.uf.as<float>(), s.itf.as<float>(), s.uf.bytes(), s.itf.bytes(),
+                            ctx->P.num_factors, static_cast<float>(eta), s.fast_prog.as<int32_t>(), s.sys_base,
+                            s.fast_err.as<int32_t>(), s.st_trace.get() ? s.st_trace.as<uint64_t>() : nullptr,
+                            tm.start(), tm.stop());
+      s.sys_base += s.sys_step;
+      ctx->stats.kernel_launches += 1;
+    }
   } else if (ctx->fast_pair) {
     for (int32_t t = 0; t < ctx->G_fast; ++t) {
       const int64_t x = smod * ctx->G_fast + t;
@@ -665,17 +672,44 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
     const int k = ctx->P.num_factors;
     ctx->fast_pair = fk == FastKernel::kPair;
     ctx->fast_sys = false;
-    if (ctx->fast_pair && want_pair_sys()) {  // every wave of a superstep must be resident at once
-      bool fits = true;
+    std::vector<int32_t> block_groups;  // systolic sweep, automatic G: one G_j per rating block
+    if (ctx->fast_pair && want_pair_sys()) {
+      int cap = 1 << 30, simds = 1 << 30;
       for (auto& s : ctx->shards) {
         DeviceGuard g(s.device);
-        fits = fits && static_cast<int64_t>(ctx->c) * ctx->G_fast <= sweep_pair_sys_capacity(k);
+        int cus = 0;
+        MF_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s.device));
+        cap = std::min(cap, sweep_pair_sys_capacity(k));
+        simds = std::min(simds, 4 * cus);
       }
+      if (const char* v = std::getenv("MFHIP_SYS_WAVES")) simds = std::max(8, std::atoi(v));  // tests pin it
+      const char* bg = std::getenv("MFHIP_BLOCK_GROUPS");
+      if (ctx->P.fast_waves == 0 && !(bg && std::string(bg) == "0")) {
+        block_groups.assign(nb2, 0);
+        for (auto& s : ctx->shards) {
+          const auto gb = choose_block_groups(ctx->rb, ctx->I, ctx->c, s.index, simds);
+          for (int64_t b = 0; b < nb2; ++b)
+            if (gb[b] > 0) block_groups[b] = gb[b];
+        }
+      }
+      // every wave of a superstep must be resident at once
+      bool fits = cap > 0;
+      for (auto& s : ctx->shards)
+        for (int32_t sm = 0; sm < ctx->nb && fits; ++sm) {
+          int64_t waves = 0;
+          for (int32_t j = 0; j < ctx->c; ++j) {
+            const int32_t p = s.index * ctx->c + j;
+            const int64_t b = static_cast<int64_t>(p) * ctx->nb + (p + sm) % ctx->nb;
+            waves += block_groups.empty() || block_groups[b] == 0 ? ctx->G_fast : block_groups[b];
+          }
+          fits = waves <= cap;
+        }
       ctx->fast_sys = fits;
+      if (!fits) block_groups.clear();
     }
     build_fast_plan(fp, ctx->rb, ctx->U, ctx->I, ctx->G_fast, k, ctx->P.lambda,
                     static_cast<uint64_t>(ctx->P.seed) * 0x9E3779B97F4A7C15ULL + 1, dummy, nullptr,
-                    ctx->fast_pair ? 2 * kPairRing : kHazardWindow);
+                    ctx->fast_pair ? 2 * kPairRing : kHazardWindow, block_groups.empty() ? nullptr : &block_groups);
     ctx->stats.pads = fp.pads;
     clk.lap("cell plan");
     {  // priority threshold: 3x the mean non-empty cell length
@@ -683,8 +717,9 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
       for (int64_t b = 0; b < nb2; ++b)
         if (fp.cell_base[b] >= 0) {
           const int32_t* o = fp.cell_off.data() + fp.cell_base[b];
-          for (int64_t c2 = 0; c2 < static_cast<int64_t>(ctx->G_fast) * ctx->G_fast; ++c2) cells += o[c2 + 1] > o[c2];
-          recs += o[static_cast<int64_t>(ctx->G_fast) * ctx->G_fast];
+          const int64_t gg = static_cast<int64_t>(fp.Gb[b]) * fp.Gb[b];
+          for (int64_t c2 = 0; c2 < gg; ++c2) cells += o[c2 + 1] > o[c2];
+          recs += o[gg];
         }
       ctx->fast_prio_len = cells ? static_cast<int32_t>(std::max<int64_t>(16, 3 * recs / cells)) : (1 << 30);
       if (const char* v = std::getenv("MFHIP_PRIO_LEN")) ctx->fast_prio_len = std::atoi(v);
@@ -692,6 +727,12 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
     ctx->fast_rb_size.assign(nb2, 0);
     for (int64_t b = 0; b < nb2; ++b) ctx->fast_rb_size[b] = ctx->rb.size(b);
     ctx->stats.groups = ctx->G_fast;
+    if (!block_groups.empty()) {  // report the mean G_j of the non-empty rating blocks
+      int64_t sum = 0, cnt = 0;
+      for (int64_t b = 0; b < nb2; ++b)
+        if (fp.cell_base[b] >= 0) { sum += fp.Gb[b]; ++cnt; }
+      ctx->stats.groups = cnt ? static_cast<int32_t>((sum + cnt / 2) / cnt) : ctx->G_fast;
+    }
     ctx->fast_dummy_u = dummy;
     ctx->fast_dummy_i = static_cast<uint32_t>(ctx->I.rows());
     for (auto& s : ctx->shards) {
@@ -703,7 +744,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
       MF_HIP(hipMemset(s.itf.as<char>() + static_cast<size_t>(ctx->fast_dummy_i) * row_bytes, 0, row_bytes));
       if (ctx->fast_pair) {
         PairPlan pp;
-        build_pair_plan(pp, fp, ctx->nb, ctx->c, s.index, k);
+        build_pair_plan(pp, fp, ctx->nb, ctx->c, s.index, k, !ctx->fast_sys);
         ctx->stats.pads += pp.noop_halves - fp.pads;  // run padding on top of the planner's
         s.st_recs.alloc(std::max<size_t>(pp.recs.size(), 1) * sizeof(PairRec));
         s.st_waves.alloc(std::max<size_t>(pp.waves.size(), 1) * sizeof(WaveDesc));
@@ -715,9 +756,18 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
         s.st_sys_host.clear();
         s.sys_base = 0;
         if (ctx->fast_sys) {
-          s.st_sys.alloc(pp.sys.size() * sizeof(WaveDesc));
-          MF_HIP(hipMemcpy(s.st_sys.get(), pp.sys.data(), pp.sys.size() * sizeof(WaveDesc), hipMemcpyHostToDevice));
-          s.fast_prog.alloc(static_cast<size_t>(ctx->c) * ctx->G_fast * kProgStride * sizeof(int32_t));
+          s.st_sys.alloc(std::max<size_t>(pp.sys.size(), 1) * sizeof(WaveDesc));
+          if (!pp.sys.empty())
+            MF_HIP(hipMemcpy(s.st_sys.get(), pp.sys.data(), pp.sys.size() * sizeof(WaveDesc), hipMemcpyHostToDevice));
+          s.st_sysw.alloc(std::max<size_t>(pp.sys_waves.size(), 1) * sizeof(SysWave));
+          if (!pp.sys_waves.empty())
+            MF_HIP(hipMemcpy(s.st_sysw.get(), pp.sys_waves.data(), pp.sys_waves.size() * sizeof(SysWave),
+                             hipMemcpyHostToDevice));
+          s.st_sys_off = pp.sys_off;
+          s.sys_step = static_cast<uint32_t>(fp.G) + 1u;
+          int64_t max_waves = 1;
+          for (int32_t sm = 0; sm < ctx->nb; ++sm) max_waves = std::max(max_waves, pp.sys_off[sm + 1] - pp.sys_off[sm]);
+          s.fast_prog.alloc(static_cast<size_t>(max_waves) * kProgStride * sizeof(int32_t));
           MF_HIP(hipMemset(s.fast_prog.get(), 0, s.fast_prog.bytes()));
           s.fast_err.alloc(16);
           MF_HIP(hipMemset(s.fast_err.get(), 0, 16));
@@ -727,7 +777,10 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
           const size_t n = ctx->fast_sys ? pp.sys.size() : pp.waves.size();
           s.st_trace.alloc(std::max<size_t>(n, 1) * 16);
           MF_HIP(hipMemset(s.st_trace.get(), 0, std::max<size_t>(n, 1) * 16));
-          if (ctx->fast_sys) s.st_sys_host = pp.sys;
+          if (ctx->fast_sys) {
+            s.st_sys_host = pp.sys;
+            s.st_sysw_host = pp.sys_waves;
+          }
           else s.st_waves_host = pp.waves;
         }
         continue;
@@ -1455,7 +1508,7 @@ int mf_debug_fast_schedule(const int32_t* u, const int32_t* i, int64_t n, int32_
                            int32_t groups, int32_t blocking, int32_t window, int32_t* block_out,
                            int32_t* substep_out, int32_t* group_out, int64_t* pos_out) {
   return guarded([&] {
-    MF_REQUIRE(n >= 0 && n_blocks >= 1 && groups >= 1, "bad argument");
+    MF_REQUIRE(n >= 0 && n_blocks >= 1 && groups != 0, "bad argument");
     MF_REQUIRE(n == 0 || (u && i && block_out && substep_out && group_out && pos_out), "null argument");
     SideLayout U, I;
     const Blocking bl = blocking == MF_BLOCKING_BALANCED ? Blocking::kBalanced : Blocking::kJvm;
@@ -1466,20 +1519,24 @@ int mf_debug_fast_schedule(const int32_t* u, const int32_t* i, int64_t n, int32_
     build_rating_blocks(rb, U, I, u, i, r.data(), n, 0, n_blocks, false, true);
     FastPlan fp;
     std::vector<int64_t> src;
-    build_fast_plan(fp, rb, U, I, groups, 1, 1.0, static_cast<uint64_t>(seed) * 0x9E3779B97F4A7C15ULL + 1,
-                    static_cast<uint32_t>(U.rows()), &src, window > 0 ? window : kHazardWindow);
+    std::vector<int32_t> block_groups;  // groups < 0: the systolic per-block choice for -groups waves
+    if (groups < 0) block_groups = choose_block_groups(rb, I, n_blocks, 0, -groups);
+    build_fast_plan(fp, rb, U, I, groups > 0 ? groups : 8, 1, 1.0,
+                    static_cast<uint64_t>(seed) * 0x9E3779B97F4A7C15ULL + 1, static_cast<uint32_t>(U.rows()), &src,
+                    window > 0 ? window : kHazardWindow, block_groups.empty() ? nullptr : &block_groups);
     const int64_t nb2 = static_cast<int64_t>(n_blocks) * n_blocks;
-    const int64_t GG = static_cast<int64_t>(groups) * groups;
     for (int64_t b = 0; b < nb2; ++b) {
       if (fp.rec_base[b] < 0) continue;
+      const int32_t G = fp.Gb[b];
+      const int64_t GG = static_cast<int64_t>(G) * G;
       const int32_t* off = fp.cell_off.data() + fp.cell_base[b];
       for (int64_t cidx = 0; cidx < GG; ++cidx)
         for (int64_t x = off[cidx]; x < off[cidx + 1]; ++x) {
           if (src[fp.rec_base[b] + x] < 0) continue;  // padding
           const int64_t j = rb.src[src[fp.rec_base[b] + x]];
           block_out[j] = static_cast<int32_t>(b);
-          substep_out[j] = static_cast<int32_t>(cidx / groups);
-          group_out[j] = static_cast<int32_t>(cidx % groups);
+          substep_out[j] = static_cast<int32_t>(cidx / G);
+          group_out[j] = static_cast<int32_t>(cidx % G);
           pos_out[j] = x - off[cidx];
         }
     }

@@ -321,15 +321,19 @@ inline uint32_t mix32(uint64_t x) {
 // by item (one contiguous run per item, so the item row stays in registers) and by a hash
 // of the user inside an item run.
 void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, const SideLayout& I,
-                     int32_t G, int32_t k, double lambda, uint64_t order_seed, uint32_t dummy_row,
-                     std::vector<int64_t>* rec_src, int32_t window) {
+                     int32_t G0, int32_t k, double lambda, uint64_t order_seed, uint32_t dummy_row,
+                     std::vector<int64_t>* rec_src, int32_t window, const std::vector<int32_t>* block_groups) {
   const int64_t kHazardWindow = window;  // shadows the default for this plan
   const uint32_t row_bytes = static_cast<uint32_t>(k) * 4u;
   const int32_t nb = rb.n_blocks;
   const int64_t nb2 = static_cast<int64_t>(nb) * nb;
-  const int64_t GG = static_cast<int64_t>(G) * G;
   fp = FastPlan();
-  fp.G = G;
+  fp.G = G0;
+  fp.Gb.assign(nb2, G0);
+  if (block_groups) {
+    for (int64_t b = 0; b < nb2; ++b) fp.Gb[b] = (*block_groups)[b] > 0 ? (*block_groups)[b] : G0;
+    fp.G = *std::max_element(fp.Gb.begin(), fp.Gb.end());
+  }
   fp.rec_base.assign(nb2, -1);
   fp.cell_base.assign(nb2, -1);
   std::vector<int64_t> blocks;
@@ -342,6 +346,8 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
   std::vector<int64_t> pads(nblk, 0);
   parallel_tasks(nblk, [&](int64_t bx) {
     const int64_t b = blocks[bx];
+    const int32_t G = fp.Gb[b];
+    const int64_t GG = static_cast<int64_t>(G) * G;
     const int32_t p = static_cast<int32_t>(b / nb), q = static_cast<int32_t>(b % nb);
     const int64_t ub = U.block_start[p], nu = U.block_start[p + 1] - ub;
     const int64_t ib = I.block_start[q], ni = I.block_start[q + 1] - ib;
@@ -489,7 +495,7 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
     fp.rec_base[blocks[bx]] = total;
     fp.cell_base[blocks[bx]] = cells;
     total += static_cast<int64_t>(outs[bx].size());
-    cells += GG + 1;
+    cells += static_cast<int64_t>(fp.Gb[blocks[bx]]) * fp.Gb[blocks[bx]] + 1;
     fp.pads += pads[bx];
   }
   fp.recs.resize(total);
@@ -505,7 +511,7 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
 }
 
 namespace {
-struct SubCell { int32_t len; int64_t beg; int32_t j, g; };
+struct SubCell { int32_t len; int64_t beg; int32_t j, g, t; };
 // The non-empty cells of every sub-step (sm, t) of this shard's rating blocks, longest first.
 std::vector<std::vector<SubCell>> collect_subs(const FastPlan& fp, int32_t nb, int32_t c, int32_t shard) {
   using Cell = SubCell;
@@ -523,10 +529,32 @@ std::vector<std::vector<SubCell>> collect_subs(const FastPlan& fp, int32_t nb, i
       for (int32_t g = 0; g < G; ++g) {
         const int64_t cb = static_cast<int64_t>(t) * G + g;
         const int32_t len = off[cb + 1] - off[cb];
-        if (len > 0) cells.push_back(Cell{len, fp.rec_base[b] + off[cb], j, g});
+        if (len > 0) cells.push_back(Cell{len, fp.rec_base[b] + off[cb], j, g, t});
       }
     }
     std::stable_sort(cells.begin(), cells.end(), [](const Cell& a, const Cell& b2) { return a.len > b2.len; });
+  });
+  return subs;
+}
+
+// The non-empty cells of every superstep sm of this shard's rating blocks (per-block G), in
+// (j, g, t) order.
+std::vector<std::vector<SubCell>> collect_supersteps(const FastPlan& fp, int32_t nb, int32_t c, int32_t shard) {
+  std::vector<std::vector<SubCell>> subs(nb);
+  parallel_tasks(nb, [&](int64_t sm) {
+    for (int32_t j = 0; j < c; ++j) {
+      const int32_t p = shard * c + j, q = static_cast<int32_t>((p + sm) % nb);
+      const int64_t b = static_cast<int64_t>(p) * nb + q;
+      if (fp.cell_base[b] < 0) continue;
+      const int32_t G = fp.Gb[b];
+      const int32_t* off = fp.cell_off.data() + fp.cell_base[b];
+      for (int32_t g = 0; g < G; ++g)
+        for (int32_t t = 0; t < G; ++t) {
+          const int64_t cb = static_cast<int64_t>(t) * G + g;
+          const int32_t len = off[cb + 1] - off[cb];
+          if (len > 0) subs[sm].push_back(SubCell{len, fp.rec_base[b] + off[cb], j, g, t});
+        }
+    }
   });
   return subs;
 }
@@ -538,12 +566,13 @@ std::vector<std::vector<SubCell>> collect_subs(const FastPlan& fp, int32_t nb, i
 // registers or the record is a no-op) and to store (an item row only where its run ends),
 // and how A's user row is forwarded: from the previous step's A or B when that was the
 // record just before A.
-void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, int32_t shard, int32_t k) {
+void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, int32_t shard, int32_t k,
+                     bool substep_waves) {
   (void)k;
   using Cell = SubCell;
   pp = PairPlan();
-  const int64_t nsub = static_cast<int64_t>(nb) * fp.G;
-  const auto subs = collect_subs(fp, nb, c, shard);
+  const auto subs = substep_waves ? collect_subs(fp, nb, c, shard) : collect_supersteps(fp, nb, c, shard);
+  const int64_t nsub = static_cast<int64_t>(subs.size());
   auto item_of = [](const FastRec& f) { return f.i & ~kPadBit; };
   auto is_pad = [](const FastRec& f) { return (f.i & kPadBit) != 0; };
   auto pairs_of = [](const FastRec* f, int64_t len) {
@@ -650,13 +679,87 @@ void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, in
     }
   });
   for (int64_t x = 0; x < nsub; ++x) pp.noop_halves += noops[x];
-  const int64_t G = fp.G;
-  pp.sys.assign(static_cast<size_t>(nb) * c * G * G, WaveDesc{0, 0, kWaveGeneric});
-  for (int64_t x = 0; x < nsub; ++x) {
-    const int64_t sm = x / G, t = x % G;
-    int64_t w = pp.sub_off[x];
-    for (const Cell& cl : subs[x]) pp.sys[((sm * c + cl.j) * G + cl.g) * G + t] = pp.waves[w++];
+  // systolic tables: superstep sm's waves are (j, g), j-major; wave (j, g) owns G_j cells
+  pp.sys_off.assign(nb + 1, 0);
+  std::vector<std::vector<int64_t>> wave0(nb, std::vector<int64_t>(c, 0));  // sys_waves index of (sm, j, g=0)
+  for (int32_t sm = 0; sm < nb; ++sm) {
+    pp.sys_off[sm] = static_cast<int64_t>(pp.sys_waves.size());
+    for (int32_t j = 0; j < c; ++j) {
+      const int32_t p = shard * c + j, q = (p + sm) % nb;
+      const int64_t b = static_cast<int64_t>(p) * nb + q;
+      const int32_t G = fp.cell_base[b] < 0 ? 0 : fp.Gb[b];
+      const int64_t w0 = static_cast<int64_t>(pp.sys_waves.size());
+      wave0[sm][j] = w0;
+      for (int32_t g = 0; g < G; ++g) {
+        const int32_t nbr = static_cast<int32_t>(w0 - pp.sys_off[sm]) + (g + 1 == G ? 0 : g + 1);
+        pp.sys_waves.push_back(SysWave{static_cast<int64_t>(pp.sys.size()), G, nbr});
+        pp.sys.resize(pp.sys.size() + G, WaveDesc{0, 0, kWaveGeneric});
+      }
+    }
   }
+  pp.sys_off[nb] = static_cast<int64_t>(pp.sys_waves.size());
+  for (int64_t x = 0; x < nsub; ++x) {
+    const int64_t sm = substep_waves ? x / fp.G : x;
+    int64_t w = pp.sub_off[x];
+    for (const Cell& cl : subs[x]) {
+      const SysWave& sw = pp.sys_waves[wave0[sm][cl.j] + cl.g];
+      pp.sys[sw.cell0 + cl.t] = pp.waves[w++];
+    }
+  }
+}
+
+std::vector<int32_t> choose_block_groups(const RatingBlocks& rb, const SideLayout& I, int32_t c, int32_t shard,
+                                         int32_t waves) {
+  const int32_t nb = rb.n_blocks;
+  const int64_t nb2 = static_cast<int64_t>(nb) * nb;
+  std::vector<int32_t> Gb(nb2, 0);
+  std::vector<int64_t> size(nb2, 0), top(nb2, 0);  // ratings, ratings of the most rated item
+  parallel_tasks(nb2, [&](int64_t b) {
+    const int32_t p = static_cast<int32_t>(b / nb), q = static_cast<int32_t>(b % nb);
+    if (p < shard * c || p >= (shard + 1) * c || rb.size(b) == 0) return;
+    const int64_t ib = I.block_start[q], ni = I.block_start[q + 1] - ib;
+    std::vector<int32_t> cnt(ni, 0);
+    int32_t mx = 0;
+    for (int64_t x = rb.start[b]; x < rb.start[b + 1]; ++x) mx = std::max(mx, ++cnt[rb.irow[x] - ib]);
+    size[b] = rb.size(b);
+    top[b] = mx;
+  });
+  auto wave_ns = [&](int64_t b, int32_t G) {
+    const double per_group = static_cast<double>(size[b]) / G;
+    return G * kSysCellNs + std::max(per_group / 2 * kSysPairNs, static_cast<double>(top[b]) / 2 * kSysRunPairNs);
+  };
+  constexpr int32_t kStep = 8, kMaxG = 1024;
+  for (int32_t sm = 0; sm < nb; ++sm) {
+    std::vector<int64_t> bs;
+    for (int32_t j = 0; j < c; ++j) {
+      const int32_t p = shard * c + j;
+      const int64_t b = static_cast<int64_t>(p) * nb + (p + sm) % nb;
+      if (size[b] > 0) bs.push_back(b);
+    }
+    if (bs.empty()) continue;
+    // smallest G (multiple of kStep) whose modelled wave time is <= T, or 0 if none
+    auto gmin = [&](int64_t b, double T) {
+      for (int32_t G = kStep; G <= kMaxG; G += kStep)
+        if (wave_ns(b, G) <= T) return G;
+      return 0;
+    };
+    double lo = 0, hi = 0;
+    for (int64_t b : bs) hi = std::max(hi, wave_ns(b, kStep));
+    for (int it = 0; it < 60; ++it) {
+      const double T = 0.5 * (lo + hi);
+      int64_t sum = 0;
+      bool ok = true;
+      for (int64_t b : bs) {
+        const int32_t G = gmin(b, T);
+        ok = ok && G > 0;
+        sum += G;
+      }
+      if (ok && sum <= waves) hi = T;
+      else lo = T;
+    }
+    for (int64_t b : bs) Gb[b] = std::max(gmin(b, hi), kStep);
+  }
+  return Gb;
 }
 
 }  // namespace mfhip

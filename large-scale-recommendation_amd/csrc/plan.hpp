@@ -113,10 +113,11 @@ struct FastRec {
 static_assert(sizeof(FastRec) == 32, "FastRec is two 16-B words");
 
 struct FastPlan {
-  int32_t G = 4;                       // rotation groups per rating block
+  int32_t G = 4;                       // rotation groups per rating block (the largest when per-block)
+  std::vector<int32_t> Gb;             // per rating block (n*n): its rotation groups
   std::vector<FastRec> recs;           // all rating blocks of this shard, cell-major per block
   std::vector<int64_t> rec_base;       // per rating block (n*n), -1 if not on this shard
-  std::vector<int32_t> cell_off;       // per included rating block: G*G+1 relative offsets
+  std::vector<int32_t> cell_off;       // per included rating block: Gb*Gb+1 relative offsets
   std::vector<int64_t> cell_base;      // per rating block: index into cell_off (-1 if absent)
   int64_t pads = 0;                    // padding records inserted
 };
@@ -160,17 +161,32 @@ struct PairRec {
   uint32_t pad_;
 };
 static_assert(sizeof(PairRec) == 64, "PairRec is four 16-B words");
+// Systolic sweep wave: its G cells are PairPlan::sys[cell0 .. cell0+G), one per sub-step; it
+// waits on wave nbr (same superstep) -- item group g+1 of the same rating block.
+struct SysWave {
+  int64_t cell0;
+  int32_t G;
+  int32_t nbr;
+};
+static_assert(sizeof(SysWave) == 16, "SysWave is one 16-B word");
+
 struct PairPlan {
   std::vector<PairRec> recs;
   std::vector<WaveDesc> waves;   // one per non-empty cell (steps = pairs), every (sm, t), sm-major
   std::vector<int64_t> sub_off;  // nb*G + 1
-  // Systolic table (k_sweep_pair_sys): the cell of every (sm, local block j, item group g,
-  // sub-step t) at [((sm*c + j)*G + g)*G + t]; steps = 0 for an empty cell.
+  // Systolic tables (k_sweep_pair_sys): the waves of superstep sm are
+  // sys_waves[sys_off[sm] .. sys_off[sm+1]) (local block j major, then item group g); their
+  // cells live in sys (steps = 0 for an empty cell).
   std::vector<WaveDesc> sys;
+  std::vector<SysWave> sys_waves;
+  std::vector<int64_t> sys_off;
   int64_t noop_halves = 0;       // pair halves that are no-ops (planner padding, repeated users)
 };
-// The plan window must be >= 2 * kPairRing records.
-void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, int32_t shard, int32_t k);
+// The plan window must be >= 2 * kPairRing records.  substep_waves: order the cells (and
+// pp.waves / sub_off) per sub-step (sm, t), longest first, for the per-sub-step launches (needs a
+// uniform G); otherwise per superstep, and only the systolic tables are meaningful.
+void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, int32_t shard, int32_t k,
+                     bool substep_waves = true);
 
 int32_t choose_groups(int64_t avg_block_ratings, int32_t blocks_per_device, int32_t fast_waves,
                       double cell_target = 150.0, int32_t default_waves = 2048);
@@ -180,8 +196,22 @@ int32_t choose_groups(int64_t avg_block_ratings, int32_t blocks_per_device, int3
 // floats (record offsets are row * k * 4 and must stay below 4 GiB).
 // window: a row recurs inside a cell only at the next position or >= window positions later
 // (the kernel's prefetch distance; kHazardWindow for kernels_fast.hip).
+// block_groups (optional, n*n): per rating block rotation groups (0 = G); otherwise G for all.
 void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, const SideLayout& I,
                      int32_t G, int32_t k, double lambda, uint64_t order_seed, uint32_t dummy_row,
-                     std::vector<int64_t>* rec_src = nullptr, int32_t window = kHazardWindow);
+                     std::vector<int64_t>* rec_src = nullptr, int32_t window = kHazardWindow,
+                     const std::vector<int32_t>* block_groups = nullptr);
+
+// Rotation groups per rating block for the systolic sweep, where every rating block of a
+// superstep is its own G_j x G_j grid and only the superstep's longest wave matters.  For each
+// superstep of this shard it picks the smallest G_j (multiples of 8) that bring every block's
+// longest wave under a common bound T, with T minimal such that sum_j G_j <= waves.  A wave's
+// time is modelled as G cells x kSysCellNs + max(block ratings / G, ratings of the block's
+// most rated item) / 2 pairs x ns per pair (no group is lighter than one item's run).
+constexpr double kSysCellNs = 3000.0;     // per-cell start, drain and hand-off (wave trace)
+constexpr double kSysPairNs = 270.0;      // mixed-cell pair step (wave trace)
+constexpr double kSysRunPairNs = 195.0;   // single-item-run pair step (wave trace)
+std::vector<int32_t> choose_block_groups(const RatingBlocks& rb, const SideLayout& I, int32_t c, int32_t shard,
+                                         int32_t waves);
 
 }  // namespace mfhip

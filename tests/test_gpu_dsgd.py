@@ -280,6 +280,7 @@ def test_systolic_sweep_equals_substep_launches(monkeypatch, k, nb, G, hot, n):
     else:
         d = synth.generate(max(400, n // 50), max(120, n // 300), n, seed=k)
     outs = []
+    monkeypatch.setenv("MFHIP_BLOCK_GROUPS", "0")  # the same uniform G for both drivers
     for sys_on in ("0", "1"):
         monkeypatch.setenv("MFHIP_PAIR_SYS", sys_on)
         with mfhip.Context(params(k, 2, nb, 3, mode=L.MODE_FAST_F32, fast_waves=-G if G else 0,
@@ -299,3 +300,22 @@ def test_systolic_multi_shard_matches_single(monkeypatch):
             ctx.fit(d.u, d.i, d.r)
             outs.append((ctx.factors(0)[1], ctx.factors(1)[1]))
     assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("k,nb,waves,hot", [(64, 2, 64, False), (128, 3, 96, True), (64, 4, 256, True)])
+def test_systolic_per_block_groups_equal_their_schedule(monkeypatch, k, nb, waves, hot):
+    """Automatic G: every rating block of a superstep gets its own G_j x G_j rotation
+    (choose_block_groups, budget `waves` per superstep); the kernel == sequential replay of that plan."""
+    monkeypatch.setenv("MFHIP_SYS_WAVES", str(waves))
+    d = hot_item_data(k) if hot else synth.generate(3000, 600, 60000, seed=k)
+    seed, lam, lr, iters = 3, 1.0, 0.002, 2
+    uids, U, iids, I = fast_replay_reference(d, k, nb, seed, -waves, iters, lam, lr)
+    with mfhip.Context(params(k, iters, nb, seed, mode=L.MODE_FAST_F32, lam=lam, lr=lr, fast_waves=0,
+                              blocking=L.BLOCKING_REFERENCE)) as ctx:
+        ctx.fit(d.u, d.i, d.r)
+        a_ids, a_u = ctx.factors(0)
+        b_ids, a_i = ctx.factors(1)
+        assert ctx.stats()["kernel_launches"] <= iters * nb  # one systolic launch per superstep
+    assert np.array_equal(a_ids, uids) and np.array_equal(b_ids, iids)
+    np.testing.assert_allclose(a_u, U, rtol=2e-4, atol=2e-5)
+    np.testing.assert_allclose(a_i, I, rtol=2e-4, atol=2e-5)

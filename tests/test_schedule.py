@@ -64,10 +64,19 @@ def fast_schedule(u, i, nb, seed, G, blocking=L.BLOCKING_REFERENCE, window=0):
     return b, t, g, p
 
 
-@pytest.mark.parametrize("nb,G,window", [(1, 4, 0), (3, 8, 0), (4, 16, 0), (3, 8, 32), (2, 4, 16)])
+@pytest.mark.parametrize("nb,G,window", [(1, 4, 0), (3, 8, 0), (4, 16, 0), (3, 8, 32), (2, 4, 16), (3, -64, 14),
+                                         (2, -16, 14)])
 def test_fast_rotation_is_conflict_free(nb, G, window):
+    """G < 0: the systolic sweep's per-rating-block groups for a budget of -G waves per superstep."""
     d = synth.generate(500, 200, 20000, seed=1)
     b, t, g, p = fast_schedule(d.u, d.i, nb, 3, G, window=window)
+    if G < 0:
+        Gb = {int(x): int(t[b == x].max()) + 1 for x in np.unique(b)}  # per block: t, g in [0, G_j)
+        assert all(int(g[b == x].max()) < Gb[x] for x in Gb)
+        assert all(v % 8 == 0 for v in Gb.values())
+        for s in range(nb):  # the superstep's waves fit the budget
+            assert sum(v for x, v in Gb.items() if (x // nb + s) % nb == x % nb) <= -G
+        G = 1024
     win = window or 8
     # blocks follow DSGD blocking of the reference
     ub = np.array([mfhip.jvm.block_of(int(x), 3, nb) for x in d.u])
@@ -77,7 +86,7 @@ def test_fast_rotation_is_conflict_free(nb, G, window):
     # item row appears in two different cells
     for s in range(nb):
         in_stratum = ((b // nb + s) % nb) == (b % nb)
-        for tt in range(G):
+        for tt in np.unique(t):
             m = in_stratum & (t == tt)
             cell = b[m].astype(np.int64) * G + g[m]
             for ids in (d.u[m], d.i[m]):
