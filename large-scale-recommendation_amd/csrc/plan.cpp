@@ -2,6 +2,8 @@
 #include "plan.hpp"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <unordered_map>
 #include <atomic>
 #include <cmath>
@@ -369,6 +371,34 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
       key[x] = {(cell << 40) | (static_cast<uint64_t>(il) << 16) | tie, x};
     }
     std::sort(key.begin(), key.end());
+    // Repeated (user, item) ratings (frequent in Zipf-distributed data: a heavy user rates a hot
+    // item dozens of times) would sit next to each other and force no-op halves into the pair
+    // steps (a pair cannot hold one user twice).  Spread them: inside an item run, the m
+    // ratings of one user go to the fractional positions (o + h_u) / m, o = 0..m-1, h_u a
+    // per-user hash in [0, 1) -- evenly over the whole run, interleaved with everyone else.
+    {
+      struct K { uint64_t run, pos; int64_t x; };
+      std::vector<K> k2(len);
+      std::unordered_map<uint32_t, std::pair<uint32_t, uint32_t>> seen;  // user -> (count, next occurrence)
+      for (int64_t y0 = 0; y0 < len;) {
+        const uint64_t run = key[y0].first & ~0xFFFFull;  // cell and item
+        int64_t y1 = y0;
+        seen.clear();
+        while (y1 < len && (key[y1].first & ~0xFFFFull) == run) seen[rb.urow[s + key[y1].second]].first++, ++y1;
+        for (int64_t y = y0; y < y1; ++y) {
+          const uint32_t urow = rb.urow[s + key[y].second];
+          auto& e = seen[urow];
+          const double h = static_cast<double>(mix32(order_seed * 0x2545F4914F6CDD1DULL ^ urow)) * (1.0 / 4294967296.0);
+          const double frac = (e.second++ + h) / e.first;
+          k2[y] = K{run, (static_cast<uint64_t>(frac * 16777216.0) << 16) | (key[y].first & 0xFFFFull), key[y].second};
+        }
+        y0 = y1;
+      }
+      std::sort(k2.begin(), k2.end(), [](const K& a, const K& b) {
+        return a.run != b.run ? a.run < b.run : a.pos != b.pos ? a.pos < b.pos : a.x < b.x;
+      });
+      for (int64_t y = 0; y < len; ++y) key[y] = {k2[y].run, k2[y].x};
+    }
     // Emit each cell as a sequence the kernel can run with a D-deep prefetch ring: every user
     // and every item row recurs either at the next position (the kernel forwards it in
     // registers: item runs and user runs) or at least kHazardWindow positions later (its
@@ -511,6 +541,9 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
 }
 
 namespace {
+// MFHIP_DEBUG_PLAN: why cells were not given the single-run path (stderr, per build).
+const bool g_plan_debug = std::getenv("MFHIP_DEBUG_PLAN") != nullptr;
+std::atomic<int64_t> g_not_single[8];
 struct SubCell { int32_t len; int64_t beg; int32_t j, g, t; };
 // The non-empty cells of every sub-step (sm, t) of this shard's rating blocks, longest first.
 std::vector<std::vector<SubCell>> collect_subs(const FastPlan& fp, int32_t nb, int32_t c, int32_t shard) {
@@ -657,9 +690,12 @@ void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, in
       }
       // one item run (no split, every later pair keeps the item): the kernel's lean path
       bool single = first[0].ia != kOffOOB && !(first[0].flags & (kPairKeepQ | kPairSplit));
-      for (const PairRec* r = first; single && r < out; ++r)
+      int why = single ? 0 : 1;
+      for (const PairRec* r = first; single && r < out; ++r) {
         single = !(r->flags & kPairSplit) && (r == first || (r->flags & kPairKeepQ)) && r->ub == r->sb &&
                  (r + 1 < out ? r->si == kOffOOB : r->si == first[0].ia);
+        if (!single) why = (r->flags & kPairSplit) ? 2 : !(r == first || (r->flags & kPairKeepQ)) ? 3 : r->ub != r->sb ? 4 : 5;
+      }
       // the lean path prefetches kPairRingSingle pairs ahead: a user row it loads must have
       // been stored by an earlier pair at least that far back
       if (single) {
@@ -669,16 +705,24 @@ void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, in
           for (uint32_t off : {r->ua, r->ub}) {
             if (off == kOffOOB) continue;
             const auto it = stored.find(off);
-            if (it != stored.end() && j - it->second < kPairRingSingle) single = false;
+            if (it != stored.end() && j - it->second < kPairRingSingle) { single = false; why = 6; }
           }
           if (r->sa != kOffOOB) stored[r->sa] = j;
           if (r->sb != kOffOOB) stored[r->sb] = j;
         }
       }
       if (single) pp.waves[w_this].cells = kWaveSingleRun;
+      else if (g_plan_debug) g_not_single[why]++;
     }
   });
   for (int64_t x = 0; x < nsub; ++x) pp.noop_halves += noops[x];
+  if (g_plan_debug) {
+    std::fprintf(stderr, "[mfhip] pair plan: cells not single-run: first %lld split %lld item-change %lld "
+                 "B-store %lld item-store %lld hazard %lld\n", (long long)g_not_single[1].load(),
+                 (long long)g_not_single[2].load(), (long long)g_not_single[3].load(), (long long)g_not_single[4].load(),
+                 (long long)g_not_single[5].load(), (long long)g_not_single[6].load());
+    for (auto& x : g_not_single) x = 0;
+  }
   // systolic tables: superstep sm's waves are (j, g), j-major; wave (j, g) owns G_j cells
   pp.sys_off.assign(nb + 1, 0);
   std::vector<std::vector<int64_t>> wave0(nb, std::vector<int64_t>(c, 0));  // sys_waves index of (sm, j, g=0)
@@ -724,9 +768,12 @@ std::vector<int32_t> choose_block_groups(const RatingBlocks& rb, const SideLayou
     size[b] = rb.size(b);
     top[b] = mx;
   });
+  double cell_ns = kSysCellNs, pair_ns = kSysPairNs, run_ns = kSysRunPairNs;
+  if (const char* v = std::getenv("MFHIP_SYS_MODEL"))  // tuning knob: "cell_ns,pair_ns,run_pair_ns"
+    std::sscanf(v, "%lf,%lf,%lf", &cell_ns, &pair_ns, &run_ns);
   auto wave_ns = [&](int64_t b, int32_t G) {
     const double per_group = static_cast<double>(size[b]) / G;
-    return G * kSysCellNs + std::max(per_group / 2 * kSysPairNs, static_cast<double>(top[b]) / 2 * kSysRunPairNs);
+    return G * cell_ns + std::max(per_group / 2 * pair_ns, static_cast<double>(top[b]) / 2 * run_ns);
   };
   constexpr int32_t kStep = 8, kMaxG = 1024;
   for (int32_t sm = 0; sm < nb; ++sm) {

@@ -208,9 +208,9 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
 // longest wave under a common bound T, with T minimal such that sum_j G_j <= waves.  A wave's
 // time is modelled as G cells x kSysCellNs + max(block ratings / G, ratings of the block's
 // most rated item) / 2 pairs x ns per pair (no group is lighter than one item's run).
-constexpr double kSysCellNs = 3000.0;     // per-cell start, drain and hand-off (wave trace)
-constexpr double kSysPairNs = 270.0;      // mixed-cell pair step (wave trace)
-constexpr double kSysRunPairNs = 195.0;   // single-item-run pair step (wave trace)
+constexpr double kSysCellNs = 4000.0;     // per-cell start, drain, hand-off and waiting (tuned, NFLX)
+constexpr double kSysPairNs = 300.0;      // mixed-cell pair step incl. no-op halves and group imbalance (tuned)
+constexpr double kSysRunPairNs = 186.0;   // single-item-run pair step (wave trace)
 std::vector<int32_t> choose_block_groups(const RatingBlocks& rb, const SideLayout& I, int32_t c, int32_t shard,
                                          int32_t waves);
 

@@ -1,0 +1,62 @@
+// Host-only probe of the fast pair plan (no GPU): reads ratings written by tools/probe/dump_ratings.py,
+// builds the systolic plan exactly as mf_dsgd_prepare does on one device, and prints per-superstep
+// wave statistics.  Build: make -C tools/probe
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "plan.hpp"
+
+using namespace mfhip;
+
+template <class T>
+std::vector<T> load(const char* path) {
+  FILE* f = std::fopen(path, "rb");
+  if (!f) { std::perror(path); std::exit(1); }
+  std::fseek(f, 0, SEEK_END);
+  const long n = std::ftell(f) / sizeof(T);
+  std::fseek(f, 0, SEEK_SET);
+  std::vector<T> v(n);
+  if (std::fread(v.data(), sizeof(T), n, f) != static_cast<size_t>(n)) std::exit(1);
+  std::fclose(f);
+  return v;
+}
+
+int main(int argc, char** argv) {
+  const char* dir = argc > 1 ? argv[1] : "/tmp";
+  const int nb = argc > 2 ? std::atoi(argv[2]) : 8, k = argc > 3 ? std::atoi(argv[3]) : 128;
+  const int waves = argc > 4 ? std::atoi(argv[4]) : 1024;
+  char p[512];
+  std::snprintf(p, sizeof p, "%s/probe_u.bin", dir); auto u = load<int32_t>(p);
+  std::snprintf(p, sizeof p, "%s/probe_i.bin", dir); auto i = load<int32_t>(p);
+  std::snprintf(p, sizeof p, "%s/probe_r.bin", dir); auto r = load<double>(p);
+  const int64_t n = static_cast<int64_t>(u.size());
+  SideLayout U, I;
+  build_side(U, u.data(), n, nb, 0, true);
+  build_side(I, i.data(), n, nb, 0, true);
+  RatingBlocks rb;
+  build_rating_blocks(rb, U, I, u.data(), i.data(), r.data(), n, 0, nb, false);
+  const auto Gb = choose_block_groups(rb, I, nb, 0, waves);
+  FastPlan fp;
+  build_fast_plan(fp, rb, U, I, 128, k, 1.0, 0 * 0x9E3779B97F4A7C15ULL + 1, static_cast<uint32_t>(U.rows()), nullptr,
+                  2 * kPairRing, &Gb);
+  PairPlan pp;
+  build_pair_plan(pp, fp, nb, nb, 0, k, false);
+  std::printf("pads %lld noop halves %lld pairs %zu\n", (long long)fp.pads, (long long)pp.noop_halves, pp.recs.size());
+  for (int sm = 0; sm < nb; ++sm) {
+    int64_t maxp = 0, maxw = -1, singles = 0, waves_sm = pp.sys_off[sm + 1] - pp.sys_off[sm];
+    for (int64_t w = pp.sys_off[sm]; w < pp.sys_off[sm + 1]; ++w) {
+      const SysWave& sw = pp.sys_waves[w];
+      int64_t pairs = 0;
+      for (int t = 0; t < sw.G; ++t) { pairs += pp.sys[sw.cell0 + t].steps; singles += pp.sys[sw.cell0 + t].cells == kWaveSingleRun; }
+      if (pairs > maxp) { maxp = pairs; maxw = w; }
+    }
+    int64_t ms = 0;
+    const SysWave& sw = pp.sys_waves[maxw];
+    for (int t = 0; t < sw.G; ++t) ms += pp.sys[sw.cell0 + t].cells == kWaveSingleRun;
+    std::printf("sm %d waves %lld single cells %lld busiest wave %lld: G %d pairs %lld single cells %lld\n", sm,
+                (long long)waves_sm, (long long)singles, (long long)(maxw - pp.sys_off[sm]), sw.G, (long long)maxp,
+                (long long)ms);
+  }
+  return 0;
+}
