@@ -55,6 +55,12 @@ class Dist:
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", str(self.rank)))
         self.dist = None
+        if self.world > 1 and os.environ.get("MFHIP_FAKE_HOSTS"):
+            # rehearsal of the RCCL ring on ONE device: RCCL refuses two ranks on one GPU of one
+            # host, so each rank claims its own host id and the ranks talk over loopback sockets
+            os.environ["NCCL_HOSTID"] = f"mfhip-rank{self.rank}"
+            os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+            os.environ.setdefault("NCCL_IB_DISABLE", "1")
         if self.world > 1:
             import torch.distributed as dist
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")

@@ -1,3 +1,12 @@
+# Rank-mode (RCCL ring) rehearsal on a one-GPU box: ranks share device 0 and claim distinct
+# RCCL host ids (MFHIP_FAKE_HOSTS), so send/recv goes over loopback sockets.  Checks det
+# bit-exactness and fast RMSE against a single-process context, then a small multi-rank bench.
 mkdir -p gpurun_out
-export NCCL_DEBUG=WARN
-timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 tools/rank_check.py --mode det > gpurun_out/rank_det.log 2>&1; echo "det rc=$?"; tail -5 gpurun_out/rank_det.log
+export NCCL_DEBUG=WARN MFHIP_FAKE_HOSTS=1
+W=${WORLD:-2}
+timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node $W --master-addr 127.0.0.1 --master-port 29511 tools/rank_check.py --mode det --blocks ${BLOCKS:-4} > gpurun_out/rank_det.log 2>&1 || { echo "det failed"; tail -20 gpurun_out/rank_det.log; exit 1; }
+grep -E "world=|RANK_CHECK" gpurun_out/rank_det.log
+timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node $W --master-addr 127.0.0.1 --master-port 29512 tools/rank_check.py --mode fast --blocks ${BLOCKS:-4} > gpurun_out/rank_fast.log 2>&1 || { echo "fast failed"; tail -20 gpurun_out/rank_fast.log; exit 1; }
+grep -E "world=|RANK_CHECK" gpurun_out/rank_fast.log
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $W --master-addr 127.0.0.1 --master-port 29513 bench.py --gpus $W --steps 2 --warmup 1 --scale ${SCALE:-0.1} > gpurun_out/rank_bench.log 2>&1 || { echo "bench failed"; tail -20 gpurun_out/rank_bench.log; exit 1; }
+tail -1 gpurun_out/rank_bench.log

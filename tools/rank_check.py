@@ -26,6 +26,12 @@ def main():
     import torch.distributed as dist
     import mfhip
     from mfhip import _lib as L
+    if os.environ.get("MFHIP_FAKE_HOSTS"):
+        # several ranks on ONE device: RCCL refuses that on one host, so each rank claims its
+        # own host id and the ranks talk over loopback sockets (a rehearsal of the ring)
+        os.environ["NCCL_HOSTID"] = "mfhip-rank" + os.environ.get("RANK", "0")
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     local = int(os.environ.get("LOCAL_RANK", rank))
