@@ -44,6 +44,8 @@ def parse():
                     help="fast-mode factor blocking (reference = new Random(id ^ seed).nextInt(n))")
     ap.add_argument("--traffic-json", default=None, help="rocprof PMC summary to fill roofline.traffic")
     ap.add_argument("--no-profile", action="store_true", help="skip the profiled replay (roofline = null)")
+    ap.add_argument("--item-split", type=int, default=0,
+                    help="fast mode: hot-item replicas, max ratings per item chain per rating block (0 = off)")
     return ap.parse_args()
 
 
@@ -141,6 +143,7 @@ def main():
     p.iterations = a.warmup + a.steps
     p.mode = L.MODE_FAST_F32 if a.mode == "fast" else L.MODE_DETERMINISTIC_F64
     p.fast_waves = a.fast_waves
+    p.fast_item_split = a.item_split
     p.fast_blocking = L.BLOCKING_BALANCED if a.blocking == "balanced" else L.BLOCKING_REFERENCE
     if D.world > 1:
         uid = D.bcast_bytes(mfhip.Context.unique_id() if D.rank == 0 else None)
@@ -219,7 +222,7 @@ def main():
             "config": {"workload": f"{a.config}-shaped DSGD {'fast' if a.mode == 'fast' else 'deterministic'}",
                        "users": int(nu * a.scale), "items": int(ni * a.scale), "ratings": int(nr * a.scale),
                        "train_ratings": int(len(tr)), "rank": k, "num_blocks": nb, "lambda": 1.0, "lr": 0.001,
-                       "lr_method": "Default", "blocking": a.blocking, "groups": st["groups"], "pad_records": st["pads"],
+                       "lr_method": "Default", "blocking": a.blocking, "item_split": a.item_split, "groups": st["groups"], "pad_records": st["pads"],
                        "parallelism": f"dsgd-ring{D.world}"},
             "rmse": round(rmse, 6), "rmse_epochs": a.warmup + a.steps, "rmse_matched": matched,
             "roofline": roof, "cpu_baseline": cpu,

@@ -91,7 +91,11 @@ typedef struct mf_params {
   /* fast-mode blocking: MF_BLOCKING_REFERENCE (default) or MF_BLOCKING_BALANCED;
      the deterministic mode always uses the reference's blocking */
   int32_t fast_blocking;
-  int32_t reserved[6];
+  /* fast-mode hot-item replicas: an item with more than this many ratings in one rating block
+     is swept as ceil(m / fast_item_split) parallel chains averaged when the superstep ends
+     (plan.hpp SplitItem).  0 (default) = off: every item is one sequential chain. */
+  int32_t fast_item_split;
+  int32_t reserved[5];
 } mf_params;
 
 /* Aggregated device statistics (timed with HIP events on the library's stream). */
@@ -221,6 +225,13 @@ int mf_debug_levels(const uint32_t* urow, const uint32_t* irow, const int32_t* o
 int mf_debug_fast_schedule(const int32_t* users, const int32_t* items, int64_t n, int32_t n_blocks,
                            int64_t seed, int32_t groups, int32_t blocking, int32_t window, int32_t* block_out,
                            int32_t* substep_out, int32_t* group_out, int64_t* pos_out);
+/* mf_debug_fast_split: mf_debug_fast_schedule with hot-item replicas (mf_params.fast_item_split
+   = item_split); replica_out[j] = 0 when rating j updates its item's own row, r >= 1 when it
+   updates replica r (merged when the superstep ends). */
+int mf_debug_fast_split(const int32_t* users, const int32_t* items, int64_t n, int32_t n_blocks,
+                        int64_t seed, int32_t groups, int32_t blocking, int32_t window, int32_t item_split,
+                        int32_t* block_out, int32_t* substep_out, int32_t* group_out, int64_t* pos_out,
+                        int32_t* replica_out);
 /* The plan window (records between two uses of a row inside a cell unless adjacent) the fast
    sweep uses at rank k: the prefetch distance of the kernel selected for k. */
 int mf_fast_plan_window(int32_t k, int32_t* window_out);

@@ -58,6 +58,10 @@ void launch_sweep_pair(hipStream_t st, const WaveDesc* waves, int nwaves, const 
 // err[0] is set when a wave gave up waiting.  trace (may be null): per cell {start, end} at
 // [2*(cell index in sys)].
 int sweep_pair_sys_capacity(int k);
+// Hot-item replicas around a fast superstep (plan.hpp SplitItem): fork before the sweep, join
+// after it, on the sweep's stream; n split items, f32 rows of k.
+void launch_split_fork(hipStream_t st, const SplitItem* sp, int n, float* I, int k);
+void launch_split_join(hipStream_t st, const SplitItem* sp, int n, float* I, int k);
 void launch_sweep_pair_sys(hipStream_t st, const SysWave* sw, const WaveDesc* sys, int nw, const PairRec* recs,
                            float* U, float* I, uint64_t u_bytes, uint64_t i_bytes, int k, float eta, int32_t* prog,
                            uint32_t base, int32_t* err, uint64_t* trace, hipEvent_t ev0, hipEvent_t ev1);

@@ -450,4 +450,36 @@ void launch_sweep_pair(hipStream_t st, const WaveDesc* waves, int nwaves, const 
   }
 }
 
+// Hot-item replicas (plan.hpp SplitItem), one workgroup per split item, any k.  fork: the item's
+// row to its R-1 replica rows; join: q = (q + sum_r q_r) / R, replicas in order (deterministic).
+__global__ __launch_bounds__(64) void k_split_fork(const SplitItem* __restrict__ sp, float* __restrict__ I, int k) {
+  const SplitItem h = sp[blockIdx.x];
+  const float* q = I + static_cast<size_t>(h.main_row) * k;
+  float* dst = I + static_cast<size_t>(h.scratch_row) * k;
+  for (int e = threadIdx.x; e < k; e += 64) {
+    const float v = q[e];
+    for (int r = 0; r < h.R - 1; ++r) dst[static_cast<size_t>(r) * k + e] = v;
+  }
+}
+
+__global__ __launch_bounds__(64) void k_split_join(const SplitItem* __restrict__ sp, float* __restrict__ I, int k) {
+  const SplitItem h = sp[blockIdx.x];
+  float* q = I + static_cast<size_t>(h.main_row) * k;
+  const float* rep = I + static_cast<size_t>(h.scratch_row) * k;
+  const float inv = 1.0f / static_cast<float>(h.R);
+  for (int e = threadIdx.x; e < k; e += 64) {
+    float acc = q[e];
+    for (int r = 0; r < h.R - 1; ++r) acc += rep[static_cast<size_t>(r) * k + e];
+    q[e] = acc * inv;
+  }
+}
+
+void launch_split_fork(hipStream_t st, const SplitItem* sp, int n, float* I, int k) {
+  if (n > 0) hipLaunchKernelGGL(k_split_fork, dim3(n), dim3(64), 0, st, sp, I, k);
+}
+
+void launch_split_join(hipStream_t st, const SplitItem* sp, int n, float* I, int k) {
+  if (n > 0) hipLaunchKernelGGL(k_split_join, dim3(n), dim3(64), 0, st, sp, I, k);
+}
+
 }  // namespace mfhip

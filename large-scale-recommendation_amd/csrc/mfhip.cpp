@@ -72,6 +72,8 @@ struct Shard {
   uint32_t sys_base = 0;                // progress-word base of the next systolic launch
   uint32_t sys_step = 1;                // base advance per launch (> the largest G_j)
   DevBuf st_trace;                      // MFHIP_WAVE_TRACE: {start, end} per wave
+  DevBuf st_split;                      // hot-item replicas (SplitItem), superstep-major
+  std::vector<int64_t> st_split_off;    // per superstep (n + 1)
   // evaluation scratch
   DevBuf ev_u, ev_i, ev_r, ev_mult, ev_out, ev_part;
   // profiling
@@ -155,6 +157,7 @@ void validate_params(const mf_params* p) {
   MF_REQUIRE(p->lr_method >= MF_LR_DEFAULT && p->lr_method <= MF_LR_XU, "unknown lr_method");
   MF_REQUIRE(p->fast_blocking == MF_BLOCKING_BALANCED || p->fast_blocking == MF_BLOCKING_REFERENCE,
              "unknown fast_blocking");
+  MF_REQUIRE(p->fast_item_split >= 0, "fast_item_split must be >= 0");
 }
 
 void init_shard(Shard& s, int device, int index) {
@@ -493,6 +496,9 @@ void fast_superstep(mf_ctx* ctx, Shard& s, int64_t superstep, double eta) {
     ups += ctx->fast_rb_size[static_cast<int64_t>(p) * n + q];
   }
   if (ups == 0) return;
+  const int64_t sp0 = s.st_split_off.empty() ? 0 : s.st_split_off[smod];
+  const int nsplit = s.st_split_off.empty() ? 0 : static_cast<int>(s.st_split_off[smod + 1] - sp0);
+  launch_split_fork(s.stream, s.st_split.as<SplitItem>() + sp0, nsplit, s.itf.as<float>(), ctx->P.num_factors);
   if (ctx->fast_pair && ctx->fast_sys) {
     const int64_t w0 = s.st_sys_off[smod], nw = s.st_sys_off[smod + 1] - w0;
     if (nw > 0) {
@@ -537,6 +543,7 @@ void fast_superstep(mf_ctx* ctx, Shard& s, int64_t superstep, double eta) {
     }
     ctx->stats.kernel_launches += ctx->G_fast;
   }
+  launch_split_join(s.stream, s.st_split.as<SplitItem>() + sp0, nsplit, s.itf.as<float>(), ctx->P.num_factors);
   MF_HIP(hipGetLastError());
   ctx->stats.updates += ups;
 }
@@ -687,7 +694,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
       if (ctx->P.fast_waves == 0 && !(bg && std::string(bg) == "0")) {
         block_groups.assign(nb2, 0);
         for (auto& s : ctx->shards) {
-          const auto gb = choose_block_groups(ctx->rb, ctx->I, ctx->c, s.index, simds);
+          const auto gb = choose_block_groups(ctx->rb, ctx->I, ctx->c, s.index, simds, ctx->P.fast_item_split);
           for (int64_t b = 0; b < nb2; ++b)
             if (gb[b] > 0) block_groups[b] = gb[b];
         }
@@ -709,7 +716,10 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
     }
     build_fast_plan(fp, ctx->rb, ctx->U, ctx->I, ctx->G_fast, k, ctx->P.lambda,
                     static_cast<uint64_t>(ctx->P.seed) * 0x9E3779B97F4A7C15ULL + 1, dummy, nullptr,
-                    ctx->fast_pair ? 2 * kPairRing : kHazardWindow, block_groups.empty() ? nullptr : &block_groups);
+                    ctx->fast_pair ? 2 * kPairRing : kHazardWindow, block_groups.empty() ? nullptr : &block_groups,
+                    ctx->P.fast_item_split, static_cast<uint32_t>(ctx->I.rows() + 1));
+    MF_REQUIRE(static_cast<uint64_t>(ctx->I.rows() + 1 + fp.scratch_rows) * k * 4 < (1ull << 32),
+               "hot-item replica rows exceed the 32-bit item slab offsets");
     ctx->stats.pads = fp.pads;
     clk.lap("cell plan");
     {  // priority threshold: 3x the mean non-empty cell length
@@ -737,8 +747,23 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
     ctx->fast_dummy_i = static_cast<uint32_t>(ctx->I.rows());
     for (auto& s : ctx->shards) {
       ensure_rows(ctx, s, kSideU, ctx->U.rows() + 2);
-      ensure_rows(ctx, s, MF_SIDE_ITEM, ctx->I.rows() + 1);
+      ensure_rows(ctx, s, MF_SIDE_ITEM, ctx->I.rows() + 1 + fp.scratch_rows);
       DeviceGuard g(s.device);
+      {  // hot-item replicas of this shard's rating blocks, per superstep
+        std::vector<SplitItem> tab;
+        s.st_split_off.assign(ctx->nb + 1, 0);
+        for (int32_t sm = 0; sm < ctx->nb; ++sm) {
+          for (int32_t j = 0; j < ctx->c; ++j) {
+            const int32_t p = s.index * ctx->c + j;
+            const int64_t b = static_cast<int64_t>(p) * ctx->nb + (p + sm) % ctx->nb;
+            tab.insert(tab.end(), fp.splits.begin() + fp.split_off[b], fp.splits.begin() + fp.split_off[b + 1]);
+          }
+          s.st_split_off[sm + 1] = static_cast<int64_t>(tab.size());
+        }
+        s.st_split.alloc(std::max<size_t>(tab.size(), 1) * sizeof(SplitItem));
+        if (!tab.empty())
+          MF_HIP(hipMemcpy(s.st_split.get(), tab.data(), tab.size() * sizeof(SplitItem), hipMemcpyHostToDevice));
+      }
       const size_t row_bytes = static_cast<size_t>(ctx->P.num_factors) * ctx->es;
       MF_HIP(hipMemset(s.uf.as<char>() + static_cast<size_t>(dummy) * row_bytes, 0, 2 * row_bytes));
       MF_HIP(hipMemset(s.itf.as<char>() + static_cast<size_t>(ctx->fast_dummy_i) * row_bytes, 0, row_bytes));
@@ -1091,6 +1116,7 @@ void mf_params_init(mf_params* p) {
   p->online_learning_rate = 0.01;  // SparkExample.scala:33 SGDUpdater(0.01)
   p->online_init = MF_INIT_PSEUDO_RANDOM;
   p->fast_waves = 0;
+  p->fast_item_split = 0;
 }
 
 const char* mf_last_error(void) { return g_last_error.c_str(); }
@@ -1507,8 +1533,15 @@ int mf_debug_levels(const uint32_t* urow, const uint32_t* irow, const int32_t* o
 int mf_debug_fast_schedule(const int32_t* u, const int32_t* i, int64_t n, int32_t n_blocks, int64_t seed,
                            int32_t groups, int32_t blocking, int32_t window, int32_t* block_out,
                            int32_t* substep_out, int32_t* group_out, int64_t* pos_out) {
+  return mf_debug_fast_split(u, i, n, n_blocks, seed, groups, blocking, window, 0, block_out, substep_out, group_out,
+                             pos_out, nullptr);
+}
+
+int mf_debug_fast_split(const int32_t* u, const int32_t* i, int64_t n, int32_t n_blocks, int64_t seed,
+                        int32_t groups, int32_t blocking, int32_t window, int32_t item_split, int32_t* block_out,
+                        int32_t* substep_out, int32_t* group_out, int64_t* pos_out, int32_t* replica_out) {
   return guarded([&] {
-    MF_REQUIRE(n >= 0 && n_blocks >= 1 && groups != 0, "bad argument");
+    MF_REQUIRE(n >= 0 && n_blocks >= 1 && groups != 0 && item_split >= 0, "bad argument");
     MF_REQUIRE(n == 0 || (u && i && block_out && substep_out && group_out && pos_out), "null argument");
     SideLayout U, I;
     const Blocking bl = blocking == MF_BLOCKING_BALANCED ? Blocking::kBalanced : Blocking::kJvm;
@@ -1520,10 +1553,12 @@ int mf_debug_fast_schedule(const int32_t* u, const int32_t* i, int64_t n, int32_
     FastPlan fp;
     std::vector<int64_t> src;
     std::vector<int32_t> block_groups;  // groups < 0: the systolic per-block choice for -groups waves
-    if (groups < 0) block_groups = choose_block_groups(rb, I, n_blocks, 0, -groups);
+    if (groups < 0) block_groups = choose_block_groups(rb, I, n_blocks, 0, -groups, item_split);
+    const uint32_t scratch_base = static_cast<uint32_t>(I.rows() + 1);
     build_fast_plan(fp, rb, U, I, groups > 0 ? groups : 8, 1, 1.0,
                     static_cast<uint64_t>(seed) * 0x9E3779B97F4A7C15ULL + 1, static_cast<uint32_t>(U.rows()), &src,
-                    window > 0 ? window : kHazardWindow, block_groups.empty() ? nullptr : &block_groups);
+                    window > 0 ? window : kHazardWindow, block_groups.empty() ? nullptr : &block_groups, item_split,
+                    scratch_base);
     const int64_t nb2 = static_cast<int64_t>(n_blocks) * n_blocks;
     for (int64_t b = 0; b < nb2; ++b) {
       if (fp.rec_base[b] < 0) continue;
@@ -1538,6 +1573,15 @@ int mf_debug_fast_schedule(const int32_t* u, const int32_t* i, int64_t n, int32_
           substep_out[j] = static_cast<int32_t>(cidx / G);
           group_out[j] = static_cast<int32_t>(cidx % G);
           pos_out[j] = x - off[cidx];
+          if (replica_out) {  // 0: the item's own row; r: its replica r (scratch row)
+            const uint32_t row = fp.recs[fp.rec_base[b] + x].i & ~kPadBit;
+            int32_t rep = 0;
+            if (row >= scratch_base)
+              for (int64_t h = fp.split_off[b]; h < fp.split_off[b + 1]; ++h)
+                if (row >= fp.splits[h].scratch_row && row < fp.splits[h].scratch_row + fp.splits[h].R - 1)
+                  rep = static_cast<int32_t>(row - fp.splits[h].scratch_row) + 1;
+            replica_out[j] = rep;
+          }
         }
     }
   });

@@ -324,7 +324,8 @@ inline uint32_t mix32(uint64_t x) {
 // of the user inside an item run.
 void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, const SideLayout& I,
                      int32_t G0, int32_t k, double lambda, uint64_t order_seed, uint32_t dummy_row,
-                     std::vector<int64_t>* rec_src, int32_t window, const std::vector<int32_t>* block_groups) {
+                     std::vector<int64_t>* rec_src, int32_t window, const std::vector<int32_t>* block_groups,
+                     int32_t split_run, uint32_t scratch_base) {
   const int64_t kHazardWindow = window;  // shadows the default for this plan
   const uint32_t row_bytes = static_cast<uint32_t>(k) * 4u;
   const int32_t nb = rb.n_blocks;
@@ -346,6 +347,38 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
   std::vector<std::vector<int64_t>> srcs(nblk);
   std::vector<std::vector<int32_t>> offs(nblk);
   std::vector<int64_t> pads(nblk, 0);
+  // hot-item replicas: per block, the items with more than split_run ratings and their R
+  std::vector<std::vector<std::pair<uint32_t, int32_t>>> hot(nblk);
+  if (split_run > 0)
+    parallel_tasks(nblk, [&](int64_t bx) {
+      const int64_t b = blocks[bx];
+      const int32_t q = static_cast<int32_t>(b % nb);
+      const int64_t ib = I.block_start[q], ni = I.block_start[q + 1] - ib;
+      std::vector<int32_t> cnt(ni, 0);
+      for (int64_t j = rb.start[b]; j < rb.start[b + 1]; ++j) cnt[rb.irow[j] - ib]++;
+      for (int64_t il = 0; il < ni; ++il)
+        if (cnt[il] > split_run)
+          hot[bx].push_back({static_cast<uint32_t>(il), static_cast<int32_t>((cnt[il] + split_run - 1) / split_run)});
+    });
+  fp.split_off.assign(nb2 + 1, 0);
+  std::vector<int64_t> split_first(nblk, 0);
+  {
+    uint32_t cursor = 0;
+    for (int64_t bx = 0, b = 0; b < nb2; ++b) {
+      fp.split_off[b + 1] = fp.split_off[b];
+      if (bx < nblk && blocks[bx] == b) {
+        const int32_t q = static_cast<int32_t>(b % nb);
+        split_first[bx] = static_cast<int64_t>(fp.splits.size());
+        for (const auto& h : hot[bx]) {
+          fp.splits.push_back(SplitItem{static_cast<uint32_t>(I.block_start[q]) + h.first, scratch_base + cursor, h.second});
+          cursor += static_cast<uint32_t>(h.second - 1);
+        }
+        fp.split_off[b + 1] = static_cast<int64_t>(fp.splits.size());
+        ++bx;
+      }
+    }
+    fp.scratch_rows = cursor;
+  }
   parallel_tasks(nblk, [&](int64_t bx) {
     const int64_t b = blocks[bx];
     const int32_t G = fp.Gb[b];
@@ -354,15 +387,46 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
     const int64_t ub = U.block_start[p], nu = U.block_start[p + 1] - ub;
     const int64_t ib = I.block_start[q], ni = I.block_start[q + 1] - ib;
     const int64_t s = rb.start[b], len = rb.size(b);
-    std::vector<int64_t> lu(nu, 0), li(ni, 0);
-    for (int64_t j = s; j < s + len; ++j) { lu[rb.urow[j] - ub]++; li[rb.irow[j] - ib]++; }
+    // virtual local items: 0..ni-1 the block's items, ni.. the replicas 1..R-1 of its hot items
+    // (a hot item's ratings go round-robin to its R chains in block order)
+    std::vector<uint32_t> vil(len), vrow;     // rating -> virtual item; virtual item -> global row
+    std::vector<uint32_t> vreal;              // virtual item -> the item's own global row (omega)
+    int64_t nv = ni;
+    {
+      std::vector<int32_t> hix(ni, -1), seen;
+      std::vector<int64_t> vbase;
+      const auto& hb = hot[bx];
+      for (size_t h = 0; h < hb.size(); ++h) {
+        hix[hb[h].first] = static_cast<int32_t>(h);
+        vbase.push_back(nv);
+        nv += hb[h].second - 1;
+      }
+      seen.assign(hb.size(), 0);
+      vrow.resize(nv);
+      vreal.resize(nv);
+      for (int64_t il = 0; il < ni; ++il) vrow[il] = vreal[il] = static_cast<uint32_t>(ib + il);
+      for (size_t h = 0; h < hb.size(); ++h)
+        for (int32_t r = 1; r < hb[h].second; ++r) {
+          vrow[vbase[h] + r - 1] = fp.splits[split_first[bx] + h].scratch_row + static_cast<uint32_t>(r - 1);
+          vreal[vbase[h] + r - 1] = static_cast<uint32_t>(ib + hb[h].first);
+        }
+      for (int64_t x = 0; x < len; ++x) {
+        const uint32_t il = rb.irow[s + x] - static_cast<uint32_t>(ib);
+        const int32_t h = hix[il];
+        if (h < 0) { vil[x] = il; continue; }
+        const int32_t r = seen[h]++ % hb[h].second;
+        vil[x] = r == 0 ? il : static_cast<uint32_t>(vbase[h] + r - 1);
+      }
+    }
+    std::vector<int64_t> lu(nu, 0), li(nv, 0);
+    for (int64_t x = 0; x < len; ++x) { lu[rb.urow[s + x] - ub]++; li[vil[x]]++; }
     std::vector<int32_t> gu, gi;
     lpt_groups(lu, G, gu);
     lpt_groups(li, G, gi);
     std::vector<std::pair<uint64_t, int64_t>> key(len);
     for (int64_t x = 0; x < len; ++x) {
       const int64_t j = s + x;
-      const uint32_t il = rb.irow[j] - static_cast<uint32_t>(ib);
+      const uint32_t il = vil[x];
       const uint32_t ul = rb.urow[j] - static_cast<uint32_t>(ub);
       const int32_t g = gi[il], h = gu[ul];
       const int64_t t = ((h - g) % G + G) % G;
@@ -413,7 +477,7 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
     out.reserve(len + len / 8 + 16);
     if (rec_src) src.reserve(len + len / 8 + 16);
     off.assign(GG + 1, 0);
-    std::vector<std::pair<int64_t, int64_t>> last_u(nu, {-1, 0}), last_i(ni, {-1, 0});
+    std::vector<std::pair<int64_t, int64_t>> last_u(nu, {-1, 0}), last_i(nv, {-1, 0});
     std::vector<std::pair<int64_t, int32_t>> uslot(nu, {-1, 0});
     struct Ent { uint32_t ul, il; int32_t ug, ig; int64_t j; };
     struct Grp { std::vector<int32_t> e; size_t head = 0; int32_t left = 0; uint32_t row = 0; };
@@ -429,7 +493,7 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
       ugs.clear();
       while (x < len && static_cast<int64_t>(key[x].first >> 40) == c) {
         const int64_t j = s + key[x].second;
-        const uint32_t il = rb.irow[j] - static_cast<uint32_t>(ib), ul = rb.urow[j] - static_cast<uint32_t>(ub);
+        const uint32_t il = vil[key[x].second], ul = rb.urow[j] - static_cast<uint32_t>(ub);
         if (igs.empty() || ents.back().il != il) { igs.emplace_back(); igs.back().row = il; }
         auto& us = uslot[ul];
         if (us.first != c) { us = {c, static_cast<int32_t>(ugs.size())}; ugs.emplace_back(); }
@@ -510,11 +574,11 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
         prev_ig = en.ig;
         const int64_t j = en.j;
         const uint32_t urow = rb.urow[j];
-        prev_irow = rb.irow[j];
+        prev_irow = vrow[en.il];
         out.push_back(FastRec{urow * row_bytes, prev_irow * row_bytes, static_cast<float>(rb.r[j]),
                               static_cast<float>(lambda / static_cast<double>(U.omega[urow])),
-                              static_cast<float>(lambda / static_cast<double>(I.omega[prev_irow])), urow, prev_irow,
-                              0});
+                              static_cast<float>(lambda / static_cast<double>(I.omega[vreal[en.il]])), urow,
+                              prev_irow, 0});
         if (rec_src) src.push_back(j);
       }
       off[c + 1] = static_cast<int32_t>(out.size());
@@ -753,7 +817,7 @@ void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, in
 }
 
 std::vector<int32_t> choose_block_groups(const RatingBlocks& rb, const SideLayout& I, int32_t c, int32_t shard,
-                                         int32_t waves) {
+                                         int32_t waves, int32_t split_run) {
   const int32_t nb = rb.n_blocks;
   const int64_t nb2 = static_cast<int64_t>(nb) * nb;
   std::vector<int32_t> Gb(nb2, 0);
@@ -766,7 +830,7 @@ std::vector<int32_t> choose_block_groups(const RatingBlocks& rb, const SideLayou
     int32_t mx = 0;
     for (int64_t x = rb.start[b]; x < rb.start[b + 1]; ++x) mx = std::max(mx, ++cnt[rb.irow[x] - ib]);
     size[b] = rb.size(b);
-    top[b] = mx;
+    top[b] = split_run > 0 ? std::min(mx, split_run) : mx;
   });
   double cell_ns = kSysCellNs, pair_ns = kSysPairNs, run_ns = kSysRunPairNs;
   if (const char* v = std::getenv("MFHIP_SYS_MODEL"))  // tuning knob: "cell_ns,pair_ns,run_pair_ns"

@@ -112,6 +112,22 @@ struct FastRec {
 };
 static_assert(sizeof(FastRec) == 32, "FastRec is two 16-B words");
 
+// Hot-item replicas (fast mode, opt-in `split_run`): inside one rating block an item with m >
+// split_run ratings is swept as R = ceil(m / split_run) independent chains -- replica 0 is the
+// item's own row, replicas 1..R-1 are scratch rows -- and averaged when the superstep ends:
+//   fork:  scratch[0 .. R-2] = q
+//   join:  q = (q + sum_{r=1..R-1} q_r) / R
+// (iterative parameter mixing; a delta sum q0 + sum_r (q_r - q0) diverges: each chain of
+// thousands of updates converges on its own, and R such corrections overshoot R-fold).
+// Every in-flight update still owns the physical rows it touches (no atomics), but the item's
+// updates are no longer one sequential chain: a relaxation of DSGDforMF.scala:404-413 that
+// shortens the hottest item's chain by R (fast mode is judged on held-out RMSE, not order).
+struct SplitItem {
+  uint32_t main_row;     // the item's global row
+  uint32_t scratch_row;  // first of R-1 scratch rows: replicas 1..R-1
+  int32_t R;
+};
+
 struct FastPlan {
   int32_t G = 4;                       // rotation groups per rating block (the largest when per-block)
   std::vector<int32_t> Gb;             // per rating block (n*n): its rotation groups
@@ -120,6 +136,9 @@ struct FastPlan {
   std::vector<int32_t> cell_off;       // per included rating block: Gb*Gb+1 relative offsets
   std::vector<int64_t> cell_base;      // per rating block: index into cell_off (-1 if absent)
   int64_t pads = 0;                    // padding records inserted
+  std::vector<SplitItem> splits;       // hot-item replicas, grouped by rating block
+  std::vector<int64_t> split_off;      // n*n + 1: rating block b owns splits [split_off[b], split_off[b+1])
+  uint32_t scratch_rows = 0;           // scratch item rows used from scratch_base on
 };
 
 // ---------------------------------------------------------------------------------------
@@ -197,10 +216,12 @@ int32_t choose_groups(int64_t avg_block_ratings, int32_t blocks_per_device, int3
 // window: a row recurs inside a cell only at the next position or >= window positions later
 // (the kernel's prefetch distance; kHazardWindow for kernels_fast.hip).
 // block_groups (optional, n*n): per rating block rotation groups (0 = G); otherwise G for all.
+// split_run > 0: hot-item replicas (SplitItem) with scratch item rows from scratch_base on.
 void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, const SideLayout& I,
                      int32_t G, int32_t k, double lambda, uint64_t order_seed, uint32_t dummy_row,
                      std::vector<int64_t>* rec_src = nullptr, int32_t window = kHazardWindow,
-                     const std::vector<int32_t>* block_groups = nullptr);
+                     const std::vector<int32_t>* block_groups = nullptr, int32_t split_run = 0,
+                     uint32_t scratch_base = 0);
 
 // Rotation groups per rating block for the systolic sweep, where every rating block of a
 // superstep is its own G_j x G_j grid and only the superstep's longest wave matters.  For each
@@ -211,7 +232,8 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
 constexpr double kSysCellNs = 4000.0;     // per-cell start, drain, hand-off and waiting (tuned, NFLX)
 constexpr double kSysPairNs = 300.0;      // mixed-cell pair step incl. no-op halves and group imbalance (tuned)
 constexpr double kSysRunPairNs = 186.0;   // single-item-run pair step (wave trace)
+// split_run > 0: an item's run counts at most split_run ratings (hot-item replicas).
 std::vector<int32_t> choose_block_groups(const RatingBlocks& rb, const SideLayout& I, int32_t c, int32_t shard,
-                                         int32_t waves);
+                                         int32_t waves, int32_t split_run = 0);
 
 }  // namespace mfhip

@@ -66,7 +66,8 @@ class mf_params(C.Structure):
         ("online_init", C.c_int32),
         ("fast_waves", C.c_int32),
         ("fast_blocking", C.c_int32),
-        ("reserved", C.c_int32 * 6),
+        ("fast_item_split", C.c_int32),
+        ("reserved", C.c_int32 * 5),
     ]
 
 
@@ -93,7 +94,7 @@ EXPORTS = [
     "mf_get_factors", "mf_set_factors", "mf_predict", "mf_rmse", "mf_empirical_risk",
     "mf_block_update", "mf_online_update", "mf_lookup", "mf_set_profiling", "mf_get_stats",
     "mf_reset_stats", "mf_jvm_shuffle", "mf_jvm_block_of", "mf_jvm_random_factors",
-    "mf_learning_rate", "mf_debug_levels", "mf_debug_fast_schedule", "mf_fast_plan_window",
+    "mf_learning_rate", "mf_debug_levels", "mf_debug_fast_schedule", "mf_debug_fast_split", "mf_fast_plan_window",
     "mf_fast_kernel_name", "mf_get_params", "mf_read_ratings", "mf_save_model", "mf_load_model",
 ]
 
@@ -152,6 +153,8 @@ def lib() -> C.CDLL:
         "mf_debug_levels": (C.c_int, [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), _i32p, C.c_int64, _i32p]),
         "mf_debug_fast_schedule": (C.c_int, [_i32p, _i32p, C.c_int64, C.c_int32, C.c_int64, C.c_int32, C.c_int32,
                                              C.c_int32, _i32p, _i32p, _i32p, _i64p]),
+        "mf_debug_fast_split": (C.c_int, [_i32p, _i32p, C.c_int64, C.c_int32, C.c_int64, C.c_int32, C.c_int32,
+                                          C.c_int32, C.c_int32, _i32p, _i32p, _i32p, _i64p, _i32p]),
         "mf_fast_plan_window": (C.c_int, [C.c_int32, _i32p]),
         "mf_fast_kernel_name": (C.c_char_p, [C.c_int32]),
         "mf_get_params": (C.c_int, [C.c_void_p, C.POINTER(mf_params)]),

@@ -64,6 +64,49 @@ def fast_schedule(u, i, nb, seed, G, blocking=L.BLOCKING_REFERENCE, window=0):
     return b, t, g, p
 
 
+def fast_schedule_split(u, i, nb, seed, G, item_split, blocking=L.BLOCKING_REFERENCE, window=0):
+    """fast_schedule plus the hot-item replica each rating updates (0 = the item's own row)."""
+    n = len(u)
+    b = np.empty(n, np.int32); t = np.empty(n, np.int32); g = np.empty(n, np.int32); p = np.empty(n, np.int64)
+    r = np.empty(n, np.int32)
+    L.check(L.lib().mf_debug_fast_split(L.ptr(L.as_i32(u), C.c_int32), L.ptr(L.as_i32(i), C.c_int32), n, nb,
+                                        seed, G, blocking, window, item_split, L.ptr(b, C.c_int32),
+                                        L.ptr(t, C.c_int32), L.ptr(g, C.c_int32), L.ptr(p, C.c_int64),
+                                        L.ptr(r, C.c_int32)))
+    return b, t, g, p, r
+
+
+@pytest.mark.parametrize("nb,G,split", [(1, 8, 50), (2, 8, 30), (3, -64, 40), (2, 16, 7)])
+def test_hot_item_replicas_split_and_stay_conflict_free(nb, G, split):
+    """fast_item_split: an item with m > split ratings in a rating block is swept as
+    R = ceil(m / split) chains of at most `split` ratings (round-robin), each chain its own
+    physical row, and within a (stratum, sub-step) no physical row appears in two cells."""
+    d = synth.generate(500, 200, 20000, seed=2)
+    b, t, g, p, rep = fast_schedule_split(d.u, d.i, nb, 3, G, split)
+    b0, t0, g0, p0 = fast_schedule(d.u, d.i, nb, 3, G)
+    assert np.array_equal(b, b0)  # the blocking does not change
+    assert rep.max() > 0  # some item was split
+    for x in np.unique(b):
+        m = b == x
+        items, cnt = np.unique(d.i[m], return_counts=True)
+        for it, c in zip(items.tolist(), cnt.tolist()):
+            rr = rep[m & (d.i == it)]
+            R = -(-c // split) if c > split else 1
+            assert rr.max() == R - 1 and rr.min() == 0
+            assert np.bincount(rr, minlength=R).max() <= split
+    Gmax = int(g.max()) + 1
+    for s in range(nb):
+        in_stratum = ((b // nb + s) % nb) == (b % nb)
+        for tt in np.unique(t[in_stratum]):
+            m = in_stratum & (t == tt)
+            cell = b[m].astype(np.int64) * Gmax + g[m]
+            phys_item = d.i[m].astype(np.int64) * 4096 + rep[m]
+            for ids in (d.u[m].astype(np.int64), phys_item):
+                owner = {}
+                for x, c in zip(ids.tolist(), cell.tolist()):
+                    assert owner.setdefault(x, c) == c
+
+
 @pytest.mark.parametrize("nb,G,window", [(1, 4, 0), (3, 8, 0), (4, 16, 0), (3, 8, 32), (2, 4, 16), (3, -64, 14),
                                          (2, -16, 14)])
 def test_fast_rotation_is_conflict_free(nb, G, window):
