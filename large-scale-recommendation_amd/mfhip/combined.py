@@ -82,3 +82,67 @@ class OnlineOfflineSpark:
         if checkpoint and self.snapshot_dir:
             self.ctx.save(os.path.join(self.snapshot_dir, f"model_{self._batches:06d}.mfsnap"))
         return ({int(a): v for a, v in zip(users, uv)}, {int(a): v for a, v in zip(items, iv)}, offline)
+
+
+class PSOfflineOnlineMF:
+    """Parameter-server offline + online model (fl/mf/PSOfflineOnlineMF.scala:28-359) on GPU-resident
+    factors, in its sequential serialisation (one worker, one PS shard, pull limits 1: every pull is
+    answered before the next is sent, so the asynchronous protocol reduces to arrival order).
+
+      * online (Online state, :139-149, :157-181): each rating is appended to the history `rs` and
+        applied with SGDUpdater.delta -- user += delta_u on the worker, item += delta_i on the PS
+        (:169-173, :250-252) -- i.e. MF_ONLINE_DELTA in arrival order;
+      * batch trigger (:75-137): the PS drops every item vector (`params.clear()`, :287), the
+        worker keeps its user vectors, then `iterations` passes over `rs` in insertion order (the
+        `Random.shuffle(rs)` result is discarded, :113) re-pull items, which re-initialise from the
+        FactorInitializer on first touch (:247-252), and push deltas (Batch state, :322-330).
+        Ratings arriving during a batch are queued and applied online after it (:221-226), which
+        is what calling `process` after `batch` does.
+    Returned vectors are the model state after the call; the per-rating worker output quirk
+    (`userVec + deltaItemVec`, :176) is not materialised."""
+
+    def __init__(self, num_factors: int, learning_rate: float = 0.01, iterations: int = 10,
+                 init: str = "pseudo_random", seed: int = 0, mode: str = "deterministic"):
+        self.k = num_factors
+        self.iterations = iterations
+        p = L.default_params()
+        p.num_factors = num_factors
+        p.online_learning_rate = learning_rate
+        p.online_init = L.INIT_SEEDED if init == "seeded" else L.INIT_PSEUDO_RANDOM
+        p.seed = seed
+        p.mode = L.MODE_FAST_F32 if mode == "fast" else L.MODE_DETERMINISTIC_F64
+        self._params = p
+        self.ctx = Context(p)
+        self._hist = ([], [], [])  # rs (:54)
+
+    def close(self) -> None:
+        self.ctx.close()
+
+    def _vectors(self, users, items) -> Tuple[Dict[int, np.ndarray], Dict[int, np.ndarray]]:
+        uv, _ = self.ctx.lookup(L.SIDE_USER, users)
+        iv, _ = self.ctx.lookup(L.SIDE_ITEM, items)
+        return {int(a): v for a, v in zip(users, uv)}, {int(a): v for a, v in zip(items, iv)}
+
+    def process(self, u, i, r) -> Tuple[Dict[int, np.ndarray], Dict[int, np.ndarray]]:
+        """Online ratings in arrival order; returns the touched user and item vectors."""
+        u = np.ascontiguousarray(u, np.int32)
+        i = np.ascontiguousarray(i, np.int32)
+        r = np.ascontiguousarray(r, np.float64)
+        for dst, src in zip(self._hist, (u, i, r)):
+            dst.append(src)
+        self.ctx.online_update(u, i, r, L.ONLINE_DELTA)
+        return self._vectors(np.unique(u), np.unique(i))
+
+    def batch(self) -> Tuple[Dict[int, np.ndarray], Dict[int, np.ndarray]]:
+        """Batch training over the whole history; returns every user and item vector."""
+        if not self._hist[0]:
+            return {}, {}
+        hu, hi, hr = (np.concatenate(x) for x in self._hist)
+        uids, uvecs = self.ctx.factors(L.SIDE_USER)
+        fresh = Context(self._params)  # PS params.clear(): items re-initialise on first pull
+        fresh.set_factors(L.SIDE_USER, uids, uvecs)  # worker userVectors survive the batch
+        for _ in range(self.iterations):
+            fresh.online_update(hu, hi, hr, L.ONLINE_DELTA)
+        self.ctx.close()
+        self.ctx = fresh
+        return self._vectors(np.unique(hu), np.unique(hi))

@@ -105,3 +105,39 @@ def test_combined_offline_online_matches_oracle(tmp_path):
             assert np.array_equal(v, np.array(items[x])), (b, "item", x)
     assert sorted(os.listdir(tmp_path)) == ["model_000005.mfsnap"]
     m.close()
+
+
+@pytest.mark.gpu
+def test_ps_offline_online_matches_oracle():
+    """PSOfflineOnlineMF.offlineOnlinePS (fl/mf/PSOfflineOnlineMF.scala:28-359), sequential
+    serialisation: online delta updates in arrival order; a batch trigger clears the PS item
+    vectors, keeps the worker's user vectors and replays the history `iterations` times in
+    insertion order.  Bit-exact against the oracle's composition of the same delta updates."""
+    from mfhip import synth
+    from mfhip.combined import PSOfflineOnlineMF
+    d = synth.generate(90, 50, 1500, seed=13)
+    k, lr, iters = 5, 0.02, 3
+    m = PSOfflineOnlineMF(k, lr, iterations=iters)
+    users, items, hist = {}, {}, []
+    steps = ["o", "o", "b", "o", "o", "o", "b", "o"]
+    x = 0
+    for s in steps:
+        if s == "o":
+            u, i, r = d.u[x:x + 250], d.i[x:x + 250], d.r[x:x + 250]
+            x += 250
+            rs = list(zip(u.tolist(), i.tolist(), r.tolist()))
+            hist += rs
+            uu, iu = m.process(u, i, r)
+            O.online_sequential(rs, users, items, k, lr, "delta")
+            assert set(uu) == set(u.tolist()) and set(iu) == set(i.tolist())
+        else:
+            uu, iu = m.batch()
+            items = {}
+            for _ in range(iters):
+                O.online_sequential(hist, users, items, k, lr, "delta")
+            assert set(uu) == set(users) and set(iu) == set(items)
+        for a, v in uu.items():
+            assert np.array_equal(v, np.array(users[a])), (s, "user", a)
+        for a, v in iu.items():
+            assert np.array_equal(v, np.array(items[a])), (s, "item", a)
+    m.close()

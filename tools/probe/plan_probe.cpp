@@ -1,6 +1,7 @@
 // Host-only probe of the fast pair plan (no GPU): reads ratings written by tools/probe/dump_ratings.py,
 // builds the systolic plan exactly as mf_dsgd_prepare does on one device, and prints per-superstep
 // wave statistics.  Build: make -C tools/probe
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -8,6 +9,14 @@
 #include "plan.hpp"
 
 using namespace mfhip;
+
+static double lap() {
+  static auto t = std::chrono::steady_clock::now();
+  const auto now = std::chrono::steady_clock::now();
+  const double d = std::chrono::duration<double>(now - t).count();
+  t = now;
+  return d;
+}
 
 template <class T>
 std::vector<T> load(const char* path) {
@@ -31,17 +40,23 @@ int main(int argc, char** argv) {
   std::snprintf(p, sizeof p, "%s/probe_i.bin", dir); auto i = load<int32_t>(p);
   std::snprintf(p, sizeof p, "%s/probe_r.bin", dir); auto r = load<double>(p);
   const int64_t n = static_cast<int64_t>(u.size());
+  lap();
   SideLayout U, I;
   build_side(U, u.data(), n, nb, 0, true);
   build_side(I, i.data(), n, nb, 0, true);
+  std::printf("build_side x2 %.3f s\n", lap());
   RatingBlocks rb;
   build_rating_blocks(rb, U, I, u.data(), i.data(), r.data(), n, 0, nb, false);
+  std::printf("rating blocks %.3f s\n", lap());
   const auto Gb = choose_block_groups(rb, I, nb, 0, waves);
+  std::printf("block groups %.3f s\n", lap());
   FastPlan fp;
   build_fast_plan(fp, rb, U, I, 128, k, 1.0, 0 * 0x9E3779B97F4A7C15ULL + 1, static_cast<uint32_t>(U.rows()), nullptr,
                   2 * kPairRing, &Gb);
+  std::printf("fast plan %.3f s\n", lap());
   PairPlan pp;
   build_pair_plan(pp, fp, nb, nb, 0, k, false);
+  std::printf("pair plan %.3f s\n", lap());
   std::printf("pads %lld noop halves %lld pairs %zu\n", (long long)fp.pads, (long long)pp.noop_halves, pp.recs.size());
   for (int sm = 0; sm < nb; ++sm) {
     int64_t maxp = 0, maxw = -1, singles = 0, waves_sm = pp.sys_off[sm + 1] - pp.sys_off[sm];
