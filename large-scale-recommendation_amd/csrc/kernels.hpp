@@ -75,4 +75,13 @@ void launch_predict(hipStream_t st, const int32_t* urow, const int32_t* irow, in
                     const void* U, const void* I, int k, bool f64, double* out, const double* r,
                     const int32_t* mult, double lambda, double* partials);
 
+// Initial factor rows on the device (DSGDforMF.scala:548-549, MatrixFactorization.scala:278-280):
+// row x, factor f = the f-th nextDouble of new Random(ids[x] ^ seed) (xor_seed) or of
+// new Random(ids[x]).  One thread per element: the JVM LCG state after m steps is
+// jump[2(m-1)] * s0 + jump[2(m-1)+1] mod 2^48 (host table, m = 1..2k), so every element is
+// computed independently and written coalesced; bit-exact with JavaRandom::nextDouble.
+// out: rows x k, double (f64) or float (rounded from the same double).
+void launch_jvm_init_rows(hipStream_t st, const int32_t* ids, int64_t rows, int k, bool xor_seed, int64_t seed,
+                          const uint64_t* jump, void* out, bool f64);
+
 }  // namespace mfhip

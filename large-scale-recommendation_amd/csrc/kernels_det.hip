@@ -13,6 +13,8 @@
 // design; the fast path (kernels_fast.hip) is the throughput path.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "kernels.hpp"
 
 namespace mfhip {
@@ -174,6 +176,28 @@ void level_dispatch(hipStream_t st, const DetEntry* e, int64_t n, void* U, void*
   else hipLaunchKernelGGL((k_level<T, 8, ARITH>), grid, block, 0, st, e, n, u, i, ru, ri, k, et);
 }
 
+// JVM LCG with jump-ahead (java.util.Random, JDK 8): element (x, f) needs the states after
+// 2f+1 and 2f+2 steps from the scrambled seed; nextDouble = ((next(26) << 27) + next(27)) * 2^-53.
+template <typename T>
+__global__ __launch_bounds__(256) void k_jvm_init_rows(const int32_t* __restrict__ ids, int64_t rows, int k,
+                                                       int xor_seed, int64_t seed, const uint64_t* __restrict__ jump,
+                                                       T* __restrict__ out) {
+  constexpr uint64_t kMult = 0x5DEECE66DULL, kMask = (1ULL << 48) - 1;
+  const int64_t total = rows * k;
+  for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < total;
+       e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t x = e / k;
+    const int f = static_cast<int>(e - x * k);
+    const int64_t id = ids[x];
+    const uint64_t s0 = (static_cast<uint64_t>(xor_seed ? (id ^ seed) : id) ^ kMult) & kMask;
+    const uint64_t s1 = (jump[4 * f] * s0 + jump[4 * f + 1]) & kMask;      // after 2f+1 steps
+    const uint64_t s2 = (jump[4 * f + 2] * s0 + jump[4 * f + 3]) & kMask;  // after 2f+2 steps
+    const int64_t hi = static_cast<int32_t>(static_cast<uint32_t>(s1 >> 22));  // next(26)
+    const int64_t lo = static_cast<int32_t>(static_cast<uint32_t>(s2 >> 21));  // next(27)
+    out[e] = static_cast<T>(static_cast<double>((hi << 27) + lo) * 0x1.0p-53);
+  }
+}
+
 template <typename T>
 void predict_dispatch(hipStream_t st, const int32_t* ur, const int32_t* ir, int64_t n, const void* U,
                       const void* I, int k, double* out, const double* r, const int32_t* mult,
@@ -210,6 +234,19 @@ void launch_predict(hipStream_t st, const int32_t* urow, const int32_t* irow, in
   const int g = predict_grid(n);
   if (f64) predict_dispatch<double>(st, urow, irow, n, U, I, k, out, r, mult, lambda, partials, g);
   else predict_dispatch<float>(st, urow, irow, n, U, I, k, out, r, mult, lambda, partials, g);
+}
+
+void launch_jvm_init_rows(hipStream_t st, const int32_t* ids, int64_t rows, int k, bool xor_seed, int64_t seed,
+                          const uint64_t* jump, void* out, bool f64) {
+  const int64_t total = rows * k;
+  if (total <= 0) return;
+  const unsigned grid = static_cast<unsigned>(std::min<int64_t>((total + 255) / 256, 65536));
+  if (f64)
+    hipLaunchKernelGGL((k_jvm_init_rows<double>), dim3(grid), dim3(256), 0, st, ids, rows, k, xor_seed ? 1 : 0, seed,
+                       jump, static_cast<double*>(out));
+  else
+    hipLaunchKernelGGL((k_jvm_init_rows<float>), dim3(grid), dim3(256), 0, st, ids, rows, k, xor_seed ? 1 : 0, seed,
+                       jump, static_cast<float*>(out));
 }
 
 }  // namespace mfhip

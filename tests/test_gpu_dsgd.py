@@ -73,6 +73,26 @@ def test_deterministic_vs_c_oracle_shapes(k, nb, seed):
             assert np.array_equal(vecs, rvecs)
 
 
+@pytest.mark.parametrize("mode,k,seed", [(L.MODE_DETERMINISTIC_F64, 10, 0), (L.MODE_DETERMINISTIC_F64, 130, -77),
+                                         (L.MODE_FAST_F32, 128, 3), (L.MODE_FAST_F32, 64, 0)])
+def test_device_factor_init_bit_exact(mode, k, seed):
+    """Initial rows generated on the GPU (launch_jvm_init_rows, LCG jump-ahead) equal k x nextDouble
+    of new Random(id ^ seed) (DSGDforMF.scala:548-549) -- f64 bitwise, f32 = the rounded double --
+    incl. negative ids and seed, before any superstep runs."""
+    d = synth.generate(500, 200, 6000, seed=21)
+    u = d.u.copy()
+    u[::97] = -u[::97] - 5  # negative ids
+    with mfhip.Context(params(k, 1, 3, seed, mode=mode)) as ctx:
+        ctx.prepare(u, d.i, d.r)
+        ctx.sync()
+        for side in (0, 1):
+            ids, vecs = ctx.factors(side)
+            want = np.array([O.random_factors(k, O.JavaRandom(int(x) ^ seed)) for x in ids])
+            if mode == L.MODE_FAST_F32:
+                want = want.astype(np.float32).astype(np.float64)
+            assert np.array_equal(vecs, want)
+
+
 @pytest.mark.parametrize("method,arg", [(1, 0.0), (2, 50.0), (3, 0.5), (4, 0.7)])
 def test_learning_rate_methods_bit_exact(method, arg):
     d = synth.generate(200, 100, 4000, seed=4)
