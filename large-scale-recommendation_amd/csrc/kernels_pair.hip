@@ -349,9 +349,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     int32_t* __restrict__ prog, uint32_t base, int32_t* __restrict__ err, uint64_t* __restrict__ trace) {
   const int lane = threadIdx.x;
   // blocks b and b+8 share an XCD: give each XCD a contiguous range of waves, so most hand-offs
-  // (g+1 -> g) stay inside one L2 (speed only; correctness does not depend on it)
+  // (g+1 -> g) stay inside one L2 (speed only; correctness does not depend on it).  XCD x holds
+  // nw/8 blocks, plus one when x < nw%8: a bijection for any nw.
   const int b = static_cast<int>(blockIdx.x);
-  const int L = (nw % 8 == 0) ? (b % 8) * (nw / 8) + b / 8 : b;
+  const int x = b % 8, per = nw / 8, extra = nw % 8;
+  const int L = x * per + min(x, extra) + b / 8;
   const SysWave w = sw[L];
   const WaveDesc* my = sys + w.cell0;
   int32_t* my_prog = prog + static_cast<int64_t>(L) * kProgStride;
