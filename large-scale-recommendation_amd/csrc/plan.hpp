@@ -229,7 +229,7 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
 // longest wave under a common bound T, with T minimal such that sum_j G_j <= waves.  A wave's
 // time is modelled as G cells x kSysCellNs + max(block ratings / G, ratings of the block's
 // most rated item) / 2 pairs x ns per pair (no group is lighter than one item's run).
-constexpr double kSysCellNs = 4000.0;     // per-cell start, drain, hand-off and waiting (tuned, NFLX)
+constexpr double kSysCellNs = 6000.0;     // per-cell start, drain, hand-off and waiting (swept on NFLX + ML20M)
 constexpr double kSysPairNs = 300.0;      // mixed-cell pair step incl. no-op halves and group imbalance (tuned)
 constexpr double kSysRunPairNs = 186.0;   // single-item-run pair step (wave trace)
 // split_run > 0: an item's run counts at most split_run ratings (hot-item replicas).
