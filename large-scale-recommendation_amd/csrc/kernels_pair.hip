@@ -215,7 +215,7 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const u4v* __restric
       for (int s = 0; s < CH; ++s) {
         if (c * CH + s >= npairs) goto run_done;
         const int slot = s % DS;
-        const uint32_t fl = rl(C0.flags, s);
+        const uint32_t fl = rl(C0.flags, s), osa = rl(C0.sa, s);
         const float kfa = static_cast<float>(fl & 0xFFu), kfb = static_cast<float>((fl >> 8) & 0xFFu);
         Row<KPL> pa;
         const Row<KPL> pb = RB[slot];
@@ -235,7 +235,7 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const u4v* __restric
           plB.v[e] = bb * b0 + wb * q1;
           q.v[e] = ab * q1 + wb * b0;
         }
-        st<KPL, UP>(urs, voff, rl(C0.sa, s), plA);
+        st<KPL, UP>(urs, voff, osa, plA);
         st<KPL, UP>(urs, voff, ob[slot], plB);
         uint32_t oa;
         if (s + DS < CH) { oa = rl(C0.ua, s + DS); ob[slot] = rl(C0.ub, s + DS); }
@@ -273,6 +273,9 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const u4v* __restric
         if (c * CH + s >= npairs) return;
         const int slot = s % D;
         const uint32_t fl = rl(C0.flags, s);
+        // store offsets named up front: the scheduler then reads them early instead of right
+        // before each store (a v_readlane feeding a buffer store's soffset costs an s_nop 4)
+        const uint32_t osa = rl(C0.sa, s), osb = rl(C0.sb, s), osia = rl(C0.sia, s), osi = rl(C0.si, s);
         // byte flags -> float coefficients (v_cvt_f32_ubyteN): forwarding, keep q, split
         const float kfa = static_cast<float>(fl & 0xFFu), kfb = static_cast<float>((fl >> 8) & 0xFFu);
         const float kq = static_cast<float>((fl >> 16) & 0xFFu), sp = static_cast<float>(fl >> 24);
@@ -302,10 +305,10 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const u4v* __restric
           plB.v[e] = bb * b0 + wb * qb0;
           q.v[e] = ab * qb0 + wb * b0;
         }
-        st<KPL, UP>(urs, voff, rl(C0.sa, s), plA);
-        st<KPL, UP>(urs, voff, rl(C0.sb, s), plB);
-        st<KPL>(irs, voff, rl(C0.sia, s), q1);
-        st<KPL>(irs, voff, rl(C0.si, s), q);
+        st<KPL, UP>(urs, voff, osa, plA);
+        st<KPL, UP>(urs, voff, osb, plB);
+        st<KPL>(irs, voff, osia, q1);
+        st<KPL>(irs, voff, osi, q);
         // rows of pair j+D (after this pair's stores)
         if (s + D < CH) MF_PREFETCH(slot, C0.ua, C0.ub, C0.ia, C0.ib, s + D);
         else MF_PREFETCH(slot, C1.w0[0], C1.w0[1], C1.w0[2], C1.w0[3], s + D - CH);
