@@ -216,6 +216,9 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const u4v* __restric
         if (c * CH + s >= npairs) goto run_done;
         const int slot = s % DS;
         const uint32_t fl = rl(C0.flags, s), osa = rl(C0.sa, s);
+        // the ring's next offsets (pair s + DS), also named up front
+        const uint32_t noa = s + DS < CH ? rl(C0.ua, s + DS) : rl(C1.w0[0], s + DS - CH);
+        const uint32_t nob = s + DS < CH ? rl(C0.ub, s + DS) : rl(C1.w0[1], s + DS - CH);
         const float kfa = static_cast<float>(fl & 0xFFu), kfb = static_cast<float>((fl >> 8) & 0xFFu);
         Row<KPL> pa;
         const Row<KPL> pb = RB[slot];
@@ -237,10 +240,8 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const u4v* __restric
         }
         st<KPL, UP>(urs, voff, osa, plA);
         st<KPL, UP>(urs, voff, ob[slot], plB);
-        uint32_t oa;
-        if (s + DS < CH) { oa = rl(C0.ua, s + DS); ob[slot] = rl(C0.ub, s + DS); }
-        else { oa = rl(C1.w0[0], s + DS - CH); ob[slot] = rl(C1.w0[1], s + DS - CH); }
-        RA[slot] = ld<KPL, UP>(urs, voff, oa);
+        ob[slot] = nob;
+        RA[slot] = ld<KPL, UP>(urs, voff, noa);
         RB[slot] = ld<KPL, UP>(urs, voff, ob[slot]);
       }
       C0 = chunk_convert(C1, eta);
@@ -276,6 +277,11 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const u4v* __restric
         // store offsets named up front: the scheduler then reads them early instead of right
         // before each store (a v_readlane feeding a buffer store's soffset costs an s_nop 4)
         const uint32_t osa = rl(C0.sa, s), osb = rl(C0.sb, s), osia = rl(C0.sia, s), osi = rl(C0.si, s);
+        const bool nin = s + D < CH;  // offsets of pair s + D (the ring's next rows)
+        const uint32_t nua = nin ? rl(C0.ua, s + D) : rl(C1.w0[0], s + D - CH);
+        const uint32_t nub = nin ? rl(C0.ub, s + D) : rl(C1.w0[1], s + D - CH);
+        const uint32_t nia = nin ? rl(C0.ia, s + D) : rl(C1.w0[2], s + D - CH);
+        const uint32_t nib = nin ? rl(C0.ib, s + D) : rl(C1.w0[3], s + D - CH);
         // byte flags -> float coefficients (v_cvt_f32_ubyteN): forwarding, keep q, split
         const float kfa = static_cast<float>(fl & 0xFFu), kfb = static_cast<float>((fl >> 8) & 0xFFu);
         const float kq = static_cast<float>((fl >> 16) & 0xFFu), sp = static_cast<float>(fl >> 24);
@@ -310,8 +316,10 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const u4v* __restric
         st<KPL>(irs, voff, osia, q1);
         st<KPL>(irs, voff, osi, q);
         // rows of pair j+D (after this pair's stores)
-        if (s + D < CH) MF_PREFETCH(slot, C0.ua, C0.ub, C0.ia, C0.ib, s + D);
-        else MF_PREFETCH(slot, C1.w0[0], C1.w0[1], C1.w0[2], C1.w0[3], s + D - CH);
+        PA[slot] = ld<KPL, UP>(urs, voff, nua);
+        PB[slot] = ld<KPL, UP>(urs, voff, nub);
+        QA[slot] = ld<KPL>(irs, voff, nia);
+        QB[slot] = ld<KPL>(irs, voff, nib);
       }
       C0 = chunk_convert(C1, eta);
       C1 = chunk_load(R, c + 2, npairs, lane);
