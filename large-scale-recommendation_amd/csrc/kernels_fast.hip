@@ -206,10 +206,14 @@ __device__ __forceinline__ void sweep_cell(int64_t beg, int len, const uint32_t*
 
   // A row that continues the previous record's run is forwarded in registers; its ring slot
   // reads a never-written dummy row instead (no load ever trails a store to a live row).
-#define MF_FETCH(slot, X, y)                                                                  \
+#define MF_FETCH(slot, X, y) MF_FETCH_AT(slot, rl(X.u, (y)), rl(X.i, (y)))
+  // The offsets are read (v_readlane) at the top of a step and the loads issued after its
+  // stores: named early, the readlanes no longer sit right before the buffer ops that take
+  // them as soffset (an s_nop hazard wait each).
+#define MF_FETCH_AT(slot, U_, I_)                                                             \
   do {                                                                                      \
-    const uint32_t uo_ = rl(X.u, (y));                                                      \
-    const uint32_t io_ = rl(X.i, (y));                                                      \
+    const uint32_t uo_ = (U_);                                                              \
+    const uint32_t io_ = (I_);                                                              \
     su[slot] = uo_;                                                                         \
     si[slot] = io_;                                                                         \
     rp[slot] = load_row<KPL, FULL, UAUX>(urs, uo_ != last_u ? uo_ : dummy_u_off, lane, k);  \
@@ -256,24 +260,27 @@ __device__ __forceinline__ void sweep_cell(int64_t beg, int len, const uint32_t*
 #pragma unroll
     for (int s = 0; s < CH; ++s) {
       if (base + s >= len) goto done;
+      const uint32_t fu_ = s + D < CH ? rl(A.u, s + D) : rl(B.u, s + D - CH);
+      const uint32_t fi_ = s + D < CH ? rl(A.i, s + D) : rl(B.i, s + D - CH);
       MF_STEP(s % D, A, s);
-      if (s + D < CH) MF_FETCH(s % D, A, s + D);
-      else MF_FETCH(s % D, B, s + D - CH);
+      MF_FETCH_AT(s % D, fu_, fi_);
     }
     chunk_prep(B, eta);
     chunk_load(recw, beg, len, base / CH + 2, lane, A);
 #pragma unroll
     for (int s = 0; s < CH; ++s) {
       if (base + CH + s >= len) goto done;
+      const uint32_t fu_ = s + D < CH ? rl(B.u, s + D) : rl(A.u, s + D - CH);
+      const uint32_t fi_ = s + D < CH ? rl(B.i, s + D) : rl(A.i, s + D - CH);
       MF_STEP(s % D, B, s);
-      if (s + D < CH) MF_FETCH(s % D, B, s + D);
-      else MF_FETCH(s % D, A, s + D - CH);
+      MF_FETCH_AT(s % D, fu_, fi_);
     }
     chunk_prep(A, eta);
     chunk_load(recw, beg, len, base / CH + 3, lane, B);
   }
 done:
 #undef MF_FETCH
+#undef MF_FETCH_AT
 #undef MF_STEP
   return;
 }
