@@ -44,6 +44,8 @@ def parse():
                     help="fast-mode factor blocking (reference = new Random(id ^ seed).nextInt(n))")
     ap.add_argument("--traffic-json", default=None, help="rocprof PMC summary to fill roofline.traffic")
     ap.add_argument("--no-profile", action="store_true", help="skip the profiled replay (roofline = null)")
+    ap.add_argument("--online-batches", type=int, default=5,
+                    help="ONLINE leg (BASELINE config 5): 1M-rating micro-batches applied to the fitted model (0 = off)")
     ap.add_argument("--item-split", type=int, default=0,
                     help="fast mode: hot-item replicas, max ratings per item chain per rating block (0 = off)")
     return ap.parse_args()
@@ -108,11 +110,23 @@ def pmc_traffic(a, k, groups, kernel):
     return None, None
 
 
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(tu, ti, tr, k, nb, supersteps):
     """Oracle C restatement (f64, exact reference order), one thread per block of a stratum."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import coracle  # checker / baseline only
-    cores = min(nb, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), os.cpu_count() or 1)
+    nproc = os.cpu_count() or 1
+    # one thread per active rating block (the Flink-slot equivalent): a superstep has nb of them
+    cores = min(nb, int(os.environ.get("OMP_NUM_THREADS", nproc)), nproc)
     m = coracle.dsgd_fit(tu, ti, tr, k=k, iterations=10, n_blocks=nb, seed=0, threads=cores,
                          max_supersteps=supersteps)
     v = m.updates / m.sweep_seconds if m.sweep_seconds > 0 else 0.0
@@ -120,7 +134,51 @@ def cpu_baseline(tu, ti, tr, k, nb, supersteps):
     return {"value": v, "unit": "updates/s", "cores": cores, "kind": "port",
             "sample": f"{supersteps} superstep(s) of the training split ({m.updates} f64 updates, k={k}, "
                       f"n={nb}), oracle/mf_oracle.c, one thread per active block",
-            "seconds": m.sweep_seconds}
+            "seconds": m.sweep_seconds, "nproc": nproc, "cpu_model": cpu_model(),
+            "cores_note": f"threads = min(numBlocks {nb}, OMP_NUM_THREADS, nproc): the reference runs one "
+                          "sequential sweep per active rating block"}
+
+
+def rmse_reference(a, arrays):
+    """The oracle's held-out RMSE after 10 epochs on exactly this data (tests/golden/rmse_ref.json,
+    written by tools/rmse_parity.py; matched by the sha256 of the train/test arrays), or None."""
+    path = os.path.join(ROOT, "tests", "golden", "rmse_ref.json")
+    if a.mode != "fast" or not os.path.exists(path):
+        return None
+    rec = json.load(open(path)).get(f"{a.config}@{a.scale:g}")
+    if not rec or rec.get("epochs") != 10:
+        return None
+    from mfhip import synth
+    if synth.fingerprint(*arrays) != rec["data_sha256"]:
+        print("[bench] rmse_ref fixture does not match this data (sha256); not used", file=sys.stderr)
+        return None
+    return rec
+
+
+def online_leg(ctx, synth, nu, ni, a, batch=1_000_000):
+    """BASELINE config 5: streaming micro-batches on top of the offline DSGD model just fitted.
+    Each batch: SGDUpdater.nextFactors in arrival order with per-user FIFO (FlinkOnlineMF.scala:
+    52-137; core/FactorUpdater.scala:37-45), unseen ids initialised on first touch; timed end to
+    end (host id lookup, dependency-level plan, H2D, kernels, sync)."""
+    import numpy as np
+    from mfhip import _lib as L
+    stream = synth.generate(max(1, int(nu * a.scale)), max(1, int(ni * a.scale)), batch * a.online_batches,
+                            seed=99, test_fraction=0.0)
+    rates, levels = [], []
+    for b in range(a.online_batches):
+        s = slice(b * batch, (b + 1) * batch)
+        ctx.reset_stats()
+        t0 = time.perf_counter()
+        ctx.online_update(stream.u[s], stream.i[s], stream.r[s], L.ONLINE_NEXT_FACTORS)
+        ctx.sync()
+        rates.append(batch / (time.perf_counter() - t0))
+        levels.append(ctx.stats()["levels"])
+    return {"metric": "online ratings/s (1M-rating micro-batches on the fitted model)",
+            "value": round(float(np.median(rates)), 1), "unit": "ratings/s", "min": round(float(min(rates)), 1),
+            "batch": batch, "batches": a.online_batches, "levels_median": float(np.median(levels)),
+            "flavour": "FlinkOnlineMF / SGDUpdater.nextFactors (lr 0.01)", "target": 10e6,
+            "dtype": "f32" if a.mode == "fast" else "f64",
+            "timing": "end to end per micro-batch: host id lookup, dependency-level plan, H2D, kernels, sync"}
 
 
 def main():
@@ -176,15 +234,16 @@ def main():
     st = ctx.stats()
     elapsed = D.reduce(t1 - t0, "max")
     updates = D.reduce(float(st["updates"]), "sum")
-    t0 = time.time()
-    rmse, matched = ctx.rmse(eu, ei, er)  # after warmup + steps epochs
-    t_eval = time.time() - t0
 
     # Roofline: replay min(steps, 2) epochs of the same workload with a start/stop event pair on
     # every sweep launch (on the library's stream; for the pair kernel recorded by the dispatch
-    # packet itself) and divide the sweep's algorithmic bytes by the summed kernel time.
+    # packet itself).  achieved = the bytes the sweep kernel requests per launch (its row loads
+    # and stores with in-range offsets plus its schedule records: mf_stats.moved_bytes, counted
+    # from the device plan) / its average launch time.  The SURVEY 8d per-update model
+    # (16k+20 B) is reported beside it as algorithmic_frac: it charges an item row per update,
+    # which this kernel keeps in registers through a run, so it overstates the bytes.
     prof_epochs = 0 if a.no_profile else min(a.steps, 2)
-    st_p = {"kernel_ms": 0.0, "kernel_launches": 0, "algorithmic_bytes": 0.0}
+    st_p = {"kernel_ms": 0.0, "kernel_launches": 0, "algorithmic_bytes": 0.0, "moved_bytes": 0.0, "updates": 0}
     if prof_epochs:
         ctx.reset_stats()
         ctx.set_profiling(True)
@@ -194,19 +253,40 @@ def main():
         ctx.set_profiling(False)
         st_p = ctx.stats()
 
+    # RMSE after exactly 10 epochs (the metric's second half): the same prepared fit restarted
+    # from its initial factors, 10 epochs, held-out RMSE; beside it the oracle's RMSE on the same
+    # data (f64, reference order) when the committed fixture matches.
+    t0 = time.time()
+    ctx.restart()
+    ctx.run(10 * nb)
+    rmse, matched = ctx.rmse(eu, ei, er)
+    t_eval = time.time() - t0
+    ref = rmse_reference(a, (tu, ti, tr, eu, ei, er)) if D.rank == 0 else None
+
     value = updates / elapsed
     bpu = 16 * k + 20 if a.mode == "fast" else 32 * k + 24
     roof = None
     if st_p["kernel_ms"] > 0:
         launches = st_p["kernel_launches"]
-        achieved = st_p["algorithmic_bytes"] / (st_p["kernel_ms"] / 1e3) / 1e9  # GB/s, this rank's sweep kernel
+        ksec = st_p["kernel_ms"] / 1e3
+        achieved = st_p["moved_bytes"] / ksec / 1e9  # GB/s, this rank's sweep kernel
         kname = L.lib().mf_fast_kernel_name(k).decode() if a.mode == "fast" else "k_level"
         traffic, traffic_src = pmc_traffic(a, k, st["groups"], kname)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kname,
-                "bytes_per_update": bpu, "avg_launch_us": round(st_p["kernel_ms"] * 1e3 / max(launches, 1), 2),
+                "bytes_per_launch": round(st_p["moved_bytes"] / max(launches, 1)),
+                "bytes_source": "mf_stats.moved_bytes: in-range row loads/stores + schedule records of the device plan",
+                "avg_launch_us": round(st_p["kernel_ms"] * 1e3 / max(launches, 1), 2),
                 "launches": launches, "profiled_epochs": prof_epochs, "traffic_source": traffic_src,
-                "wall_frac": round(value / D.world * bpu / 1e9 / HBM_PEAK_GBS, 4)}
+                "algorithmic_bytes_per_update": bpu,
+                "algorithmic_frac": round(st_p["algorithmic_bytes"] / ksec / 1e9 / HBM_PEAK_GBS, 4),
+                "traffic_frac": (round(traffic / (st_p["kernel_ms"] / max(launches, 1) / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
+                                 if traffic else None),
+                "kernel_ms_per_epoch": round(st_p["kernel_ms"] / prof_epochs, 3)}
+
+    online = None
+    if D.world == 1 and a.online_batches > 0:
+        online = online_leg(ctx, synth, nu, ni, a)
 
     cpu = None
     if D.rank == 0 and D.world == 1 and not a.no_cpu_baseline:
@@ -214,7 +294,7 @@ def main():
 
     if D.rank == 0:
         out = {
-            "metric": "SGD rating updates/sec (node) at rank 128; RMSE after 10 epochs",
+            "metric": "SGD rating updates/sec (node) at rank 128, 1/2/4/8 GPU; RMSE after 10 epochs",
             "value": round(value, 1), "unit": "updates/s", "n_gpus": D.world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed * 1e3 / max(a.steps, 1), 3),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
@@ -224,8 +304,12 @@ def main():
                        "train_ratings": int(len(tr)), "rank": k, "num_blocks": nb, "lambda": 1.0, "lr": 0.001,
                        "lr_method": "Default", "blocking": a.blocking, "item_split": a.item_split, "groups": st["groups"], "pad_records": st["pads"],
                        "parallelism": f"dsgd-ring{D.world}"},
-            "rmse": round(rmse, 6), "rmse_epochs": a.warmup + a.steps, "rmse_matched": matched,
-            "roofline": roof, "cpu_baseline": cpu,
+            "rmse": round(rmse, 6), "rmse_epochs": 10, "rmse_matched": matched,
+            "rmse_ref": round(ref["oracle_rmse"], 6) if ref else None,
+            "rmse_rel": round((rmse - ref["oracle_rmse"]) / ref["oracle_rmse"], 5) if ref else None,
+            "rmse_ref_source": "tests/golden/rmse_ref.json (tools/rmse_parity.py, oracle f64, same data sha256)"
+                               if ref else None,
+            "roofline": roof, "cpu_baseline": cpu, "online": online,
             "setup_s": {"generate": round(t_gen, 2), "prepare": round(t_prep, 2), "rmse_eval": round(t_eval, 3)},
         }
         print(json.dumps(out), flush=True)

@@ -109,7 +109,9 @@ typedef struct mf_stats {
   int32_t groups;            /* fast mode: rotation groups per rating block      */
   int32_t reserved0;
   int64_t pads;              /* fast mode: no-op records the plan inserted       */
-  int32_t reserved[2];
+  double moved_bytes;        /* bytes the sweep kernels request from memory: every row load and
+                                store they issue (forwarded rows and no-op halves excluded) plus
+                                the schedule records they read; an upper bound on HBM traffic */
 } mf_stats;
 
 typedef struct mf_ctx mf_ctx;
@@ -140,6 +142,10 @@ int mf_dsgd_prepare(mf_ctx* ctx, const int32_t* users, const int32_t* items, con
 int mf_dsgd_run(mf_ctx* ctx, int64_t supersteps);
 int mf_dsgd_superstep(mf_ctx* ctx, int64_t* done);
 int mf_dsgd_set_superstep(mf_ctx* ctx, int64_t done);
+/* Start the prepared fit over: factors back to their initial values (k x nextDouble of
+   new Random(id ^ seed), DSGDforMF.scala:548-549) and the superstep counter to 0; blocking
+   and the device schedule are kept.  mf_dsgd_run(iterations * numBlocks) then repeats fitSGD. */
+int mf_dsgd_restart(mf_ctx* ctx);
 int mf_sync(mf_ctx* ctx);
 
 /* unblock (DSGDforMF.scala:245-255) -> factorsOption (MatrixFactorization.scala:64).
@@ -195,6 +201,18 @@ int mf_block_update(mf_ctx* ctx, const double* r, const int32_t* uidx, const int
 int mf_online_update(mf_ctx* ctx, const int32_t* users, const int32_t* items,
                      const double* ratings, int64_t n, int flavour, int num_partitions,
                      int64_t* touched_users, int64_t* touched_items);
+/* mf_online_update plus the per-rating records the reference's operators emit, row j of the
+   caller's n x k buffers (either may be NULL) for rating j in arrival order:
+     MF_ONLINE_NEXT_FACTORS: user_out = nextUserVector, item_out = nextItemVector, the pair
+       ItemOperator collects (fl/mf/online/FlinkOnlineMF.scala:131-135);
+     MF_ONLINE_DELTA: user_out = userVec + deltaItemVec, the worker's ps.output
+       (fl/mf/PSOfflineOnlineMF.scala:176, userVec before this rating's update), item_out =
+       deltaItemVec, the vector pushed to the PS (:174).
+   MF_ONLINE_SPARK_SWEEP emits only touched rows (OfflineSpark.scala:33-67): outputs must be NULL. */
+int mf_online_update_out(mf_ctx* ctx, const int32_t* users, const int32_t* items,
+                         const double* ratings, int64_t n, int flavour, int num_partitions,
+                         int64_t* touched_users, int64_t* touched_items, double* user_out,
+                         double* item_out);
 /* Vectors for specific ids (found[j] = 0 for unknown ids). */
 int mf_lookup(mf_ctx* ctx, int side, const int32_t* ids, int64_t n, double* vecs_out,
               uint8_t* found);
@@ -232,6 +250,12 @@ int mf_debug_fast_split(const int32_t* users, const int32_t* items, int64_t n, i
                         int64_t seed, int32_t groups, int32_t blocking, int32_t window, int32_t item_split,
                         int32_t* block_out, int32_t* substep_out, int32_t* group_out, int64_t* pos_out,
                         int32_t* replica_out);
+/* mf_debug_ring_schedule: the item-block ring step ring_shift runs after superstep `superstep`
+   (1-based) on rank `rank` of `world` with n blocks (n = c * world): the item block it sends
+   (*out_blk) to rank *dst and the one it receives (*in_blk) from rank *src -- nextRatingBlock
+   (DSGDforMF.scala:611-619) over ranks. */
+int mf_debug_ring_schedule(int32_t rank, int32_t world, int32_t n_blocks, int64_t superstep, int32_t* out_blk,
+                           int32_t* in_blk, int32_t* dst, int32_t* src);
 /* The plan window (records between two uses of a row inside a cell unless adjacent) the fast
    sweep uses at rank k: the prefetch distance of the kernel selected for k. */
 int mf_fast_plan_window(int32_t k, int32_t* window_out);

@@ -20,6 +20,12 @@ enum class Arith : int {
 // (kDsgd) or SGDUpdater's learningRate (kSgdNext).
 void launch_level(hipStream_t st, const DetEntry* entries, int64_t n, void* U, void* I,
                   const void* regU, const void* regI, int k, double eta, Arith arith, bool f64);
+// Per-rating records of the online operators (mf_online_update_out), f64 rows of k at
+// [src[entry] * k]: kOutNext = (user', item') (FlinkOnlineMF.scala:131-135), kOutDelta =
+// (user + deltaItem, deltaItem) with user before the update (PSOfflineOnlineMF.scala:174-176).
+enum class OnlineOut : int { kNone = 0, kOutNext = 1, kOutDelta = 2 };
+void launch_level_out(hipStream_t st, const DetEntry* entries, int64_t n, void* U, void* I, int k, double eta, bool f64,
+                      OnlineOut mode, const int32_t* src, double* uout, double* iout);
 
 // Fast-mode sweep, one rotation sub-step t for nblk rating blocks of one superstep.
 struct FastBlk {

@@ -87,6 +87,52 @@ __global__ __launch_bounds__(256) void k_level(const DetEntry* __restrict__ ent,
   }
 }
 
+// k_level's SGDUpdater arithmetic (core/FactorUpdater.scala:37-53) plus the per-rating record
+// the online operator emits, f64 row src[j] of uout / iout (either may be null):
+//   OUT == 1: (user', item'), FlinkOnlineMF.ItemOperator's collect (:131-135)
+//   OUT == 2: (user + deltaItem, deltaItem), deltaItem = (lr*e)*user with user BEFORE the
+//             update: the PS worker's ps.output and ps.push (PSOfflineOnlineMF.scala:174-176)
+template <typename T, int KPL, int OUT>
+__global__ __launch_bounds__(256) void k_level_out(const DetEntry* __restrict__ ent, int64_t n, T* __restrict__ U,
+                                                   T* __restrict__ I, int k, T eta, const int32_t* __restrict__ src,
+                                                   double* __restrict__ uout, double* __restrict__ iout) {
+  const int lane = threadIdx.x & 63;
+  const int64_t j = static_cast<int64_t>(blockIdx.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (j >= n) return;
+  const uint32_t ur = ent[j].u, ir = ent[j].i;
+  const T r = static_cast<T>(ent[j].r);
+  T* p = U + static_cast<size_t>(ur) * k;
+  T* q = I + static_cast<size_t>(ir) * k;
+  T pv[KPL], qv[KPL], pr[KPL];
+#pragma unroll
+  for (int c = 0; c < KPL; ++c) {
+    const int f = lane + 64 * c;
+    pv[c] = f < k ? p[f] : T(0);
+    qv[c] = f < k ? q[f] : T(0);
+    pr[c] = pv[c] * qv[c];
+  }
+  const T e = r - seq_dot<T, KPL>(pr, k);
+  const T le = eta * e;
+  const size_t o = static_cast<size_t>(src[j]) * k;
+#pragma unroll
+  for (int c = 0; c < KPL; ++c) {
+    const int f = lane + 64 * c;
+    if (f < k) {
+      const T pn = pv[c] + le * qv[c], qn = qv[c] + le * pv[c];
+      p[f] = pn;
+      q[f] = qn;
+      if constexpr (OUT == 1) {
+        if (uout) uout[o + f] = static_cast<double>(pn);
+        if (iout) iout[o + f] = static_cast<double>(qn);
+      } else {
+        const T di = le * pv[c];
+        if (uout) uout[o + f] = static_cast<double>(pv[c] + di);
+        if (iout) iout[o + f] = static_cast<double>(di);
+      }
+    }
+  }
+}
+
 // predictRating gathers, one pair per LANE: every lane sums its own pair's products in order
 // f = 0..k-1 (the F2jBLAS.ddot order, bit-exact in f64), so a wave runs 64 independent
 // k-long add chains instead of one readlane chain per pair.  Rows are staged through LDS in
@@ -219,6 +265,32 @@ void launch_level(hipStream_t st, const DetEntry* entries, int64_t n, void* U, v
   } else {
     if (arith == Arith::kDsgd) level_dispatch<float, 0>(st, entries, n, U, I, regU, regI, k, eta);
     else level_dispatch<float, 1>(st, entries, n, U, I, regU, regI, k, eta);
+  }
+}
+
+template <typename T, int OUT>
+void level_out_dispatch(hipStream_t st, const DetEntry* e, int64_t n, void* U, void* I, int k, double eta,
+                        const int32_t* src, double* uo, double* io) {
+  const dim3 grid(static_cast<unsigned>((n + 3) / 4)), block(256);
+  T* u = static_cast<T*>(U);
+  T* i = static_cast<T*>(I);
+  const T et = static_cast<T>(eta);
+  if (k <= 64) hipLaunchKernelGGL((k_level_out<T, 1, OUT>), grid, block, 0, st, e, n, u, i, k, et, src, uo, io);
+  else if (k <= 128) hipLaunchKernelGGL((k_level_out<T, 2, OUT>), grid, block, 0, st, e, n, u, i, k, et, src, uo, io);
+  else if (k <= 256) hipLaunchKernelGGL((k_level_out<T, 4, OUT>), grid, block, 0, st, e, n, u, i, k, et, src, uo, io);
+  else hipLaunchKernelGGL((k_level_out<T, 8, OUT>), grid, block, 0, st, e, n, u, i, k, et, src, uo, io);
+}
+
+void launch_level_out(hipStream_t st, const DetEntry* entries, int64_t n, void* U, void* I, int k, double eta, bool f64,
+                      OnlineOut mode, const int32_t* src, double* uout, double* iout) {
+  if (n <= 0) return;
+  const bool next = mode == OnlineOut::kOutNext;
+  if (f64) {
+    if (next) level_out_dispatch<double, 1>(st, entries, n, U, I, k, eta, src, uout, iout);
+    else level_out_dispatch<double, 2>(st, entries, n, U, I, k, eta, src, uout, iout);
+  } else {
+    if (next) level_out_dispatch<float, 1>(st, entries, n, U, I, k, eta, src, uout, iout);
+    else level_out_dispatch<float, 2>(st, entries, n, U, I, k, eta, src, uout, iout);
   }
 }
 

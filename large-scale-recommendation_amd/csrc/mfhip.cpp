@@ -74,6 +74,7 @@ struct Shard {
   DevBuf st_trace;                      // MFHIP_WAVE_TRACE: {start, end} per wave
   DevBuf st_split;                      // hot-item replicas (SplitItem), superstep-major
   std::vector<int64_t> st_split_off;    // per superstep (n + 1)
+  std::vector<double> sm_bytes;         // per superstep index (s-1) mod n: bytes the sweep requests
   // evaluation scratch
   DevBuf ev_u, ev_i, ev_r, ev_mult, ev_out, ev_part;
   // profiling
@@ -111,6 +112,8 @@ struct mf_ctx {
   bool profiling = false;
   std::vector<int32_t> rows_by_id_u, rows_by_id_i;  // ascending-id row permutations
   bool order_dirty = true;
+  int64_t init_seed = 0;      // seed of the initial factors (P.seed, or a random one when unseeded)
+  std::string failed;         // non-empty: a device-side bound tripped; the fit must be prepared again
 };
 
 namespace mfhip {
@@ -362,12 +365,20 @@ void sync_all(mf_ctx* ctx) {
       MF_HIP(hipMemcpy(&err, s.fast_err.get(), sizeof(err), hipMemcpyDeviceToHost));
       if (err) {
         MF_HIP(hipMemset(s.fast_err.get(), 0, sizeof(err)));
-        fail(MF_ERR_TIMEOUT, "fast sweep: a wave waited > 1 s for its neighbour (workgroups not co-resident?); "
-                             "set MFHIP_PAIR_SYS=0 (or MFHIP_FAST_KERNEL=cell)");
+        // waves that gave up skipped the rest of their cells: the model is partly updated, so
+        // the context refuses further supersteps and reads until the fit is prepared again
+        ctx->failed = "fast sweep: a wave waited > 1 s for its neighbour (workgroups not co-resident?); "
+                      "set MFHIP_PAIR_SYS=0 (or MFHIP_FAST_KERNEL=cell)";
+        fail(MF_ERR_TIMEOUT, ctx->failed);
       }
     }
   }
   collect_profile(ctx);
+}
+
+void require_healthy(const mf_ctx* ctx) {
+  if (!ctx->failed.empty())
+    fail(MF_ERR_STATE, "the context failed earlier (" + ctx->failed + "); prepare the fit again");
 }
 
 // ---------------------------------------------------------------------------------------
@@ -398,6 +409,14 @@ void init_rows_on_device(mf_ctx* ctx, Shard& s, int side, const int32_t* ids, in
   MF_HIP(hipStreamSynchronize(s.stream));  // the temporaries die here
 }
 
+// Every shard's slabs := the initial factors of every row (fitSGD's starting point).
+void init_factors(mf_ctx* ctx) {
+  for (int side = 0; side < 2; ++side) {
+    SideLayout& S = side == kSideU ? ctx->U : ctx->I;
+    for (auto& s : ctx->shards) init_rows_on_device(ctx, s, side, S.row_id.data(), S.rows(), true, ctx->init_seed);
+  }
+}
+
 void build_model(mf_ctx* ctx, const int32_t* u, const int32_t* i, int64_t n) {
   const bool seeded = ctx->P.has_seed != 0;
   const Blocking bl = !ctx->f64 && ctx->P.fast_blocking == MF_BLOCKING_BALANCED ? Blocking::kBalanced : Blocking::kJvm;
@@ -406,18 +425,18 @@ void build_model(mf_ctx* ctx, const int32_t* u, const int32_t* i, int64_t n) {
   for (int side = 0; side < 2; ++side) {
     SideLayout& S = side == kSideU ? ctx->U : ctx->I;
     std::vector<double> reg(S.rows());
-    int64_t seed = ctx->P.seed;
-    if (!seeded) {
-      std::random_device rd;
-      seed = (static_cast<int64_t>(rd()) << 32) ^ rd();
-    }
     for (int64_t x = 0; x < S.rows(); ++x) reg[x] = ctx->P.lambda / static_cast<double>(S.omega[x]);
     for (auto& s : ctx->shards) {
       ensure_rows(ctx, s, side, std::max<int64_t>(S.rows(), 1));
-      init_rows_on_device(ctx, s, side, S.row_id.data(), S.rows(), true, seed);
       upload_regs(ctx, s, side, 0, reg.data(), S.rows());
     }
   }
+  ctx->init_seed = ctx->P.seed;
+  if (!seeded) {
+    std::random_device rd;
+    ctx->init_seed = (static_cast<int64_t>(rd()) << 32) ^ rd();
+  }
+  init_factors(ctx);
   ctx->have_model = true;
   ctx->order_dirty = true;
 }
@@ -506,6 +525,8 @@ void det_superstep(mf_ctx* ctx, Shard& s, int64_t superstep, int32_t iteration, 
   ctx->stats.levels += lp.levels();
   ctx->stats.updates += static_cast<int64_t>(lp.entries.size());
   ctx->stats.kernel_launches += lp.levels();
+  // per update: two f64 rows read and written, the 16-B entry, the two lambda/omega values
+  ctx->stats.moved_bytes += static_cast<double>(lp.entries.size()) * (32.0 * ctx->P.num_factors + 32.0);
 }
 
 void fast_superstep(mf_ctx* ctx, Shard& s, int64_t superstep, double eta) {
@@ -570,6 +591,23 @@ void fast_superstep(mf_ctx* ctx, Shard& s, int64_t superstep, double eta) {
   launch_split_join(s.stream, s.st_split.as<SplitItem>() + sp0, nsplit, s.itf.as<float>(), ctx->P.num_factors);
   MF_HIP(hipGetLastError());
   ctx->stats.updates += ups;
+  if (!s.sm_bytes.empty()) ctx->stats.moved_bytes += s.sm_bytes[smod];
+}
+
+// One step of the item-block ring after superstep s (1-based) for shard / rank g of G, n = c*G
+// blocks: rating block (p, q) hands its item block to (p-1, q) (nextRatingBlock, :611-619), so
+// shard g, which just ran item block (g*c + s-1) mod n in its first user block, sends it to
+// shard g-1 and receives ((g+1)*c + s-1) mod n from shard g+1.
+struct RingStep {
+  int32_t out_blk, in_blk, dst, src;
+};
+RingStep ring_step(int32_t g, int32_t G, int32_t c, int32_t n, int64_t superstep) {
+  RingStep r;
+  r.out_blk = static_cast<int32_t>((static_cast<int64_t>(g) * c + superstep - 1) % n);
+  r.in_blk = static_cast<int32_t>((static_cast<int64_t>((g + 1) % G) * c + superstep - 1) % n);
+  r.dst = (g + G - 1) % G;
+  r.src = (g + 1) % G;
+  return r;
 }
 
 // nextRatingBlock rotation (:611-619) across shards after superstep s.
@@ -584,20 +622,18 @@ void ring_shift(mf_ctx* ctx, int64_t superstep) {
   if (ctx->rank_mode) {
     Shard& s = ctx->shards[0];
     DeviceGuard g(s.device);
-    const int gi = s.index;
-    const int32_t out_blk = static_cast<int32_t>((static_cast<int64_t>(gi) * ctx->c + superstep - 1) % n);
-    const int32_t in_blk = static_cast<int32_t>((static_cast<int64_t>((gi + 1) % ctx->G) * ctx->c + superstep - 1) % n);
+    const RingStep rs = ring_step(s.index, ctx->G, ctx->c, n, superstep);
     int64_t o0, oc, i0, ic;
-    rows_of(out_blk, o0, oc);
-    rows_of(in_blk, i0, ic);
+    rows_of(rs.out_blk, o0, oc);
+    rows_of(rs.in_blk, i0, ic);
     char* base = s.itf.as<char>();
     MF_NCCL(ncclGroupStart());
     if (oc > 0)
-      MF_NCCL(ncclSend(base + o0 * k * ctx->es, oc * k, ctx->f64 ? ncclFloat64 : ncclFloat32,
-                       (gi + ctx->G - 1) % ctx->G, ctx->comm, s.stream));
+      MF_NCCL(ncclSend(base + o0 * k * ctx->es, oc * k, ctx->f64 ? ncclFloat64 : ncclFloat32, rs.dst, ctx->comm,
+                       s.stream));
     if (ic > 0)
-      MF_NCCL(ncclRecv(base + i0 * k * ctx->es, ic * k, ctx->f64 ? ncclFloat64 : ncclFloat32,
-                       (gi + 1) % ctx->G, ctx->comm, s.stream));
+      MF_NCCL(ncclRecv(base + i0 * k * ctx->es, ic * k, ctx->f64 ? ncclFloat64 : ncclFloat32, rs.src, ctx->comm,
+                       s.stream));
     MF_NCCL(ncclGroupEnd());
   } else {
     // in-process shards: peer copy on the sender's stream, receiver waits on an event
@@ -606,10 +642,10 @@ void ring_shift(mf_ctx* ctx, int64_t superstep) {
       MF_HIP(hipEventRecord(src.done, src.stream));
     }
     for (auto& src : ctx->shards) {
-      Shard& dst = *local_shard(ctx, (src.index + ctx->G - 1) % ctx->G);
-      const int32_t blk = static_cast<int32_t>((static_cast<int64_t>(src.index) * ctx->c + superstep - 1) % n);
+      const RingStep rs = ring_step(src.index, ctx->G, ctx->c, n, superstep);
+      Shard& dst = *local_shard(ctx, rs.dst);
       int64_t r0, cnt;
-      rows_of(blk, r0, cnt);
+      rows_of(rs.out_blk, r0, cnt);
       if (cnt == 0) continue;
       DeviceGuard g(src.device);
       MF_HIP(hipStreamWaitEvent(src.stream, dst.done, 0));  // dst finished superstep s
@@ -622,19 +658,20 @@ void ring_shift(mf_ctx* ctx, int64_t superstep) {
       MF_HIP(hipEventRecord(src.done, src.stream));
     }
     for (auto& dst : ctx->shards) {
-      Shard& src = *local_shard(ctx, (dst.index + 1) % ctx->G);
+      Shard& src = *local_shard(ctx, ring_step(dst.index, ctx->G, ctx->c, n, superstep).src);
       DeviceGuard g(dst.device);
       MF_HIP(hipStreamWaitEvent(dst.stream, src.done, 0));
     }
   }
   for (int32_t g = 0; g < ctx->G; ++g) {
-    const int32_t blk = static_cast<int32_t>((static_cast<int64_t>(g) * ctx->c + superstep - 1) % n);
-    ctx->item_loc[blk] = (g + ctx->G - 1) % ctx->G;
+    const RingStep rs = ring_step(g, ctx->G, ctx->c, n, superstep);
+    ctx->item_loc[rs.out_blk] = rs.dst;
   }
 }
 
 void run_supersteps(mf_ctx* ctx, int64_t count) {
   MF_REQUIRE(ctx->prepared, "mf_dsgd_run before mf_dsgd_prepare");
+  require_healthy(ctx);
   for (int64_t x = 0; x < count; ++x) {
     const int64_t s = ctx->superstep_done + 1;
     const int32_t iteration = static_cast<int32_t>(s / ctx->nb);  // getSuperstepNumber / numBlocks (:476)
@@ -657,8 +694,8 @@ void reset_item_loc(mf_ctx* ctx) {
   for (int64_t s = 1; s <= ctx->superstep_done; ++s)
     if (ctx->G > 1)
       for (int32_t g = 0; g < ctx->G; ++g) {
-        const int32_t blk = static_cast<int32_t>((static_cast<int64_t>(g) * ctx->c + s - 1) % ctx->nb);
-        ctx->item_loc[blk] = (g + ctx->G - 1) % ctx->G;
+        const RingStep rs = ring_step(g, ctx->G, ctx->c, ctx->nb, s);
+        ctx->item_loc[rs.out_blk] = rs.dst;
       }
 }
 
@@ -677,6 +714,7 @@ struct PhaseClock {
 void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, int64_t n) {
   MF_REQUIRE(n >= 0, "negative rating count");
   MF_REQUIRE(n == 0 || (u && i && r), "null rating arrays");
+  ctx->failed.clear();
   sync_all(ctx);
   PhaseClock clk;
   ctx->nb = std::max(1, ctx->P.num_blocks);
@@ -723,18 +761,27 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
             if (gb[b] > 0) block_groups[b] = gb[b];
         }
       }
-      // every wave of a superstep must be resident at once
+      // every wave of a superstep must be resident at once -- on a device shared by several
+      // shards (their streams run concurrently) or, in rank mode, by MFHIP_DEVICE_SHARERS ranks
+      // (the one-GPU rehearsal of the ring), all of theirs together
+      if (const char* v = std::getenv("MFHIP_DEVICE_SHARERS"))
+        if (ctx->rank_mode && std::atoi(v) > 1) cap /= std::atoi(v);
       bool fits = cap > 0;
-      for (auto& s : ctx->shards)
-        for (int32_t sm = 0; sm < ctx->nb && fits; ++sm) {
+      for (int32_t sm = 0; sm < ctx->nb && fits; ++sm) {
+        std::vector<std::pair<int, int64_t>> per_dev;  // (device, waves of superstep sm)
+        for (auto& s : ctx->shards) {
           int64_t waves = 0;
           for (int32_t j = 0; j < ctx->c; ++j) {
             const int32_t p = s.index * ctx->c + j;
             const int64_t b = static_cast<int64_t>(p) * ctx->nb + (p + sm) % ctx->nb;
             waves += block_groups.empty() || block_groups[b] == 0 ? ctx->G_fast : block_groups[b];
           }
-          fits = waves <= cap;
+          auto it = std::find_if(per_dev.begin(), per_dev.end(), [&](const auto& e) { return e.first == s.device; });
+          if (it == per_dev.end()) per_dev.emplace_back(s.device, waves);
+          else it->second += waves;
         }
+        for (const auto& e : per_dev) fits = fits && e.second <= cap;
+      }
       ctx->fast_sys = fits;
       if (!fits) block_groups.clear();
     }
@@ -795,6 +842,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
         PairPlan pp;
         build_pair_plan(pp, fp, ctx->nb, ctx->c, s.index, k, !ctx->fast_sys);
         ctx->stats.pads += pp.noop_halves - fp.pads;  // run padding on top of the planner's
+        s.sm_bytes = pp.sm_bytes;
         s.st_recs.alloc(std::max<size_t>(pp.recs.size(), 1) * sizeof(PairRec));
         s.st_waves.alloc(std::max<size_t>(pp.waves.size(), 1) * sizeof(WaveDesc));
         if (!pp.recs.empty())
@@ -833,6 +881,24 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
           else s.st_waves_host = pp.waves;
         }
         continue;
+      }
+      {  // requested bytes per superstep: 32-B record, user row in + out, item row per run in + out
+        s.sm_bytes.assign(ctx->nb, 0.0);
+        const double row_bytes = 4.0 * k;
+        for (int32_t sm = 0; sm < ctx->nb; ++sm)
+          for (int32_t j = 0; j < ctx->c; ++j) {
+            const int32_t p = s.index * ctx->c + j;
+            const int64_t b = static_cast<int64_t>(p) * ctx->nb + (p + sm) % ctx->nb;
+            if (fp.cell_base[b] < 0) continue;
+            const int32_t* o = fp.cell_off.data() + fp.cell_base[b];
+            const int64_t GG = static_cast<int64_t>(fp.Gb[b]) * fp.Gb[b];
+            const FastRec* f = fp.recs.data() + fp.rec_base[b];
+            int64_t runs = 0;
+            for (int64_t cc = 0; cc < GG; ++cc)
+              for (int32_t x = o[cc]; x < o[cc + 1]; ++x)
+                runs += x == o[cc] || ((f[x].i ^ f[x - 1].i) & ~kPadBit) != 0;
+            s.sm_bytes[sm] += (32.0 + 2.0 * row_bytes) * o[GG] + 2.0 * row_bytes * static_cast<double>(runs);
+          }
       }
       s.fast_recs.alloc(std::max<size_t>(fp.recs.size(), 1) * sizeof(FastRec));
       s.fast_cells.alloc(std::max<size_t>(fp.cell_off.size(), 1) * sizeof(int32_t));
@@ -916,6 +982,7 @@ EvalOut evaluate(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* 
   MF_REQUIRE(ctx->have_model, "The MatrixFactorization model has not been fitted to data. "
                               "Prior to predicting values, it has to be trained on data.");
   MF_REQUIRE(n >= 0, "negative count");
+  require_healthy(ctx);
   EvalOut res;
   if (n == 0) return res;
   Shard& s = ctx->shards[0];
@@ -1009,10 +1076,13 @@ int32_t online_row(mf_ctx* ctx, SideLayout& S, int32_t id, std::vector<int32_t>&
 }
 
 void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, int64_t n, int flavour,
-                   int num_partitions, int64_t* tu, int64_t* ti) {
+                   int num_partitions, int64_t* tu, int64_t* ti, double* uout = nullptr, double* iout = nullptr) {
   MF_REQUIRE(ctx->shards.size() == 1 && !ctx->rank_mode, "online updates run on a single-device context");
   MF_REQUIRE(flavour >= MF_ONLINE_NEXT_FACTORS && flavour <= MF_ONLINE_SPARK_SWEEP, "unknown online flavour");
   MF_REQUIRE(n >= 0 && (n == 0 || (u && i && r)), "bad rating arrays");
+  MF_REQUIRE(!(uout || iout) || flavour != MF_ONLINE_SPARK_SWEEP,
+             "MF_ONLINE_SPARK_SWEEP emits touched rows only (OfflineSpark.scala:33-67): no per-rating outputs");
+  require_healthy(ctx);
   Shard& s = ctx->shards[0];
   if (!ctx->have_model) {
     ctx->U = SideLayout();
@@ -1038,6 +1108,9 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
   }
   if (tu) *tu = cu;
   if (ti) *ti = ci;
+  // new rows take the slab rows the fast DSGD schedule keeps zeroed (padding / idle prefetch
+  // rows past the real ones): that schedule is void now, a further fit must prepare again
+  if (ctx->prepared && !ctx->f64 && (!fu.empty() || !fi.empty())) ctx->prepared = false;
   // first-touch initialisation of unseen ids
   const bool xor_seed = ctx->P.online_init == MF_INIT_SEEDED;
   for (int side = 0; side < 2; ++side) {
@@ -1086,7 +1159,9 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
   sq.i_lo = 0;
   sq.i_hi = static_cast<uint32_t>(ctx->I.rows());
   LevelPlan lp;
-  build_level_plan({sq}, lp);
+  const bool outs = uout || iout;
+  std::vector<int32_t> src;
+  build_level_plan({sq}, lp, outs ? &src : nullptr);
   DeviceGuard g(s.device);
   const size_t bytes = lp.entries.size() * sizeof(DetEntry);
   MF_HIP(hipStreamSynchronize(s.stream));
@@ -1094,14 +1169,30 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
   s.det_dev.alloc(bytes);
   std::memcpy(s.det_pin.as<void>(), lp.entries.data(), bytes);
   MF_HIP(hipMemcpyAsync(s.det_dev.get(), s.det_pin.as<void>(), bytes, hipMemcpyHostToDevice, s.stream));
+  DevBuf dsrc, duo, dio;
+  const size_t obytes = static_cast<size_t>(n) * k * sizeof(double);
+  if (outs) {
+    dsrc.alloc(src.size() * sizeof(int32_t));
+    MF_HIP(hipMemcpyAsync(dsrc.get(), src.data(), src.size() * sizeof(int32_t), hipMemcpyHostToDevice, s.stream));
+    if (uout) duo.alloc(obytes);
+    if (iout) dio.alloc(obytes);
+  }
+  const OnlineOut om = flavour == MF_ONLINE_DELTA ? OnlineOut::kOutDelta : OnlineOut::kOutNext;
   for (int64_t l = 0; l < lp.levels(); ++l) {
     const int64_t b0 = lp.level_start[l], cnt = lp.level_start[l + 1] - b0;
     LaunchTimer t(s, ctx->profiling);
-    launch_level(s.stream, s.det_dev.as<DetEntry>() + b0, cnt, s.uf.get(), s.itf.get(), s.regu.get(),
-                 s.regi.get(), k, ctx->P.online_learning_rate, Arith::kSgdNext, ctx->f64);
+    if (outs)
+      launch_level_out(s.stream, s.det_dev.as<DetEntry>() + b0, cnt, s.uf.get(), s.itf.get(), k,
+                       ctx->P.online_learning_rate, ctx->f64, om, dsrc.as<int32_t>() + b0,
+                       uout ? duo.as<double>() : nullptr, iout ? dio.as<double>() : nullptr);
+    else
+      launch_level(s.stream, s.det_dev.as<DetEntry>() + b0, cnt, s.uf.get(), s.itf.get(), s.regu.get(),
+                   s.regi.get(), k, ctx->P.online_learning_rate, Arith::kSgdNext, ctx->f64);
   }
   MF_HIP(hipGetLastError());
   MF_HIP(hipStreamSynchronize(s.stream));
+  if (uout) MF_HIP(hipMemcpy(uout, duo.get(), obytes, hipMemcpyDeviceToHost));
+  if (iout) MF_HIP(hipMemcpy(iout, dio.get(), obytes, hipMemcpyDeviceToHost));
   ctx->stats.levels += lp.levels();
   ctx->stats.kernel_launches += lp.levels();
   ctx->stats.updates += n;
@@ -1269,6 +1360,18 @@ int mf_dsgd_set_superstep(mf_ctx* ctx, int64_t done) {
   });
 }
 
+int mf_dsgd_restart(mf_ctx* ctx) {
+  return guarded([&] {
+    MF_REQUIRE(ctx, "null context");
+    MF_REQUIRE(ctx->prepared, "mf_dsgd_restart before mf_dsgd_prepare");
+    ctx->failed.clear();
+    sync_all(ctx);
+    init_factors(ctx);
+    ctx->superstep_done = 0;
+    reset_item_loc(ctx);
+  });
+}
+
 int mf_sync(mf_ctx* ctx) {
   return guarded([&] {
     MF_REQUIRE(ctx, "null context");
@@ -1301,6 +1404,7 @@ int mf_get_factors(mf_ctx* ctx, int side, int32_t* ids, double* vecs, int64_t ca
     MF_REQUIRE(ctx, "null context");
     MF_REQUIRE(side == MF_SIDE_USER || side == MF_SIDE_ITEM, "bad side");
     MF_REQUIRE(ctx->have_model, "The MatrixFactorization model has not been fitted to data.");
+    require_healthy(ctx);
     Shard& s = ctx->shards[0];
     if (ctx->rank_mode) { if (side == MF_SIDE_ITEM) allgather_items(ctx); }
     else consolidate(ctx, s);
@@ -1454,6 +1558,15 @@ int mf_online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const doub
   return guarded([&] {
     MF_REQUIRE(ctx, "null context");
     online_update(ctx, u, i, r, n, flavour, num_partitions, touched_users, touched_items);
+  });
+}
+
+int mf_online_update_out(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, int64_t n, int flavour,
+                         int num_partitions, int64_t* touched_users, int64_t* touched_items, double* user_out,
+                         double* item_out) {
+  return guarded([&] {
+    MF_REQUIRE(ctx, "null context");
+    online_update(ctx, u, i, r, n, flavour, num_partitions, touched_users, touched_items, user_out, item_out);
   });
 }
 
@@ -1617,6 +1730,20 @@ const char* mf_fast_kernel_name(int32_t k) {
     case FastKernel::kPersistent: return "k_fast_superstep";
     default: return "k_fast_substep";
   }
+}
+
+int mf_debug_ring_schedule(int32_t rank, int32_t world, int32_t n_blocks, int64_t superstep, int32_t* out_blk,
+                           int32_t* in_blk, int32_t* dst, int32_t* src) {
+  return guarded([&] {
+    MF_REQUIRE(out_blk && in_blk && dst && src, "null argument");
+    MF_REQUIRE(world >= 1 && rank >= 0 && rank < world && n_blocks >= 1 && n_blocks % world == 0 && superstep >= 1,
+               "bad ring arguments (n_blocks must be a multiple of world, superstep >= 1)");
+    const RingStep rs = ring_step(rank, world, n_blocks / world, n_blocks, superstep);
+    *out_blk = rs.out_blk;
+    *in_blk = rs.in_blk;
+    *dst = rs.dst;
+    *src = rs.src;
+  });
 }
 
 int mf_fast_plan_window(int32_t k, int32_t* window_out) {

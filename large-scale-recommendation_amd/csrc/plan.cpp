@@ -224,7 +224,7 @@ void build_rating_blocks(RatingBlocks& rb, const SideLayout& U, const SideLayout
 // level of the previous update of the same item row) along each sequence's order.  Updates
 // of one level touch pairwise-distinct rows, so running a level in parallel and the levels
 // in order reproduces the sequential result bit for bit.
-void build_level_plan(const std::vector<OrderedSeq>& seqs, LevelPlan& out) {
+void build_level_plan(const std::vector<OrderedSeq>& seqs, LevelPlan& out, std::vector<int32_t>* src) {
   const int64_t ns = static_cast<int64_t>(seqs.size());
   std::vector<std::vector<int32_t>> lvl(ns);
   std::vector<std::vector<int64_t>> cnt(ns);
@@ -261,11 +261,14 @@ void build_level_plan(const std::vector<OrderedSeq>& seqs, LevelPlan& out) {
   }
   out.level_start[L] = pos;
   out.entries.resize(pos);
+  if (src) src->resize(pos);
   parallel_tasks(ns, [&](int64_t x) {
     const OrderedSeq& q = seqs[x];
     for (int64_t j = 0; j < q.len; ++j) {
       const int64_t e = q.order ? q.order[j] : j;
-      out.entries[cur[x][lvl[x][j]]++] = DetEntry{q.u[e], q.i[e], q.r[e]};
+      const int64_t at = cur[x][lvl[x][j]]++;
+      out.entries[at] = DetEntry{q.u[e], q.i[e], q.r[e]};
+      if (src) (*src)[at] = static_cast<int32_t>(e);
     }
   });
 }
@@ -665,7 +668,6 @@ std::vector<std::vector<SubCell>> collect_supersteps(const FastPlan& fp, int32_t
 // record just before A.
 void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, int32_t shard, int32_t k,
                      bool substep_waves) {
-  (void)k;
   using Cell = SubCell;
   pp = PairPlan();
   const auto subs = substep_waves ? collect_subs(fp, nb, c, shard) : collect_supersteps(fp, nb, c, shard);
@@ -692,6 +694,8 @@ void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, in
   }
   pp.recs.resize(total);
   std::vector<int64_t> noops(nsub, 0);
+  std::vector<double> sub_bytes(nsub, 0.0);  // bytes the kernel requests for the cells of sx
+  const double row_bytes = 4.0 * k;
   parallel_tasks(nsub, [&](int64_t sx) {
     int64_t w = pp.sub_off[sx];
     for (const Cell& cl : subs[sx]) {
@@ -777,9 +781,24 @@ void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, in
       }
       if (single) pp.waves[w_this].cells = kWaveSingleRun;
       else if (g_plan_debug) g_not_single[why]++;
+      // what the kernel requests: the 64-B record of every pair and every row access with an
+      // in-range offset (the lean path: the item row once in, once out, B's row stored where
+      // it was loaded from)
+      int64_t rows = 0;
+      for (const PairRec* r = first; r < out; ++r) {
+        if (single) {
+          rows += (r->ua != kOffOOB) + 2 * (r->ub != kOffOOB) + (r->sa != kOffOOB);
+        } else {
+          for (uint32_t off : {r->ua, r->ub, r->ia, r->ib, r->sa, r->sb, r->sia, r->si}) rows += off != kOffOOB;
+        }
+      }
+      if (single && out > first) rows += 2;
+      sub_bytes[sx] += 64.0 * static_cast<double>(out - first) + row_bytes * static_cast<double>(rows);
     }
   });
   for (int64_t x = 0; x < nsub; ++x) pp.noop_halves += noops[x];
+  pp.sm_bytes.assign(nb, 0.0);
+  for (int64_t x = 0; x < nsub; ++x) pp.sm_bytes[substep_waves ? x / fp.G : x] += sub_bytes[x];
   if (g_plan_debug) {
     std::fprintf(stderr, "[mfhip] pair plan: cells not single-run: first %lld split %lld item-change %lld "
                  "B-store %lld item-store %lld hazard %lld\n", (long long)g_not_single[1].load(),

@@ -87,7 +87,8 @@ struct OrderedSeq {
   int64_t len;
   uint32_t u_lo, u_hi, i_lo, i_hi;  // row ranges touched (for the level trackers)
 };
-void build_level_plan(const std::vector<OrderedSeq>& seqs, LevelPlan& out);
+// src (optional): per entry, its index e into the sequence's u / i / r arrays (single sequence).
+void build_level_plan(const std::vector<OrderedSeq>& seqs, LevelPlan& out, std::vector<int32_t>* src = nullptr);
 
 // ---------------------------------------------------------------------------------------
 // Fast mode.
@@ -200,6 +201,7 @@ struct PairPlan {
   std::vector<SysWave> sys_waves;
   std::vector<int64_t> sys_off;
   int64_t noop_halves = 0;       // pair halves that are no-ops (planner padding, repeated users)
+  std::vector<double> sm_bytes;  // per superstep index: bytes the sweep requests (records + in-range rows)
 };
 // The plan window must be >= 2 * kPairRing records.  substep_waves: order the cells (and
 // pp.waves / sub_off) per sub-step (sm, t), longest first, for the per-sub-step launches (needs a

@@ -82,7 +82,7 @@ class mf_stats(C.Structure):
         ("groups", C.c_int32),
         ("reserved0", C.c_int32),
         ("pads", C.c_int64),
-        ("reserved", C.c_int32 * 2),
+        ("moved_bytes", C.c_double),
     ]
 
 
@@ -96,6 +96,7 @@ EXPORTS = [
     "mf_reset_stats", "mf_jvm_shuffle", "mf_jvm_block_of", "mf_jvm_random_factors",
     "mf_learning_rate", "mf_debug_levels", "mf_debug_fast_schedule", "mf_debug_fast_split", "mf_fast_plan_window",
     "mf_fast_kernel_name", "mf_get_params", "mf_read_ratings", "mf_save_model", "mf_load_model",
+    "mf_dsgd_restart", "mf_online_update_out", "mf_debug_ring_schedule",
 ]
 
 _i32p = C.POINTER(C.c_int32)
@@ -161,6 +162,10 @@ def lib() -> C.CDLL:
         "mf_read_ratings": (C.c_int, [C.c_char_p, C.c_char, C.c_int32, _i32p, _i32p, _f64p, C.c_int64, _i64p]),
         "mf_save_model": (C.c_int, [C.c_void_p, C.c_char_p]),
         "mf_load_model": (C.c_int, [C.c_void_p, C.c_char_p, _i64p]),
+        "mf_dsgd_restart": (C.c_int, [_ctxp]),
+        "mf_online_update_out": (C.c_int, [_ctxp, _i32p, _i32p, _f64p, C.c_int64, C.c_int, C.c_int, _i64p, _i64p,
+                                           _f64p, _f64p]),
+        "mf_debug_ring_schedule": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int64, _i32p, _i32p, _i32p, _i32p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -183,7 +188,24 @@ def ptr(a: np.ndarray, ctype):
 
 
 def as_i32(a) -> np.ndarray:
-    return np.ascontiguousarray(a, dtype=np.int32)
+    """Ids as the reference's Int: values outside int32 are rejected, not wrapped."""
+    arr = np.asarray(a)
+    if arr.dtype != np.int32 and arr.size:
+        if arr.dtype.kind not in "iub":
+            raise ValueError(f"ids must be integers, got {arr.dtype}")
+        lo, hi = int(arr.min()), int(arr.max())
+        if lo < -2**31 or hi >= 2**31:
+            raise ValueError(f"id out of the Int range: [{lo}, {hi}]")
+    return np.ascontiguousarray(arr, dtype=np.int32)
+
+
+def same_length(*arrays) -> int:
+    """Rating columns must be parallel arrays: the C side reads len(first) elements of each."""
+    n = len(arrays[0])
+    for a in arrays[1:]:
+        if len(a) != n:
+            raise ValueError(f"columns differ in length: {[len(x) for x in arrays]}")
+    return n
 
 
 def as_f64(a) -> np.ndarray:

@@ -98,13 +98,18 @@ class PSOfflineOnlineMF:
         FactorInitializer on first touch (:247-252), and push deltas (Batch state, :322-330).
         Ratings arriving during a batch are queued and applied online after it (:221-226), which
         is what calling `process` after `batch` does.
-    Returned vectors are the model state after the call; the per-rating worker output quirk
-    (`userVec + deltaItemVec`, :176) is not materialised."""
+    Returned vectors are the model state after the call.  With emit_outputs (default) every
+    rating's worker output -- ps.output(user, userVec + deltaItemVec), userVec before the update
+    (:176), the reference's stream out of this operator -- is kept in `self.output` after each
+    call as (user ids, n x k vectors) in application order (mf_online_update_out)."""
 
     def __init__(self, num_factors: int, learning_rate: float = 0.01, iterations: int = 10,
-                 init: str = "pseudo_random", seed: int = 0, mode: str = "deterministic"):
+                 init: str = "pseudo_random", seed: int = 0, mode: str = "deterministic",
+                 emit_outputs: bool = True):
         self.k = num_factors
         self.iterations = iterations
+        self.emit_outputs = emit_outputs
+        self.output = (np.empty(0, np.int32), np.empty((0, num_factors)))
         p = L.default_params()
         p.num_factors = num_factors
         p.online_learning_rate = learning_rate
@@ -130,8 +135,21 @@ class PSOfflineOnlineMF:
         r = np.ascontiguousarray(r, np.float64)
         for dst, src in zip(self._hist, (u, i, r)):
             dst.append(src)
-        self.ctx.online_update(u, i, r, L.ONLINE_DELTA)
+        self._apply(self.ctx, [(u, i, r)])
         return self._vectors(np.unique(u), np.unique(i))
+
+    def _apply(self, ctx: Context, passes) -> None:
+        """SGDUpdater.delta updates in order (vectorUpdateAndPush, :167-180), keeping the outputs."""
+        ids, outs = [], []
+        for u, i, r in passes:
+            if self.emit_outputs:
+                uo, _ = ctx.online_update_out(u, i, r, L.ONLINE_DELTA)
+                ids.append(u)
+                outs.append(uo)
+            else:
+                ctx.online_update(u, i, r, L.ONLINE_DELTA)
+        if self.emit_outputs:
+            self.output = (np.concatenate(ids), np.concatenate(outs))
 
     def batch(self) -> Tuple[Dict[int, np.ndarray], Dict[int, np.ndarray]]:
         """Batch training over the whole history; returns every user and item vector."""
@@ -141,8 +159,7 @@ class PSOfflineOnlineMF:
         uids, uvecs = self.ctx.factors(L.SIDE_USER)
         fresh = Context(self._params)  # PS params.clear(): items re-initialise on first pull
         fresh.set_factors(L.SIDE_USER, uids, uvecs)  # worker userVectors survive the batch
-        for _ in range(self.iterations):
-            fresh.online_update(hu, hi, hr, L.ONLINE_DELTA)
+        self._apply(fresh, [(hu, hi, hr)] * self.iterations)
         self.ctx.close()
         self.ctx = fresh
         return self._vectors(np.unique(hu), np.unique(hi))

@@ -7,7 +7,7 @@ from typing import Optional, Sequence, Tuple
 import numpy as np
 
 from . import _lib as L
-from ._lib import as_f64, as_i32, check, ptr
+from ._lib import as_f64, as_i32, check, ptr, same_length
 
 
 class Context:
@@ -57,10 +57,12 @@ class Context:
     # -- DSGD ------------------------------------------------------------------
     def fit(self, u, i, r) -> None:
         u, i, r = as_i32(u), as_i32(i), as_f64(r)
+        same_length(u, i, r)
         check(L.lib().mf_dsgd_fit(self._h, ptr(u, C.c_int32), ptr(i, C.c_int32), ptr(r, C.c_double), len(u)))
 
     def prepare(self, u, i, r) -> None:
         u, i, r = as_i32(u), as_i32(i), as_f64(r)
+        same_length(u, i, r)
         check(L.lib().mf_dsgd_prepare(self._h, ptr(u, C.c_int32), ptr(i, C.c_int32), ptr(r, C.c_double), len(u)))
 
     def run(self, supersteps: int) -> None:
@@ -68,6 +70,10 @@ class Context:
 
     def sync(self) -> None:
         check(L.lib().mf_sync(self._h))
+
+    def restart(self) -> None:
+        """Factors back to their initial values and superstep 0; blocking and schedule kept."""
+        check(L.lib().mf_dsgd_restart(self._h))
 
     @property
     def superstep(self) -> int:
@@ -95,7 +101,10 @@ class Context:
 
     def set_factors(self, side: int, ids, vecs) -> None:
         ids = as_i32(ids)
-        vecs = as_f64(vecs).reshape(len(ids), self.k)
+        vecs = as_f64(vecs)
+        if vecs.size != len(ids) * self.k:
+            raise ValueError(f"vecs must hold len(ids) x k = {len(ids)} x {self.k} values, got {vecs.size}")
+        vecs = vecs.reshape(len(ids), self.k)
         check(L.lib().mf_set_factors(self._h, side, ptr(ids, C.c_int32), ptr(vecs, C.c_double), len(ids)))
 
     def lookup(self, side: int, ids) -> Tuple[np.ndarray, np.ndarray]:
@@ -109,7 +118,7 @@ class Context:
     # -- evaluation ------------------------------------------------------------
     def predict(self, u, i) -> Tuple[np.ndarray, np.ndarray]:
         u, i = as_i32(u), as_i32(i)
-        n = len(u)
+        n = same_length(u, i)
         out = np.empty(max(n, 1), np.float64)
         found = np.empty(max(n, 1), np.uint8)
         check(L.lib().mf_predict(self._h, ptr(u, C.c_int32), ptr(i, C.c_int32), n, ptr(out, C.c_double),
@@ -118,6 +127,7 @@ class Context:
 
     def rmse(self, u, i, r) -> Tuple[float, int]:
         u, i, r = as_i32(u), as_i32(i), as_f64(r)
+        same_length(u, i, r)
         v = C.c_double(0.0)
         m = C.c_int64(0)
         check(L.lib().mf_rmse(self._h, ptr(u, C.c_int32), ptr(i, C.c_int32), ptr(r, C.c_double), len(u),
@@ -126,6 +136,7 @@ class Context:
 
     def empirical_risk(self, u, i, r, lam: float) -> float:
         u, i, r = as_i32(u), as_i32(i), as_f64(r)
+        same_length(u, i, r)
         v = C.c_double(0.0)
         check(L.lib().mf_empirical_risk(self._h, ptr(u, C.c_int32), ptr(i, C.c_int32), ptr(r, C.c_double), len(u),
                                         float(lam), C.byref(v)))
@@ -134,10 +145,25 @@ class Context:
     # -- online ----------------------------------------------------------------
     def online_update(self, u, i, r, flavour: int = L.ONLINE_NEXT_FACTORS, num_partitions: int = 0):
         u, i, r = as_i32(u), as_i32(i), as_f64(r)
+        same_length(u, i, r)
         tu, ti = C.c_int64(0), C.c_int64(0)
         check(L.lib().mf_online_update(self._h, ptr(u, C.c_int32), ptr(i, C.c_int32), ptr(r, C.c_double), len(u),
                                        flavour, num_partitions, C.byref(tu), C.byref(ti)))
         return tu.value, ti.value
+
+    def online_update_out(self, u, i, r, flavour: int = L.ONLINE_NEXT_FACTORS):
+        """online_update plus the per-rating records the operators emit (mf_online_update_out):
+        NEXT_FACTORS -> (user', item') per rating (FlinkOnlineMF.scala:131-135); DELTA ->
+        (userVec + deltaItemVec, deltaItemVec) per rating (PSOfflineOnlineMF.scala:174-176)."""
+        u, i, r = as_i32(u), as_i32(i), as_f64(r)
+        n = same_length(u, i, r)
+        uo = np.empty((max(n, 1), self.k), np.float64)
+        io = np.empty((max(n, 1), self.k), np.float64)
+        tu, ti = C.c_int64(0), C.c_int64(0)
+        check(L.lib().mf_online_update_out(self._h, ptr(u, C.c_int32), ptr(i, C.c_int32), ptr(r, C.c_double), n,
+                                           flavour, 0, C.byref(tu), C.byref(ti), ptr(uo, C.c_double),
+                                           ptr(io, C.c_double)))
+        return uo[:n], io[:n]
 
     # -- snapshots (TemporaryPath persistence, DSGDforMF.scala:291-296, 330-349) --
     def save(self, path: str) -> None:
@@ -150,7 +176,7 @@ class Context:
         check(L.lib().mf_load_model(self._h, path.encode(), C.byref(step)))
         return step.value
 
-        # -- stats -----------------------------------------------------------------
+    # -- stats -----------------------------------------------------------------
     def set_profiling(self, on: bool) -> None:
         check(L.lib().mf_set_profiling(self._h, 1 if on else 0))
 
@@ -173,6 +199,7 @@ def block_update(r, uidx, iidx, users, uomega, items, iomega, k, iteration, rati
         ctx = Context(p)
     try:
         r, uidx, iidx = as_f64(r), as_i32(uidx), as_i32(iidx)
+        same_length(r, uidx, iidx)
         users = as_f64(users).copy()
         items = as_f64(items).copy()
         uomega, iomega = as_i32(uomega), as_i32(iomega)

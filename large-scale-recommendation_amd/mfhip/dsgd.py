@@ -84,8 +84,9 @@ class LearningRateMethod:
 
 def _columns(data) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
     if isinstance(data, tuple) and len(data) == 3 and hasattr(data[0], "__len__") and not np.isscalar(data[0]):
-        u, i, r = data
-        return L.as_i32(u), L.as_i32(i), L.as_f64(r)
+        u, i, r = L.as_i32(data[0]), L.as_i32(data[1]), L.as_f64(data[2])
+        L.same_length(u, i, r)
+        return u, i, r
     arr = list(data)
     if not arr:
         return np.empty(0, np.int32), np.empty(0, np.int32), np.empty(0, np.float64)
@@ -97,7 +98,9 @@ def _columns(data) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
 
 def _pairs(data) -> Tuple[np.ndarray, np.ndarray]:
     if isinstance(data, tuple) and len(data) == 2 and hasattr(data[0], "__len__") and not np.isscalar(data[0]):
-        return L.as_i32(data[0]), L.as_i32(data[1])
+        u, i = L.as_i32(data[0]), L.as_i32(data[1])
+        L.same_length(u, i)
+        return u, i
     arr = list(data)
     u = np.fromiter((t[0] for t in arr), np.int32, len(arr))
     i = np.fromiter((t[1] for t in arr), np.int32, len(arr))

@@ -6,6 +6,7 @@ all ranks of a multi-GPU job generate identical data and the thread count does n
 from __future__ import annotations
 
 import ctypes as C
+import hashlib
 import os
 from dataclasses import dataclass
 
@@ -70,3 +71,11 @@ def generate(n_users: int, n_items: int, n: int, seed: int = 42, perm_seed: int 
 def config(name: str, scale: float = 1.0, **kw) -> Ratings:
     nu, ni, n, _, _ = CONFIGS[name]
     return generate(max(1, int(nu * scale)), max(1, int(ni * scale)), max(1, int(n * scale)), **kw)
+
+
+def fingerprint(*arrays) -> str:
+    """sha256 over the raw bytes of the given arrays (pins a committed fixture to its data)."""
+    h = hashlib.sha256()
+    for a in arrays:
+        h.update(np.ascontiguousarray(a).view(np.uint8).data)
+    return h.hexdigest()

@@ -264,10 +264,14 @@ def sgd_delta(lr: float, rating: float, user: List[float], item: List[float]):
 
 def online_sequential(ratings: Sequence[Tuple[int, int, float]], users: Dict[int, List[float]],
                       items: Dict[int, List[float]], k: int, lr: float, flavour: str = "next",
-                      init=pseudo_random_factor) -> Tuple[List[int], List[int]]:
+                      init=pseudo_random_factor, emitted: list | None = None) -> Tuple[List[int], List[int]]:
     """FlinkOnlineMF (fl/mf/online/FlinkOnlineMF.scala:52-137) under synchronous feedback: ratings
     applied in arrival order, each user FIFO (LockableStateWithQueue), first touch initialises.
     flavour "delta" is the PS path (PSOfflineOnlineMF.scala:167-180): vec + delta.
+    emitted (optional list): per rating, the pair of vectors the operator emits --
+    "next": (nextUserVector, nextItemVector), ItemOperator's out.collect (FlinkOnlineMF.scala:131-135);
+    "delta": (userVec + deltaItemVec, deltaItemVec), the worker's ps.output (:176) with userVec the
+    vector before this rating's update, and the vector pushed to the PS (:174).
     Returns the user / item ids touched, in first-touch order."""
     tu, ti = [], []
     for u, i, r in ratings:
@@ -277,10 +281,14 @@ def online_sequential(ratings: Sequence[Tuple[int, int, float]], users: Dict[int
             items[i] = init(i, k)
         if flavour == "delta":
             du, di = sgd_delta(lr, r, users[u], items[i])
+            if emitted is not None:
+                emitted.append(([a + b for a, b in zip(users[u], di)], list(di)))
             users[u] = [a + b for a, b in zip(users[u], du)]
             items[i] = [a + b for a, b in zip(items[i], di)]
         else:
             users[u], items[i] = sgd_next_factors(lr, r, users[u], items[i])
+            if emitted is not None:
+                emitted.append((list(users[u]), list(items[i])))
         if u not in tu:
             tu.append(u)
         if i not in ti:

@@ -73,3 +73,27 @@ def test_last_error_is_set():
     lib = L.lib()
     assert lib.mf_jvm_shuffle(0, -1, None) == L.MF_ERR_INVALID
     assert b"bad argument" in lib.mf_last_error()
+
+
+def test_jni_shim_compiles_against_the_header():
+    """jni/mfhip_jni.c (the binding INTEGRATION.md gives a Scala maintainer) against include/mfhip.h:
+    every call's arity and pointer types must match the C ABI (-Werror).  No JDK here, so a
+    minimal jni.h stand-in (tests/jni_stub) supplies the JNI types; nothing is linked or run."""
+    import shutil
+    import subprocess
+    gcc = shutil.which("gcc")
+    if gcc is None:
+        pytest.skip("no gcc")
+    r = subprocess.run([gcc, "-std=c99", "-fsyntax-only", "-Wall", "-Wextra", "-Wno-unused-parameter", "-Werror",
+                        "-Werror=incompatible-pointer-types", "-Werror=implicit-function-declaration",
+                        "-I", os.path.join(ROOT, "tests", "jni_stub"), "-I", os.path.join(ROOT, "include"),
+                        os.path.join(ROOT, "jni", "mfhip_jni.c")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+def test_every_java_native_has_a_jni_function():
+    java = open(os.path.join(ROOT, "jni", "MfHip.java")).read()
+    natives = set(re.findall(r"public static native [\w\[\]]+ (\w+)\(", java))
+    shim = open(os.path.join(ROOT, "jni", "mfhip_jni.c")).read()
+    defined = set(re.findall(r"JFN\((\w+)\)\(", shim))
+    assert natives and natives == defined, (natives ^ defined)

@@ -128,16 +128,48 @@ def test_ps_offline_online_matches_oracle():
             rs = list(zip(u.tolist(), i.tolist(), r.tolist()))
             hist += rs
             uu, iu = m.process(u, i, r)
-            O.online_sequential(rs, users, items, k, lr, "delta")
+            emitted = []
+            O.online_sequential(rs, users, items, k, lr, "delta", emitted=emitted)
             assert set(uu) == set(u.tolist()) and set(iu) == set(i.tolist())
+            assert np.array_equal(m.output[0], u)
         else:
             uu, iu = m.batch()
             items = {}
+            emitted = []
             for _ in range(iters):
-                O.online_sequential(hist, users, items, k, lr, "delta")
+                O.online_sequential(hist, users, items, k, lr, "delta", emitted=emitted)
             assert set(uu) == set(users) and set(iu) == set(items)
+        # the worker's per-rating stream, ps.output(user, userVec + deltaItemVec) (:176), bit-exact
+        assert np.array_equal(m.output[1], np.array([a for a, _ in emitted])), s
         for a, v in uu.items():
             assert np.array_equal(v, np.array(users[a])), (s, "user", a)
         for a, v in iu.items():
             assert np.array_equal(v, np.array(items[a])), (s, "item", a)
     m.close()
+
+
+@pytest.mark.parametrize("flavour,name", [(L.ONLINE_NEXT_FACTORS, "next"), (L.ONLINE_DELTA, "delta")])
+def test_per_rating_outputs_bit_exact(flavour, name):
+    """mf_online_update_out: the records the operators emit per rating -- Flink's ItemOperator
+    (user', item') (FlinkOnlineMF.scala:131-135), the PS worker (userVec + deltaItemVec,
+    deltaItemVec) (PSOfflineOnlineMF.scala:174-176) -- in arrival order over several dependency
+    levels (repeated users and items), bit-exact against the oracle's sequential replay."""
+    rng = np.random.default_rng(17)
+    n, k, lr = 5000, 24, 0.004
+    u = rng.integers(0, 300, n).astype(np.int32)
+    i = (rng.zipf(1.4, n) % 120).astype(np.int32)
+    r = rng.integers(1, 6, n).astype(np.float64)
+    p = L.default_params()
+    p.num_factors, p.online_learning_rate = k, lr
+    with mfhip.Context(p) as ctx:
+        uo, io = ctx.online_update_out(u[:3000], i[:3000], r[:3000], flavour)
+        uo2, io2 = ctx.online_update_out(u[3000:], i[3000:], r[3000:], flavour)
+        fu, fi = ctx.factors(0), ctx.factors(1)
+    users, items, emitted = {}, {}, []
+    O.online_sequential(list(zip(u.tolist(), i.tolist(), r.tolist())), users, items, k, lr, name, emitted=emitted)
+    assert np.array_equal(np.concatenate([uo, uo2]), np.array([a for a, _ in emitted]))
+    assert np.array_equal(np.concatenate([io, io2]), np.array([b for _, b in emitted]))
+    assert np.array_equal(fu[1], np.array([users[x] for x in fu[0].tolist()]))
+    assert np.array_equal(fi[1], np.array([items[x] for x in fi[0].tolist()]))
+    with mfhip.Context(p) as ctx, pytest.raises(mfhip.MFError, match="touched rows"):
+        ctx.online_update_out(u[:10], i[:10], r[:10], L.ONLINE_SPARK_SWEEP)
