@@ -72,6 +72,16 @@ void launch_sweep_pair_sys(hipStream_t st, const SysWave* sw, const WaveDesc* sy
                            float* U, float* I, uint64_t u_bytes, uint64_t i_bytes, int k, float eta, int32_t* prog,
                            uint32_t base, int32_t* err, uint64_t* trace, hipEvent_t ev0, hipEvent_t ev1);
 
+// Deterministic persistent sweep (kernels_detsweep.hip): one launch per superstep, nw waves of
+// 64 lanes, all of which must be resident at once (nw <= det_sweep_capacity(k)).  Entries are
+// build_det_step's SoA arrays; ticket: one int32 per user row, zero before the launch; err[0]
+// set when a wave gave up waiting.  ev0 / ev1 (may be null): dispatch-recorded timing events.
+int det_sweep_capacity(int k);
+void launch_det_sweep(hipStream_t st, const DetWave* waves, int nw, const uint32_t* eu, const uint32_t* ei,
+                      const uint32_t* eq, const double* er, double* U, double* I, const double* regU,
+                      const double* regI, int k, double eta, int32_t* ticket, int32_t* err, hipEvent_t ev0,
+                      hipEvent_t ev1);
+
 // Gather-dot over resolved pairs (row -1 = unknown id).  out[j] = p.q summed left to right in
 // f64 (predictRating's ddot).  When r != nullptr every workgroup writes partials[3*wg + c]:
 //   c=0: sum (r - p.q)^2, c=1: matched count, c=2: sum mult*((r-p.q)^2 + lambda*(p.p + q.q)).

@@ -18,6 +18,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <future>
 #include <memory>
 #include <mutex>
 #include <numeric>
@@ -49,6 +50,16 @@ struct DeviceGuard {
     if (_r != ncclSuccess) ::mfhip::fail(MF_ERR_COMM, std::string(#call) + ": " + ncclGetErrorString(_r)); \
   } while (0)
 
+// Deterministic persistent sweep: one superstep's entries, staged in pinned memory by a host
+// thread while the previous superstep runs, then copied to the device (fixed SoA offsets).
+struct DetBuf {
+  PinnedBuf pin;
+  DevBuf dev;
+  hipEvent_t copied = nullptr;  // the H2D from `pin` finished (pin may be rewritten)
+  bool pending = false;         // `copied` was recorded and not yet waited for
+  int64_t n = 0, nw = 0, keeps = 0, defers = 0;
+};
+
 struct Shard {
   int device = 0;
   int index = 0;  // global shard index (== rank in rank mode)
@@ -75,6 +86,11 @@ struct Shard {
   DevBuf st_split;                      // hot-item replicas (SplitItem), superstep-major
   std::vector<int64_t> st_split_off;    // per superstep (n + 1)
   std::vector<double> sm_bytes;         // per superstep index (s-1) mod n: bytes the sweep requests
+  // deterministic persistent sweep (kernels_detsweep.hip)
+  DetSweepLayout det_layout;
+  DetBuf det_buf[2];
+  DevBuf det_ticket, det_err;
+  int64_t det_n_max = 0, det_nw_max = 0;
   // evaluation scratch
   DevBuf ev_u, ev_i, ev_r, ev_mult, ev_out, ev_part;
   // profiling
@@ -107,6 +123,7 @@ struct mf_ctx {
   bool fast_persistent = false;  // MFHIP_FAST_KERNEL=persistent selects the systolic single launch
   bool fast_pair = false;         // two updates per step (kernels_pair.hip), k in {64, 128, 256}
   bool fast_sys = false;          // pair cells as one systolic launch per superstep (k_sweep_pair_sys)
+  bool det_sweep = false;         // deterministic mode: one persistent k_det_sweep launch per superstep
   std::vector<int64_t> fast_rb_size;  // per rating block (fast mode)
   mf_stats stats{};
   bool profiling = false;
@@ -177,6 +194,8 @@ void destroy_shard(Shard& s) {
   (void)hipStreamSynchronize(s.stream);
   for (auto e : s.ev) (void)hipEventDestroy(e);
   s.ev.clear();
+  for (auto& b : s.det_buf)
+    if (b.copied) (void)hipEventDestroy(b.copied);
   (void)hipEventDestroy(s.done);
   (void)hipStreamDestroy(s.stream);
   s.stream = nullptr;
@@ -360,15 +379,19 @@ void sync_all(mf_ctx* ctx) {
   for (auto& s : ctx->shards) {
     DeviceGuard g(s.device);
     MF_HIP(hipStreamSynchronize(s.stream));
-    if (s.fast_err.get()) {
+    for (DevBuf* eb : {&s.fast_err, &s.det_err}) {
+      if (!eb->get()) continue;
       int32_t err = 0;
-      MF_HIP(hipMemcpy(&err, s.fast_err.get(), sizeof(err), hipMemcpyDeviceToHost));
+      MF_HIP(hipMemcpy(&err, eb->get(), sizeof(err), hipMemcpyDeviceToHost));
       if (err) {
-        MF_HIP(hipMemset(s.fast_err.get(), 0, sizeof(err)));
-        // waves that gave up skipped the rest of their cells: the model is partly updated, so
+        MF_HIP(hipMemset(eb->get(), 0, sizeof(err)));
+        // waves that gave up skipped the rest of their work: the model is partly updated, so
         // the context refuses further supersteps and reads until the fit is prepared again
-        ctx->failed = "fast sweep: a wave waited > 1 s for its neighbour (workgroups not co-resident?); "
-                      "set MFHIP_PAIR_SYS=0 (or MFHIP_FAST_KERNEL=cell)";
+        ctx->failed = eb == &s.fast_err
+                          ? "fast sweep: a wave waited > 1 s for its neighbour (workgroups not co-resident?); "
+                            "set MFHIP_PAIR_SYS=0 (or MFHIP_FAST_KERNEL=cell)"
+                          : "deterministic sweep: a wave waited > 1 s for a user ticket (waves not co-resident?); "
+                            "set MFHIP_DET_KERNEL=level";
         fail(MF_ERR_TIMEOUT, ctx->failed);
       }
     }
@@ -669,9 +692,143 @@ void ring_shift(mf_ctx* ctx, int64_t superstep) {
   }
 }
 
+// Fixed SoA layout of a DetBuf for at most n entries and nw waves (256-B aligned regions).
+struct DetOffsets {
+  size_t waves, u, i, qf, r, total;
+};
+DetOffsets det_offsets(int64_t n, int64_t nw) {
+  auto up = [](size_t x) { return (x + 255) & ~static_cast<size_t>(255); };
+  DetOffsets o;
+  o.waves = 0;
+  o.u = up(static_cast<size_t>(nw) * sizeof(DetWave));
+  o.i = o.u + up(static_cast<size_t>(n) * 4);
+  o.qf = o.i + up(static_cast<size_t>(n) * 4);
+  o.r = o.qf + up(static_cast<size_t>(n) * 4);
+  o.total = o.r + up(static_cast<size_t>(n) * 8);
+  return o;
+}
+
+// The rating blocks shard s runs in superstep `superstep` and their shuffle seeds
+// (new Random(iteration ^ ratingBlockId ^ seed), DSGDforMF.scala:392).
+void det_blocks(const mf_ctx* ctx, const Shard& s, int64_t superstep, std::vector<int64_t>& blocks,
+                std::vector<int64_t>& seeds) {
+  const int32_t n = ctx->nb;
+  const int32_t iteration = static_cast<int32_t>(superstep / n);
+  blocks.clear();
+  seeds.clear();
+  for (int32_t j = 0; j < ctx->c; ++j) {
+    const int32_t p = s.index * ctx->c + j;
+    const int32_t q = static_cast<int32_t>((p + superstep - 1) % n);
+    const int64_t b = static_cast<int64_t>(p) * n + q;  // toRatingBlockId (:597-601)
+    if (ctx->rb.size(b) == 0) continue;
+    blocks.push_back(b);
+    seeds.push_back(static_cast<int64_t>(iteration ^ static_cast<int32_t>(b)) ^ ctx->P.seed);
+  }
+}
+
+// Host side of one superstep for every local shard, into det_buf[slot] (runs on a worker thread
+// while the device runs the previous superstep).
+void det_build(mf_ctx* ctx, int64_t superstep, int slot) {
+  std::vector<int64_t> blocks, seeds;
+  for (auto& s : ctx->shards) {
+    DetBuf& db = s.det_buf[slot];
+    det_blocks(ctx, s, superstep, blocks, seeds);
+    db.n = db.nw = db.keeps = db.defers = 0;
+    for (int64_t b : blocks) {
+      db.n += ctx->rb.size(b);
+      db.nw += s.det_layout.block_waves[b];
+    }
+    if (db.n == 0) continue;
+    const DetOffsets o = det_offsets(s.det_n_max, s.det_nw_max);
+    char* base = db.pin.as<char>();
+    DetStepOut out{reinterpret_cast<DetWave*>(base + o.waves), reinterpret_cast<uint32_t*>(base + o.u),
+                   reinterpret_cast<uint32_t*>(base + o.i), reinterpret_cast<uint32_t*>(base + o.qf),
+                   reinterpret_cast<double*>(base + o.r)};
+    build_det_step(ctx->rb, ctx->U, ctx->I, s.det_layout, blocks, seeds, ctx->P.has_seed != 0, out);
+    for (int64_t x = 0; x < db.n; ++x) {
+      db.keeps += (out.qf[x] & kDetKeepQ) != 0;
+      db.defers += (out.qf[x] & kDetDeferQ) != 0;
+    }
+  }
+}
+
+// Deterministic supersteps with the persistent sweep: the host builds superstep s+1's entries
+// while the device runs superstep s.
+void det_run(mf_ctx* ctx, int64_t count) {
+  const int k = ctx->P.num_factors;
+  const int64_t s0 = ctx->superstep_done + 1;
+  for (auto& sh : ctx->shards)  // a previous call's last copies may still read the staging buffers
+    for (auto& db : sh.det_buf)
+      if (db.pending) {
+        DeviceGuard g(sh.device);
+        MF_HIP(hipEventSynchronize(db.copied));
+        db.pending = false;
+      }
+  std::future<void> next = std::async(std::launch::async, det_build, ctx, s0, 0);
+  for (int64_t x = 0; x < count; ++x) {
+    const int64_t s = s0 + x;
+    const int slot = static_cast<int>(x & 1);
+    next.get();
+    const int32_t iteration = static_cast<int32_t>(s / ctx->nb);  // :476
+    const double eta = learning_rate(ctx->P.lr_method, ctx->P.learning_rate, iteration + 1, ctx->P.lambda,
+                                     ctx->P.lr_arg);  // :383-386
+    for (auto& sh : ctx->shards) {
+      DetBuf& db = sh.det_buf[slot];
+      if (db.n == 0) continue;
+      DeviceGuard g(sh.device);
+      const DetOffsets o = det_offsets(sh.det_n_max, sh.det_nw_max);
+      const char* hp = db.pin.as<char>();
+      char* dp = db.dev.as<char>();
+      const std::pair<size_t, size_t> regions[] = {{o.waves, static_cast<size_t>(db.nw) * sizeof(DetWave)},
+                                                   {o.u, static_cast<size_t>(db.n) * 4},
+                                                   {o.i, static_cast<size_t>(db.n) * 4},
+                                                   {o.qf, static_cast<size_t>(db.n) * 4},
+                                                   {o.r, static_cast<size_t>(db.n) * 8}};
+      for (const auto& rg : regions)
+        MF_HIP(hipMemcpyAsync(dp + rg.first, hp + rg.first, rg.second, hipMemcpyHostToDevice, sh.stream));
+      if (!db.copied) MF_HIP(hipEventCreateWithFlags(&db.copied, hipEventDisableTiming));
+      MF_HIP(hipEventRecord(db.copied, sh.stream));
+      db.pending = true;
+      MF_HIP(hipMemsetAsync(sh.det_ticket.get(), 0, sh.det_ticket.bytes(), sh.stream));
+      LaunchTimer tm(sh, ctx->profiling, true);
+      launch_det_sweep(sh.stream, reinterpret_cast<const DetWave*>(dp + o.waves), static_cast<int>(db.nw),
+                       reinterpret_cast<const uint32_t*>(dp + o.u), reinterpret_cast<const uint32_t*>(dp + o.i),
+                       reinterpret_cast<const uint32_t*>(dp + o.qf), reinterpret_cast<const double*>(dp + o.r),
+                       sh.uf.as<double>(), sh.itf.as<double>(), sh.regu.as<double>(), sh.regi.as<double>(), k, eta,
+                       sh.det_ticket.as<int32_t>(), sh.det_err.as<int32_t>(), tm.start(), tm.stop());
+      MF_HIP(hipGetLastError());
+      ctx->stats.updates += db.n;
+      ctx->stats.kernel_launches += 1;
+      // rows: user in + out per update, item in / out where not kept in registers; per update
+      // the 20-B entry, two lambda/omega doubles and the ticket poll + store
+      ctx->stats.moved_bytes += 8.0 * k * static_cast<double>(4 * db.n - db.keeps - db.defers) + 44.0 * db.n;
+    }
+    ring_shift(ctx, s);
+    ctx->superstep_done = s;
+    ctx->stats.supersteps++;
+    if (x + 1 < count) {
+      const int other = slot ^ 1;  // superstep s-1's staging buffer: its copy must be done
+      for (auto& sh : ctx->shards) {
+        DetBuf& db = sh.det_buf[other];
+        if (db.pending) {
+          DeviceGuard g(sh.device);
+          MF_HIP(hipEventSynchronize(db.copied));
+          db.pending = false;
+        }
+      }
+      next = std::async(std::launch::async, det_build, ctx, s + 1, other);
+    }
+  }
+  ctx->stats.algorithmic_bytes = static_cast<double>(ctx->stats.updates) * bytes_per_update(ctx);
+}
+
 void run_supersteps(mf_ctx* ctx, int64_t count) {
   MF_REQUIRE(ctx->prepared, "mf_dsgd_run before mf_dsgd_prepare");
   require_healthy(ctx);
+  if (ctx->f64 && ctx->det_sweep) {
+    if (count > 0) det_run(ctx, count);
+    return;
+  }
   for (int64_t x = 0; x < count; ++x) {
     const int64_t s = ctx->superstep_done + 1;
     const int32_t iteration = static_cast<int32_t>(s / ctx->nb);  // getSuperstepNumber / numBlocks (:476)
@@ -711,6 +868,54 @@ struct PhaseClock {
   }
 };
 
+// Deterministic mode: the persistent sweep's item -> wave layout and staging buffers, unless
+// MFHIP_DET_KERNEL=level (one launch per dependency level, det_superstep) or the device cannot
+// hold a superstep's waves.  Waves per superstep and shard: half the device's resident capacity
+// (shared by the shards on that device; MFHIP_DET_WAVES overrides).
+void prepare_det_sweep(mf_ctx* ctx) {
+  const char* kv = std::getenv("MFHIP_DET_KERNEL");
+  if (kv && std::string(kv) == "level") return;
+  int cap = 1 << 30;
+  for (auto& s : ctx->shards) {
+    DeviceGuard g(s.device);
+    int sharers = 0;
+    for (auto& o : ctx->shards) sharers += o.device == s.device;
+    if (const char* v = std::getenv("MFHIP_DEVICE_SHARERS"))
+      if (ctx->rank_mode) sharers = std::max(sharers, std::atoi(v));
+    cap = std::min(cap, det_sweep_capacity(ctx->P.num_factors) / std::max(1, sharers));
+  }
+  if (cap < 1) return;
+  int32_t waves = std::max(1, cap / 2);
+  if (const char* v = std::getenv("MFHIP_DET_WAVES")) waves = std::clamp(std::atoi(v), 1, cap);
+  const int32_t n = ctx->nb;
+  for (auto& s : ctx->shards) {
+    build_det_layout(s.det_layout, ctx->rb, ctx->U, ctx->I, ctx->c, s.index, waves);
+    s.det_n_max = s.det_nw_max = 0;
+    for (int32_t sm = 0; sm < n; ++sm) {
+      int64_t cnt = 0, nw = 0;
+      for (int32_t j = 0; j < ctx->c; ++j) {
+        const int32_t p = s.index * ctx->c + j;
+        const int64_t b = static_cast<int64_t>(p) * n + (p + sm) % n;
+        cnt += ctx->rb.size(b);
+        nw += s.det_layout.block_waves[b];
+      }
+      s.det_n_max = std::max(s.det_n_max, cnt);
+      s.det_nw_max = std::max(s.det_nw_max, nw);
+    }
+    DeviceGuard g(s.device);
+    const size_t bytes = std::max<size_t>(det_offsets(s.det_n_max, s.det_nw_max).total, 256);
+    for (auto& db : s.det_buf) {
+      if (db.pending) { MF_HIP(hipEventSynchronize(db.copied)); db.pending = false; }
+      db.pin.alloc(bytes);
+      db.dev.alloc(bytes);
+    }
+    s.det_ticket.alloc(static_cast<size_t>(std::max<int64_t>(ctx->U.rows(), 1)) * 4);
+    s.det_err.alloc(16);
+    MF_HIP(hipMemset(s.det_err.get(), 0, 16));
+  }
+  ctx->det_sweep = true;
+}
+
 void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, int64_t n) {
   MF_REQUIRE(n >= 0, "negative rating count");
   MF_REQUIRE(n == 0 || (u && i && r), "null rating arrays");
@@ -727,6 +932,9 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
   build_rating_blocks(ctx->rb, ctx->U, ctx->I, u, i, r, n, lo, hi, ctx->f64 && ctx->P.has_seed);
   clk.lap("rating blocks");
   const int64_t nb2 = static_cast<int64_t>(ctx->nb) * ctx->nb;
+  ctx->det_sweep = false;
+  if (ctx->f64) prepare_det_sweep(ctx);
+  clk.lap("deterministic sweep layout");
   if (!ctx->f64) {
     const int64_t local = ctx->rb.start[nb2];
     const int64_t blocks_local = static_cast<int64_t>(hi - lo) * ctx->nb;

@@ -273,6 +273,111 @@ void build_level_plan(const std::vector<OrderedSeq>& seqs, LevelPlan& out, std::
   });
 }
 
+// ---------------------------------------------------------------------------------------
+// Deterministic persistent sweep (plan.hpp DetSweepLayout).
+void build_det_layout(DetSweepLayout& L, const RatingBlocks& rb, const SideLayout& U, const SideLayout& I, int32_t c,
+                      int32_t shard, int32_t waves_per_superstep) {
+  (void)U;
+  const int32_t nb = rb.n_blocks;
+  const int64_t nb2 = static_cast<int64_t>(nb) * nb;
+  L.block_waves.assign(nb2, 0);
+  L.item_wave.assign(nb2, {});
+  // per superstep sm: the shard's blocks (p, (p+sm) mod n) share the wave budget by size
+  for (int32_t sm = 0; sm < nb; ++sm) {
+    int64_t total = 0;
+    for (int32_t j = 0; j < c; ++j) {
+      const int32_t p = shard * c + j;
+      total += rb.size(static_cast<int64_t>(p) * nb + (p + sm) % nb);
+    }
+    if (total == 0) continue;
+    for (int32_t j = 0; j < c; ++j) {
+      const int32_t p = shard * c + j;
+      const int64_t b = static_cast<int64_t>(p) * nb + (p + sm) % nb;
+      if (rb.size(b) == 0) continue;
+      L.block_waves[b] = static_cast<int32_t>(
+          std::max<int64_t>(1, static_cast<int64_t>(waves_per_superstep) * rb.size(b) / total));
+    }
+  }
+  parallel_tasks(nb2, [&](int64_t b) {
+    if (L.block_waves[b] == 0) return;
+    const int32_t q = static_cast<int32_t>(b % nb);
+    const int64_t i0 = I.block_start[q], ni = I.block_start[q + 1] - i0;
+    std::vector<int64_t> cnt(ni, 0);
+    for (int64_t x = rb.start[b]; x < rb.start[b + 1]; ++x) cnt[rb.irow[x] - i0]++;
+    std::vector<int32_t> items;
+    for (int64_t x = 0; x < ni; ++x)
+      if (cnt[x] > 0) items.push_back(static_cast<int32_t>(x));
+    const int32_t W = std::max<int32_t>(1, std::min<int32_t>(L.block_waves[b], static_cast<int32_t>(items.size())));
+    L.block_waves[b] = W;
+    // LPT: heaviest item first onto the least-loaded wave (ties: lower wave), so the hottest
+    // items sit alone in their waves
+    std::stable_sort(items.begin(), items.end(), [&](int32_t a, int32_t c2) { return cnt[a] > cnt[c2]; });
+    using Load = std::pair<int64_t, int32_t>;
+    std::priority_queue<Load, std::vector<Load>, std::greater<Load>> heap;
+    for (int32_t w = 0; w < W; ++w) heap.emplace(0, w);
+    auto& iw = L.item_wave[b];
+    iw.assign(ni, -1);
+    for (int32_t it : items) {
+      Load top = heap.top();
+      heap.pop();
+      iw[it] = top.second;
+      top.first += cnt[it];
+      heap.push(top);
+    }
+  });
+}
+
+void build_det_step(const RatingBlocks& rb, const SideLayout& U, const SideLayout& I, const DetSweepLayout& L,
+                    const std::vector<int64_t>& blocks, const std::vector<int64_t>& seeds, bool seeded,
+                    const DetStepOut& out) {
+  const int32_t nb = rb.n_blocks;
+  const int64_t nbk = static_cast<int64_t>(blocks.size());
+  std::vector<int64_t> e0(nbk + 1, 0), w0(nbk + 1, 0);  // entry / wave offsets of each block
+  for (int64_t x = 0; x < nbk; ++x) {
+    e0[x + 1] = e0[x] + rb.size(blocks[x]);
+    w0[x + 1] = w0[x] + L.block_waves[blocks[x]];
+  }
+  std::vector<uint64_t> rseeds(nbk);
+  if (!seeded) {
+    std::random_device rd;
+    for (auto& v : rseeds) v = (static_cast<uint64_t>(rd()) << 32) ^ rd();
+  }
+  parallel_tasks(nbk, [&](int64_t x) {
+    const int64_t b = blocks[x], len = rb.size(b), st = rb.start[b];
+    if (len == 0) return;
+    const int32_t p = static_cast<int32_t>(b / nb), q = static_cast<int32_t>(b % nb);
+    const int64_t u0 = U.block_start[p], nu = U.block_start[p + 1] - u0, i0 = I.block_start[q];
+    std::vector<int32_t> order(len);
+    JavaRandom rng(seeded ? seeds[x] : static_cast<int64_t>(rseeds[x]));
+    scala_shuffle(rng, order.data(), len);  // DSGDforMF.scala:392-393
+    const auto& iw = L.item_wave[b];
+    const int32_t W = L.block_waves[b];
+    std::vector<int64_t> woff(W + 1, 0);
+    for (int64_t j = 0; j < len; ++j) woff[iw[rb.irow[st + order[j]] - i0] + 1]++;
+    for (int32_t w = 0; w < W; ++w) woff[w + 1] += woff[w];
+    for (int32_t w = 0; w < W; ++w)
+      out.waves[w0[x] + w] = DetWave{e0[x] + woff[w], static_cast<int32_t>(woff[w + 1] - woff[w]), 0};
+    std::vector<int32_t> useq(nu, 0);
+    std::vector<int64_t> cur(woff.begin(), woff.end() - 1);
+    for (int64_t j = 0; j < len; ++j) {
+      const int64_t e = st + order[j];
+      const uint32_t ur = rb.urow[e], ir = rb.irow[e];
+      const int64_t at = e0[x] + cur[iw[ir - i0]]++;
+      out.u[at] = ur;
+      out.i[at] = ir;
+      out.qf[at] = static_cast<uint32_t>(useq[ur - u0]++);
+      out.r[at] = rb.r[e];
+    }
+    for (int32_t w = 0; w < W; ++w) {  // items repeated back to back stay in registers
+      const int64_t a = e0[x] + woff[w], z = e0[x] + woff[w + 1];
+      for (int64_t y = a; y < z; ++y) {
+        if (y > a && out.i[y - 1] == out.i[y]) out.qf[y] |= kDetKeepQ;
+        if (y + 1 < z && out.i[y + 1] == out.i[y]) out.qf[y] |= kDetDeferQ;
+      }
+    }
+  });
+}
+
 // G trades launch/cell overhead and the record padding forced by heavy users (large G) against
 // cell imbalance (small G).  The per-superstep critical path is the sum over sub-steps of the
 // longest cell; on the NFLX-shaped synthetic it is minimal near ~150 ratings per average cell

@@ -90,6 +90,46 @@ struct OrderedSeq {
 // src (optional): per entry, its index e into the sequence's u / i / r arrays (single sequence).
 void build_level_plan(const std::vector<OrderedSeq>& seqs, LevelPlan& out, std::vector<int32_t>* src = nullptr);
 
+// Deterministic mode, one persistent launch per superstep (kernels_detsweep.hip).  Every item
+// of a rating block belongs to one wave (LPT over rating counts, fixed for the whole fit), which
+// applies the updates of its items in the reference's shuffled order (DSGDforMF.scala:392-413);
+// the only cross-wave dependency left is a user's previous update, which the wave awaits through
+// a per-user ticket (useq = the number of earlier updates of that user in the superstep).  Every
+// wave's entries are in increasing shuffle position, so the unfinished entry with the smallest
+// position can always run: with all waves resident the sweep cannot deadlock.
+constexpr uint32_t kDetUseqMask = (1u << 30) - 1;
+constexpr uint32_t kDetKeepQ = 1u << 30;   // same item as the wave's previous entry: row in registers
+constexpr uint32_t kDetDeferQ = 1u << 31;  // same item as the wave's next entry: no store yet
+struct DetWave {
+  int64_t begin;  // first entry
+  int32_t count;
+  int32_t pad_;
+};
+static_assert(sizeof(DetWave) == 16, "DetWave is one 16-B word");
+
+struct DetSweepLayout {
+  std::vector<int32_t> block_waves;             // n*n: waves of each rating block of this shard (0: none)
+  std::vector<std::vector<int32_t>> item_wave;  // n*n: local item row of the block's item block -> wave
+};
+// waves_per_superstep: budget of resident waves for one superstep of this shard; every block of a
+// superstep gets a share proportional to its ratings (>= 1, <= its distinct items).
+void build_det_layout(DetSweepLayout& L, const RatingBlocks& rb, const SideLayout& U, const SideLayout& I, int32_t c,
+                      int32_t shard, int32_t waves_per_superstep);
+
+// One superstep's entries (SoA, wave-major, each wave in shuffle-position order) for the rating
+// blocks `blocks` with their shuffle seeds (order = scala_shuffle(new Random(seed)), :392-393;
+// seeded = false: a random seed).  Sizes: waves = sum of block_waves, entries = sum of block sizes.
+struct DetStepOut {
+  DetWave* waves;
+  uint32_t* u;   // global user row
+  uint32_t* i;   // global item row
+  uint32_t* qf;  // useq | kDetKeepQ | kDetDeferQ
+  double* r;
+};
+void build_det_step(const RatingBlocks& rb, const SideLayout& U, const SideLayout& I, const DetSweepLayout& L,
+                    const std::vector<int64_t>& blocks, const std::vector<int64_t>& seeds, bool seeded,
+                    const DetStepOut& out);
+
 // ---------------------------------------------------------------------------------------
 // Fast mode.
 // Fast-mode record (32 B).  The kernel reads the first five words: byte offsets of the user

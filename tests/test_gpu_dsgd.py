@@ -435,3 +435,23 @@ def test_systolic_per_block_groups_equal_their_schedule(monkeypatch, k, nb, wave
     assert np.array_equal(a_ids, uids) and np.array_equal(b_ids, iids)
     np.testing.assert_allclose(a_u, U, rtol=2e-4, atol=2e-5)
     np.testing.assert_allclose(a_i, I, rtol=2e-4, atol=2e-5)
+
+
+@pytest.mark.parametrize("k,nb,shards", [(64, 4, 1), (128, 4, 2), (100, 3, 1), (256, 2, 2)])
+def test_deterministic_persistent_sweep_bit_exact_hot_items(k, nb, shards):
+    """k_det_sweep (one persistent launch per superstep; items owned by waves, per-user tickets)
+    == the C oracle's sequential reference order, bitwise, on data with a very hot item (long
+    same-item runs kept in registers) and heavy users (long ticket chains), on 1 or 2 shards."""
+    d = hot_item_data(k)
+    big = synth.generate(3000, 500, 60000, seed=k)
+    d.u = np.concatenate([d.u, big.u + 1000])
+    d.i = np.concatenate([d.i, big.i])
+    d.r = np.concatenate([d.r, big.r])
+    m = coracle.dsgd_fit(d.u, d.i, d.r, k=k, iterations=2, n_blocks=nb, seed=7, threads=4)
+    with mfhip.Context(params(k, 2, nb, 7), devices=[0] * shards) as ctx:
+        ctx.fit(d.u, d.i, d.r)
+        assert ctx.stats()["kernel_launches"] <= 2 * nb * shards  # the persistent sweep ran
+        for side in (0, 1):
+            ids, vecs = ctx.factors(side)
+            rids, rvecs = m.factors(side)
+            assert np.array_equal(ids, rids) and np.array_equal(vecs, rvecs)
