@@ -48,91 +48,173 @@ __device__ __forceinline__ void st_sc1(double* p, double v) {
 }
 
 // ((0 + x0) + x1) + ... over f = 0..k-1 (F2jBLAS.ddot / Scala foldLeft order); lane l holds
-// element l + 64c in prod[c].
+// element l + 64c in prod[c].  The products go through a wave-private LDS row and every lane
+// reads them back in order as broadcast 16-B reads, so the dependent f64 add chain takes its
+// operands from VGPRs (a v_readlane per element would add a readlane + hazard nop per add).
 template <int KPL>
-__device__ __forceinline__ double seq_dot(const double (&prod)[KPL], int k) {
+__device__ __forceinline__ double seq_dot(const double (&prod)[KPL], int k, double* lds, int lane) {
+#pragma unroll
+  for (int c = 0; c < KPL; ++c) lds[64 * c + lane] = prod[c];
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the wave's own LDS writes are done
+  __builtin_amdgcn_wave_barrier();
   double acc = 0.0;
-  if (k == 64 * KPL) {  // fully unrolled: the readlanes issue ahead of the dependent add chain
+  const double2* l2 = reinterpret_cast<const double2*>(lds);
+  if (k == 64 * KPL) {
 #pragma unroll
-    for (int c = 0; c < KPL; ++c)
-#pragma unroll
-      for (int l = 0; l < 64; ++l) acc = acc + rld(prod[c], l);
-    return acc;
+    for (int x = 0; x < 32 * KPL; ++x) {
+      const double2 v = l2[x];
+      acc = acc + v.x;
+      acc = acc + v.y;
+    }
+  } else {
+    const int half = k >> 1;
+    for (int x = 0; x < half; ++x) {
+      const double2 v = l2[x];
+      acc = acc + v.x;
+      acc = acc + v.y;
+    }
+    if (k & 1) acc = acc + lds[k - 1];
   }
-#pragma unroll
-  for (int c = 0; c < KPL; ++c) {
-    const int lim = min(64, k - 64 * c);
-    for (int l = 0; l < lim; ++l) acc = acc + rld(prod[c], l);
-  }
+  __builtin_amdgcn_wave_barrier();  // every lane has read before the next entry rewrites the row
   return acc;
 }
 
+// Entry fields of a wave's entry list, 64 per lane-register chunk.
+struct DetChunk {
+  uint32_t u, i, q;
+  double r;
+};
+__device__ __forceinline__ DetChunk det_chunk(const uint32_t* eu, const uint32_t* ei, const uint32_t* eq,
+                                              const double* er, int64_t begin, int64_t count, int64_t c0, int lane) {
+  const int64_t j = c0 + lane;
+  const bool in = j < count;
+  const int64_t x = begin + (in ? j : 0);
+  return DetChunk{in ? eu[x] : 0u, in ? ei[x] : 0u, in ? eq[x] : 0u, in ? er[x] : 0.0};
+}
+
+__device__ __forceinline__ int32_t poll(const int32_t* t) {
+  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// Pipelined per wave: at entry j the row of entry j+1 is prefetched when the ticket poll issued
+// one entry earlier already showed it ready, and entry j+2's ticket is polled; entry j-1's row
+// stores drain while entry j computes, and its ticket is published after that drain (and always
+// before the wave blocks on a ticket, so a published ticket never waits on this wave).
 template <int KPL>
 __global__ __launch_bounds__(64) void k_det_sweep(const DetWave* __restrict__ waves, const uint32_t* __restrict__ eu,
                                                   const uint32_t* __restrict__ ei, const uint32_t* __restrict__ eq,
                                                   const double* __restrict__ er, double* U, double* I,
                                                   const double* __restrict__ regU, const double* __restrict__ regI,
                                                   int k, double eta, int32_t* ticket, int32_t* err) {
+  __shared__ double lds[64 * KPL];
   const int lane = threadIdx.x;
   const DetWave d = waves[blockIdx.x];
-  double q[KPL];
+  const int64_t cnt = d.count;
+  if (cnt == 0) return;
+  auto row_load = [&](double (&v)[KPL], const double* base) {
 #pragma unroll
-  for (int c = 0; c < KPL; ++c) q[c] = 0.0;
-  for (int64_t c0 = 0; c0 < d.count; c0 += 64) {
-    // 64 entries, one per lane (coalesced), broadcast with readlane
-    const int64_t x = d.begin + c0 + lane;
-    const bool in = c0 + lane < d.count;
-    const uint32_t mu = in ? eu[x] : 0u, mi = in ? ei[x] : 0u, mq = in ? eq[x] : 0u;
-    const double mr = in ? er[x] : 0.0;
-    const int n = static_cast<int>(min<int64_t>(64, d.count - c0));
+    for (int c = 0; c < KPL; ++c) {
+      const int f = lane + 64 * c;
+      v[c] = f < k ? ld_sc1(base + f) : 0.0;
+    }
+  };
+  DetChunk C0 = det_chunk(eu, ei, eq, er, d.begin, cnt, 0, lane);
+  DetChunk C1 = det_chunk(eu, ei, eq, er, d.begin, cnt, 64, lane);
+  // fields of entry j + dj (dj in 0..2) relative to the chunk pair (C0 = j's chunk)
+  auto fu = [&](int s, int dj) { return s + dj < 64 ? rl(C0.u, s + dj) : rl(C1.u, s + dj - 64); };
+  auto fq = [&](int s, int dj) { return s + dj < 64 ? rl(C0.q, s + dj) : rl(C1.q, s + dj - 64); };
+
+  double q[KPL], P[KPL];
+#pragma unroll
+  for (int c = 0; c < KPL; ++c) q[c] = P[c] = 0.0;
+  // entry 0: its ticket read now; entry 1's ticket polled ahead
+  int32_t okP = 0;
+  {
+    const uint32_t u0 = rl(C0.u, 0);
+    if (poll(ticket + u0) == static_cast<int32_t>(rl(C0.q, 0) & kDetUseqMask)) {
+      okP = 1;
+      row_load(P, U + static_cast<size_t>(u0) * k);
+    }
+  }
+  int32_t tk1 = cnt > 1 ? poll(ticket + fu(0, 1)) : 0;
+  int32_t* pend = nullptr;  // entry j-1's ticket, published once its stores have drained
+  int32_t pend_val = 0;
+
+  for (int64_t c0 = 0; c0 < cnt; c0 += 64) {
+    if (c0 > 0) {
+      C0 = C1;
+      C1 = det_chunk(eu, ei, eq, er, d.begin, cnt, c0 + 64, lane);
+    }
+    const int n = static_cast<int>(min<int64_t>(64, cnt - c0));
     for (int s = 0; s < n; ++s) {
-      const uint32_t u = rl(mu, s), i = rl(mi, s), qf = rl(mq, s);
-      const double r = rld(mr, s);
+      const int64_t j = c0 + s;
+      const uint32_t u = rl(C0.u, s), i = rl(C0.i, s), qf = rl(C0.q, s);
+      const double r = rld(C0.r, s);
       const int32_t useq = static_cast<int32_t>(qf & kDetUseqMask);
-      int32_t* tk = ticket + u;
-      if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(tk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != useq) {
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
-        for (;;) {
-          __builtin_amdgcn_s_sleep(1);
-          if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(tk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == useq)
-            break;
-          if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0)
-            return;
+      // prefetch entry j+1's row if its ticket was ready when polled; poll entry j+2
+      double PN[KPL];
+      int32_t okN = 0;
+#pragma unroll
+      for (int c = 0; c < KPL; ++c) PN[c] = 0.0;
+      if (j + 1 < cnt) {
+        const uint32_t un = fu(s, 1);
+        if (tk1 == static_cast<int32_t>(fq(s, 1) & kDetUseqMask) && un != u) {
+          okN = 1;
+          row_load(PN, U + static_cast<size_t>(un) * k);
+        }
+      }
+      const int32_t tk2 = j + 2 < cnt ? poll(ticket + fu(s, 2)) : 0;
+      // entry j's user row: prefetched, or (rarely) wait for its ticket now
+      if (!okP) {
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): entry j-1's stores landed
+        if (lane == 0 && pend) __hip_atomic_store(pend, pend_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pend = nullptr;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // bounded wait (100 MHz clock)
+        while (poll(ticket + u) != useq) {
+          if (poll(err) != 0) return;
           if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {  // ~1 s: a producer never ran
             if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return;
           }
+          __builtin_amdgcn_s_sleep(1);
         }
+        row_load(P, U + static_cast<size_t>(u) * k);
       }
-      double* pp = U + static_cast<size_t>(u) * k;
       double* qp = I + static_cast<size_t>(i) * k;
-      double pv[KPL], pr[KPL];
-      const bool keep = (qf & kDetKeepQ) != 0;
-#pragma unroll
-      for (int c = 0; c < KPL; ++c) {
-        const int f = lane + 64 * c;
-        pv[c] = f < k ? ld_sc1(pp + f) : 0.0;
-        if (!keep) q[c] = f < k ? ld_sc1(qp + f) : 0.0;
-      }
+      if (!(qf & kDetKeepQ)) row_load(q, qp);  // the item's previous store drained at entry j-1
       const double ru = regU[u], ri = regI[i];  // lambda / omega (read-only in the sweep)
+      double pr[KPL];
 #pragma unroll
-      for (int c = 0; c < KPL; ++c) pr[c] = pv[c] * q[c];
-      const double e = r - seq_dot<KPL>(pr, k);  // :405
+      for (int c = 0; c < KPL; ++c) pr[c] = P[c] * q[c];
+      const double e = r - seq_dot<KPL>(pr, k, lds, lane);  // :405
+      double pn[KPL];
+#pragma unroll
+      for (int c = 0; c < KPL; ++c) {
+        pn[c] = P[c] - eta * (ru * P[c] - e * q[c]);  // :407-408
+        q[c] = q[c] - eta * (ri * q[c] - e * P[c]);   // :409-410 (old p)
+      }
+      // entry j-1's stores are long issued: drain them and publish its ticket
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+      if (lane == 0 && pend) __hip_atomic_store(pend, pend_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      double* pp = U + static_cast<size_t>(u) * k;
 #pragma unroll
       for (int c = 0; c < KPL; ++c) {
         const int f = lane + 64 * c;
-        const double pn = pv[c] - eta * (ru * pv[c] - e * q[c]);  // :407-408
-        const double qn = q[c] - eta * (ri * q[c] - e * pv[c]);   // :409-410 (old p)
-        q[c] = qn;
         if (f < k) {
-          st_sc1(pp + f, pn);
-          if (!(qf & kDetDeferQ)) st_sc1(qp + f, qn);
+          st_sc1(pp + f, pn[c]);
+          if (!(qf & kDetDeferQ)) st_sc1(qp + f, q[c]);
         }
       }
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this entry's row stores have landed
-      if (lane == 0) __hip_atomic_store(tk, useq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      pend = ticket + u;
+      pend_val = useq + 1;
+#pragma unroll
+      for (int c = 0; c < KPL; ++c) P[c] = PN[c];
+      okP = okN;
+      tk1 = tk2;
     }
   }
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  if (lane == 0 && pend) __hip_atomic_store(pend, pend_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int KPL>
