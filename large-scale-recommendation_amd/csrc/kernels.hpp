@@ -77,10 +77,13 @@ void launch_sweep_pair_sys(hipStream_t st, const SysWave* sw, const WaveDesc* sy
 // build_det_step's SoA arrays; ticket: one int32 per user row, zero before the launch; err[0]
 // set when a wave gave up waiting.  ev0 / ev1 (may be null): dispatch-recorded timing events.
 int det_sweep_capacity(int k);
+// Entry arrays are read in 64-entry chunks up to 192 entries past a wave's end (kDetPad slack).
+// u_bytes / i_bytes: slab sizes (< 4 GiB, 32-bit row offsets); dummy_ticket: a scratch word.
+constexpr int64_t kDetPad = 256;
 void launch_det_sweep(hipStream_t st, const DetWave* waves, int nw, const uint32_t* eu, const uint32_t* ei,
-                      const uint32_t* eq, const double* er, double* U, double* I, const double* regU,
-                      const double* regI, int k, double eta, int32_t* ticket, int32_t* err, hipEvent_t ev0,
-                      hipEvent_t ev1);
+                      const uint32_t* eq, const double* er, double* U, double* I, uint64_t u_bytes, uint64_t i_bytes,
+                      const double* regU, const double* regI, int k, double eta, int32_t* ticket,
+                      int32_t* dummy_ticket, int32_t* err, hipEvent_t ev0, hipEvent_t ev1);
 
 // Gather-dot over resolved pairs (row -1 = unknown id).  out[j] = p.q summed left to right in
 // f64 (predictRating's ddot).  When r != nullptr every workgroup writes partials[3*wg + c]:

@@ -79,109 +79,151 @@ __device__ __forceinline__ double seq_dot(const double (&prod)[KPL], int k, doub
   return acc;
 }
 
-// Entry fields of a wave's entry list, 64 per lane-register chunk.
+// Entry fields of a wave's entry list, 64 per lane-register chunk (the host pads every entry
+// array by 64, so a chunk load never needs a bounds branch).
 struct DetChunk {
   uint32_t u, i, q;
   double r;
 };
 __device__ __forceinline__ DetChunk det_chunk(const uint32_t* eu, const uint32_t* ei, const uint32_t* eq,
-                                              const double* er, int64_t begin, int64_t count, int64_t c0, int lane) {
-  const int64_t j = c0 + lane;
-  const bool in = j < count;
-  const int64_t x = begin + (in ? j : 0);
-  return DetChunk{in ? eu[x] : 0u, in ? ei[x] : 0u, in ? eq[x] : 0u, in ? er[x] : 0.0};
+                                              const double* er, int64_t x) {
+  return DetChunk{eu[x], ei[x], eq[x], er[x]};
 }
 
 __device__ __forceinline__ int32_t poll(const int32_t* t) {
   return __builtin_amdgcn_readfirstlane(__hip_atomic_load(t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
+// The same load without reading it: the wave waits for it only where the value is used.
+__device__ __forceinline__ int32_t poll_issue(const int32_t* t) {
+  return __hip_atomic_load(t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
-// Pipelined per wave: at entry j the row of entry j+1 is prefetched when the ticket poll issued
-// one entry earlier already showed it ready, and entry j+2's ticket is polled; entry j-1's row
-// stores drain while entry j computes, and its ticket is published after that drain (and always
-// before the wave blocks on a ticket, so a published ticket never waits on this wave).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t raw_rsrc(const void* base, uint64_t bytes) {
+  const uint32_t n = bytes > 0xFFFFF000ull ? 0xFFFFF000u : static_cast<uint32_t>(bytes);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, n, 0x00020000);
+}
+constexpr int kSC1 = 16;                   // buffer cache policy: sc1 (L1 bypass, write-through)
+constexpr uint32_t kOOB = 0xFFFFF000u;     // a row offset past the slab: the load returns 0, no store
+
+template <int KPL>
+struct DRow {
+  double v[KPL];
+};
+// f64 row of k: lane holds elements lane + 64c at byte voff[c] of the row (voff[c] is past any
+// slab for elements >= k: those lanes load zeros and store nothing); an out-of-range row offset
+// loads zeros and stores nothing.
+template <int KPL>
+__device__ __forceinline__ DRow<KPL> ldrow(__amdgpu_buffer_rsrc_t rs, const uint32_t (&voff)[KPL], uint32_t off) {
+  DRow<KPL> r;
+#pragma unroll
+  for (int c = 0; c < KPL; ++c) {
+    const auto x = __builtin_amdgcn_raw_buffer_load_b64(rs, voff[c], off, kSC1);
+    r.v[c] = __longlong_as_double(static_cast<long long>((static_cast<uint64_t>(x[1]) << 32) | x[0]));
+  }
+  return r;
+}
+template <int KPL>
+__device__ __forceinline__ void strow(__amdgpu_buffer_rsrc_t rs, const uint32_t (&voff)[KPL], uint32_t off,
+                                      const double (&v)[KPL]) {
+  using u2 = uint32_t __attribute__((ext_vector_type(2)));
+#pragma unroll
+  for (int c = 0; c < KPL; ++c) {
+    const uint64_t b = static_cast<uint64_t>(__double_as_longlong(v[c]));
+    __builtin_amdgcn_raw_buffer_store_b64(u2{static_cast<uint32_t>(b), static_cast<uint32_t>(b >> 32)}, rs, voff[c],
+                                          off, kSC1);
+  }
+}
+
+// vmcnt(N) in the gfx9 encoding (expcnt 7, lgkmcnt 15 left unconstrained).
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70 & ~0xF);
+}
+
+// Per wave, a fixed sequence of memory operations per entry j (so the compiler's vmcnt counting
+// is exact and the prefetches stay in flight across the next entry):
+//   compute j with the user row and item row prefetched at entry j-2 (kept item: registers);
+//   wait until entry j-1's stores have drained (vmcnt(2*KPL + 1): only entry j-1's prefetches
+//   and poll are younger) and publish its ticket;
+//   store j's user row (and item row unless the next entry keeps it);
+//   prefetch entry j+2's user row if its ticket, polled at entry j-1, was ready (else an
+//   out-of-range offset: entry j+2 then waits and loads itself), and its item row unless kept
+//   (issued after entry j's stores: a wave reads its own earlier stores);
+//   poll entry j+3's ticket.
+// A wave blocks on a ticket only after publishing its own pending one, so no published ticket
+// ever waits on the blocked wave.
 template <int KPL>
 __global__ __launch_bounds__(64) void k_det_sweep(const DetWave* __restrict__ waves, const uint32_t* __restrict__ eu,
                                                   const uint32_t* __restrict__ ei, const uint32_t* __restrict__ eq,
                                                   const double* __restrict__ er, double* U, double* I,
-                                                  const double* __restrict__ regU, const double* __restrict__ regI,
-                                                  int k, double eta, int32_t* ticket, int32_t* err) {
+                                                  uint64_t u_bytes, uint64_t i_bytes, const double* __restrict__ regU,
+                                                  const double* __restrict__ regI, int k, double eta,
+                                                  int32_t* ticket, int32_t* dummy_ticket, int32_t* err) {
   __shared__ double lds[64 * KPL];
   const int lane = threadIdx.x;
   const DetWave d = waves[blockIdx.x];
   const int64_t cnt = d.count;
   if (cnt == 0) return;
-  auto row_load = [&](double (&v)[KPL], const double* base) {
+  const __amdgpu_buffer_rsrc_t urs = raw_rsrc(U, u_bytes), irs = raw_rsrc(I, i_bytes);
+  uint32_t voff[KPL];
 #pragma unroll
-    for (int c = 0; c < KPL; ++c) {
-      const int f = lane + 64 * c;
-      v[c] = f < k ? ld_sc1(base + f) : 0.0;
-    }
-  };
-  DetChunk C0 = det_chunk(eu, ei, eq, er, d.begin, cnt, 0, lane);
-  DetChunk C1 = det_chunk(eu, ei, eq, er, d.begin, cnt, 64, lane);
-  // fields of entry j + dj (dj in 0..2) relative to the chunk pair (C0 = j's chunk)
-  auto fu = [&](int s, int dj) { return s + dj < 64 ? rl(C0.u, s + dj) : rl(C1.u, s + dj - 64); };
-  auto fq = [&](int s, int dj) { return s + dj < 64 ? rl(C0.q, s + dj) : rl(C1.q, s + dj - 64); };
+  for (int c = 0; c < KPL; ++c) voff[c] = lane + 64 * c < k ? static_cast<uint32_t>(lane + 64 * c) * 8u : 0x80000000u;
+  const uint32_t rowb = static_cast<uint32_t>(k) * 8u;
 
-  double q[KPL], P[KPL];
+  DetChunk C0 = det_chunk(eu, ei, eq, er, d.begin + lane);
+  DetChunk C1 = det_chunk(eu, ei, eq, er, d.begin + 64 + lane);
+  // prologue: entries 0 and 1 read synchronously, entry 2's ticket polled ahead
+  DRow<KPL> PR[2], QR[2];
+  int32_t OK[2];
 #pragma unroll
-  for (int c = 0; c < KPL; ++c) q[c] = P[c] = 0.0;
-  // entry 0: its ticket read now; entry 1's ticket polled ahead
-  int32_t okP = 0;
-  {
-    const uint32_t u0 = rl(C0.u, 0);
-    if (poll(ticket + u0) == static_cast<int32_t>(rl(C0.q, 0) & kDetUseqMask)) {
-      okP = 1;
-      row_load(P, U + static_cast<size_t>(u0) * k);
-    }
+  for (int y = 0; y < 2; ++y) {
+    const bool live = y < cnt;
+    const uint32_t u = rl(C0.u, y), i = rl(C0.i, y), qf = rl(C0.q, y);
+    OK[y] = live && poll(ticket + u) == static_cast<int32_t>(qf & kDetUseqMask);
+    PR[y] = ldrow<KPL>(urs, voff, OK[y] ? u * rowb : kOOB);
+    QR[y] = ldrow<KPL>(irs, voff, live && !(qf & kDetKeepQ) ? i * rowb : kOOB);
   }
-  int32_t tk1 = cnt > 1 ? poll(ticket + fu(0, 1)) : 0;
-  int32_t* pend = nullptr;  // entry j-1's ticket, published once its stores have drained
+  int32_t TK = poll_issue(cnt > 2 ? ticket + rl(C0.u, 2) : dummy_ticket);
+  int32_t* pend = dummy_ticket;  // entry j-1's ticket word and value, published after its drain
   int32_t pend_val = 0;
+  double q[KPL];
+#pragma unroll
+  for (int c = 0; c < KPL; ++c) q[c] = 0.0;
 
-  for (int64_t c0 = 0; c0 < cnt; c0 += 64) {
-    if (c0 > 0) {
-      C0 = C1;
-      C1 = det_chunk(eu, ei, eq, er, d.begin, cnt, c0 + 64, lane);
-    }
-    const int n = static_cast<int>(min<int64_t>(64, cnt - c0));
-    for (int s = 0; s < n; ++s) {
+  for (int64_t c0 = 0;; c0 += 64) {
+#pragma unroll
+    for (int s = 0; s < 64; ++s) {
       const int64_t j = c0 + s;
+      if (j >= cnt) goto done;
+      const int slot = s & 1;
       const uint32_t u = rl(C0.u, s), i = rl(C0.i, s), qf = rl(C0.q, s);
       const double r = rld(C0.r, s);
       const int32_t useq = static_cast<int32_t>(qf & kDetUseqMask);
-      // prefetch entry j+1's row if its ticket was ready when polled; poll entry j+2
-      double PN[KPL];
-      int32_t okN = 0;
-#pragma unroll
-      for (int c = 0; c < KPL; ++c) PN[c] = 0.0;
-      if (j + 1 < cnt) {
-        const uint32_t un = fu(s, 1);
-        if (tk1 == static_cast<int32_t>(fq(s, 1) & kDetUseqMask) && un != u) {
-          okN = 1;
-          row_load(PN, U + static_cast<size_t>(un) * k);
-        }
-      }
-      const int32_t tk2 = j + 2 < cnt ? poll(ticket + fu(s, 2)) : 0;
-      // entry j's user row: prefetched, or (rarely) wait for its ticket now
-      if (!okP) {
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): entry j-1's stores landed
-        if (lane == 0 && pend) __hip_atomic_store(pend, pend_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        pend = nullptr;
+      if (!OK[slot]) {  // the ticket was not ready at prefetch time: publish ours, wait, load
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        __hip_atomic_store(pend, pend_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pend = dummy_ticket;
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // bounded wait (100 MHz clock)
         while (poll(ticket + u) != useq) {
           if (poll(err) != 0) return;
           if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {  // ~1 s: a producer never ran
-            if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return;
           }
           __builtin_amdgcn_s_sleep(1);
         }
-        row_load(P, U + static_cast<size_t>(u) * k);
+        PR[slot] = ldrow<KPL>(urs, voff, u * rowb);
+        // wait here, inside the slow path: otherwise the compiler's wait for the row at its use
+        // (after the merge) must cover this youngest load and drains the fast path's prefetches
+        __builtin_amdgcn_s_waitcnt(0x0F70);
       }
-      double* qp = I + static_cast<size_t>(i) * k;
-      if (!(qf & kDetKeepQ)) row_load(q, qp);  // the item's previous store drained at entry j-1
+      double P[KPL];
+#pragma unroll
+      for (int c = 0; c < KPL; ++c) {
+        P[c] = PR[slot].v[c];
+        if (!(qf & kDetKeepQ)) q[c] = QR[slot].v[c];
+      }
       const double ru = regU[u], ri = regI[i];  // lambda / omega (read-only in the sweep)
       double pr[KPL];
 #pragma unroll
@@ -193,28 +235,29 @@ __global__ __launch_bounds__(64) void k_det_sweep(const DetWave* __restrict__ wa
         pn[c] = P[c] - eta * (ru * P[c] - e * q[c]);  // :407-408
         q[c] = q[c] - eta * (ri * q[c] - e * P[c]);   // :409-410 (old p)
       }
-      // entry j-1's stores are long issued: drain them and publish its ticket
-      __builtin_amdgcn_s_waitcnt(0x0F70);
-      if (lane == 0 && pend) __hip_atomic_store(pend, pend_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      double* pp = U + static_cast<size_t>(u) * k;
-#pragma unroll
-      for (int c = 0; c < KPL; ++c) {
-        const int f = lane + 64 * c;
-        if (f < k) {
-          st_sc1(pp + f, pn[c]);
-          if (!(qf & kDetDeferQ)) st_sc1(qp + f, q[c]);
-        }
-      }
+      wait_vmcnt<2 * KPL + 1>();  // entry j-1's stores have landed
+      __hip_atomic_store(pend, pend_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      strow<KPL>(urs, voff, u * rowb, pn);
+      strow<KPL>(irs, voff, (qf & kDetDeferQ) ? kOOB : i * rowb, q);
       pend = ticket + u;
       pend_val = useq + 1;
-#pragma unroll
-      for (int c = 0; c < KPL; ++c) P[c] = PN[c];
-      okP = okN;
-      tk1 = tk2;
+      // prefetch entry j+2, poll entry j+3
+      const uint32_t u2 = s + 2 < 64 ? rl(C0.u, s + 2) : rl(C1.u, s + 2 - 64);
+      const uint32_t i2 = s + 2 < 64 ? rl(C0.i, s + 2) : rl(C1.i, s + 2 - 64);
+      const uint32_t q2 = s + 2 < 64 ? rl(C0.q, s + 2) : rl(C1.q, s + 2 - 64);
+      const uint32_t u3 = s + 3 < 64 ? rl(C0.u, s + 3) : rl(C1.u, s + 3 - 64);
+      const bool live2 = j + 2 < cnt;
+      OK[slot] = live2 && __builtin_amdgcn_readfirstlane(TK) == static_cast<int32_t>(q2 & kDetUseqMask);
+      PR[slot] = ldrow<KPL>(urs, voff, OK[slot] ? u2 * rowb : kOOB);
+      QR[slot] = ldrow<KPL>(irs, voff, live2 && !(q2 & kDetKeepQ) ? i2 * rowb : kOOB);
+      TK = poll_issue(j + 3 < cnt ? ticket + u3 : dummy_ticket);
     }
+    C0 = C1;
+    C1 = det_chunk(eu, ei, eq, er, d.begin + c0 + 128 + lane);
   }
+done:
   __builtin_amdgcn_s_waitcnt(0x0F70);
-  if (lane == 0 && pend) __hip_atomic_store(pend, pend_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(pend, pend_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int KPL>
@@ -236,14 +279,14 @@ int det_sweep_capacity(int k) {
 }
 
 void launch_det_sweep(hipStream_t st, const DetWave* waves, int nw, const uint32_t* eu, const uint32_t* ei,
-                      const uint32_t* eq, const double* er, double* U, double* I, const double* regU,
-                      const double* regI, int k, double eta, int32_t* ticket, int32_t* err, hipEvent_t ev0,
-                      hipEvent_t ev1) {
+                      const uint32_t* eq, const double* er, double* U, double* I, uint64_t u_bytes, uint64_t i_bytes,
+                      const double* regU, const double* regI, int k, double eta, int32_t* ticket,
+                      int32_t* dummy_ticket, int32_t* err, hipEvent_t ev0, hipEvent_t ev1) {
   if (nw <= 0) return;
   const dim3 g(static_cast<unsigned>(nw)), b(64);
 #define MF_DET(KPL)                                                                                              \
-  hipExtLaunchKernelGGL((k_det_sweep<KPL>), g, b, 0, st, ev0, ev1, 0, waves, eu, ei, eq, er, U, I, regU, regI, k, \
-                        eta, ticket, err)
+  hipExtLaunchKernelGGL((k_det_sweep<KPL>), g, b, 0, st, ev0, ev1, 0, waves, eu, ei, eq, er, U, I, u_bytes, i_bytes, \
+                        regU, regI, k, eta, ticket, dummy_ticket, err)
   if (k <= 64) MF_DET(1);
   else if (k <= 128) MF_DET(2);
   else if (k <= 256) MF_DET(4);

@@ -699,12 +699,13 @@ struct DetOffsets {
 DetOffsets det_offsets(int64_t n, int64_t nw) {
   auto up = [](size_t x) { return (x + 255) & ~static_cast<size_t>(255); };
   DetOffsets o;
+  const size_t ne = static_cast<size_t>(n + kDetPad);  // the sweep reads whole chunks past a wave's end
   o.waves = 0;
   o.u = up(static_cast<size_t>(nw) * sizeof(DetWave));
-  o.i = o.u + up(static_cast<size_t>(n) * 4);
-  o.qf = o.i + up(static_cast<size_t>(n) * 4);
-  o.r = o.qf + up(static_cast<size_t>(n) * 4);
-  o.total = o.r + up(static_cast<size_t>(n) * 8);
+  o.i = o.u + up(ne * 4);
+  o.qf = o.i + up(ne * 4);
+  o.r = o.qf + up(ne * 4);
+  o.total = o.r + up(ne * 8);
   return o;
 }
 
@@ -794,8 +795,9 @@ void det_run(mf_ctx* ctx, int64_t count) {
       launch_det_sweep(sh.stream, reinterpret_cast<const DetWave*>(dp + o.waves), static_cast<int>(db.nw),
                        reinterpret_cast<const uint32_t*>(dp + o.u), reinterpret_cast<const uint32_t*>(dp + o.i),
                        reinterpret_cast<const uint32_t*>(dp + o.qf), reinterpret_cast<const double*>(dp + o.r),
-                       sh.uf.as<double>(), sh.itf.as<double>(), sh.regu.as<double>(), sh.regi.as<double>(), k, eta,
-                       sh.det_ticket.as<int32_t>(), sh.det_err.as<int32_t>(), tm.start(), tm.stop());
+                       sh.uf.as<double>(), sh.itf.as<double>(), sh.uf.bytes(), sh.itf.bytes(), sh.regu.as<double>(),
+                       sh.regi.as<double>(), k, eta, sh.det_ticket.as<int32_t>(),
+                       sh.det_ticket.as<int32_t>() + ctx->U.rows(), sh.det_err.as<int32_t>(), tm.start(), tm.stop());
       MF_HIP(hipGetLastError());
       ctx->stats.updates += db.n;
       ctx->stats.kernel_launches += 1;
@@ -885,6 +887,9 @@ void prepare_det_sweep(mf_ctx* ctx) {
     cap = std::min(cap, det_sweep_capacity(ctx->P.num_factors) / std::max(1, sharers));
   }
   if (cap < 1) return;
+  const uint64_t k8 = static_cast<uint64_t>(ctx->P.num_factors) * 8;
+  if (static_cast<uint64_t>(ctx->U.rows()) * k8 >= 0xFFFFF000ull || static_cast<uint64_t>(ctx->I.rows()) * k8 >= 0xFFFFF000ull)
+    return;  // the sweep addresses each f64 slab with 32-bit offsets
   int32_t waves = std::max(1, cap / 2);
   if (const char* v = std::getenv("MFHIP_DET_WAVES")) waves = std::clamp(std::atoi(v), 1, cap);
   const int32_t n = ctx->nb;
@@ -909,7 +914,7 @@ void prepare_det_sweep(mf_ctx* ctx) {
       db.pin.alloc(bytes);
       db.dev.alloc(bytes);
     }
-    s.det_ticket.alloc(static_cast<size_t>(std::max<int64_t>(ctx->U.rows(), 1)) * 4);
+    s.det_ticket.alloc(static_cast<size_t>(ctx->U.rows() + 1) * 4);  // + the sweep's scratch word
     s.det_err.alloc(16);
     MF_HIP(hipMemset(s.det_err.get(), 0, 16));
   }
