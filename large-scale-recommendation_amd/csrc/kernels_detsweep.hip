@@ -141,18 +141,19 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70 & ~0xF);
 }
 
-// Per wave, a fixed sequence of memory operations per entry j (so the compiler's vmcnt counting
-// is exact and the prefetches stay in flight across the next entry):
-//   compute j with the user row and item row prefetched at entry j-2 (kept item: registers);
-//   wait until entry j-1's stores have drained (vmcnt(2*KPL + 1): only entry j-1's prefetches
-//   and poll are younger) and publish its ticket;
-//   store j's user row (and item row unless the next entry keeps it);
-//   prefetch entry j+2's user row if its ticket, polled at entry j-1, was ready (else an
-//   out-of-range offset: entry j+2 then waits and loads itself), and its item row unless kept
-//   (issued after entry j's stores: a wave reads its own earlier stores);
-//   poll entry j+3's ticket.
-// A wave blocks on a ticket only after publishing its own pending one, so no published ticket
-// ever waits on the blocked wave.
+// Per wave, entry j runs as (one memory-operation sequence per entry, no branch on the common
+// path, so the compiler's vmcnt bookkeeping stays exact):
+//   (a) prefetch entry j+1's user row -- if its ticket, polled at entry j-1, was ready; else an
+//       out-of-range offset (zeros, entry j+1 then waits and loads itself) -- and its item row
+//       unless j+1 keeps j's (issued after every earlier store of this wave: a wave reads its own
+//       earlier stores), and poll entry j+2's ticket;
+//   (b) compute entry j from the rows prefetched at entry j-1 (the sequential dot via LDS);
+//   (c) wait only for entry j-1's stores (vmcnt(2*KPL + 1): (a)'s operations are younger) and
+//       publish entry j-1's ticket;
+//   (d) store entry j's user row and its item row unless entry j+1 keeps it.
+// So a row load overlaps one entry's compute and a store drain the next entry's.  A wave blocks
+// on a ticket only after publishing its own pending one, so no published ticket ever waits on a
+// blocked wave.
 template <int KPL>
 __global__ __launch_bounds__(64) void k_det_sweep(const DetWave* __restrict__ waves, const uint32_t* __restrict__ eu,
                                                   const uint32_t* __restrict__ ei, const uint32_t* __restrict__ eq,
@@ -173,35 +174,47 @@ __global__ __launch_bounds__(64) void k_det_sweep(const DetWave* __restrict__ wa
 
   DetChunk C0 = det_chunk(eu, ei, eq, er, d.begin + lane);
   DetChunk C1 = det_chunk(eu, ei, eq, er, d.begin + 64 + lane);
-  // prologue: entries 0 and 1 read synchronously, entry 2's ticket polled ahead
-  DRow<KPL> PR[2], QR[2];
-  int32_t OK[2];
-#pragma unroll
-  for (int y = 0; y < 2; ++y) {
-    const bool live = y < cnt;
-    const uint32_t u = rl(C0.u, y), i = rl(C0.i, y), qf = rl(C0.q, y);
-    OK[y] = live && poll(ticket + u) == static_cast<int32_t>(qf & kDetUseqMask);
-    PR[y] = ldrow<KPL>(urs, voff, OK[y] ? u * rowb : kOOB);
-    QR[y] = ldrow<KPL>(irs, voff, live && !(qf & kDetKeepQ) ? i * rowb : kOOB);
+  // field of entry (chunk-relative) s + dj, dj in {0, 1, 2}
+  auto fld = [&](uint32_t a0, uint32_t a1, int s, int dj) { return s + dj < 64 ? rl(a0, s + dj) : rl(a1, s + dj - 64); };
+
+  // entry 0 read synchronously; entry 1's ticket polled ahead
+  DRow<KPL> P, Q;
+  int32_t okP;
+  {
+    const uint32_t u0 = rl(C0.u, 0), i0 = rl(C0.i, 0), q0 = rl(C0.q, 0);
+    okP = poll(ticket + u0) == static_cast<int32_t>(q0 & kDetUseqMask);
+    P = ldrow<KPL>(urs, voff, okP ? u0 * rowb : kOOB);
+    Q = ldrow<KPL>(irs, voff, i0 * rowb);
   }
-  int32_t TK = poll_issue(cnt > 2 ? ticket + rl(C0.u, 2) : dummy_ticket);
+  int32_t tk1 = poll_issue(cnt > 1 ? ticket + rl(C0.u, 1) : dummy_ticket);
+  __builtin_amdgcn_s_waitcnt(0x0F70);
   int32_t* pend = dummy_ticket;  // entry j-1's ticket word and value, published after its drain
   int32_t pend_val = 0;
   double q[KPL];
 #pragma unroll
   for (int c = 0; c < KPL; ++c) q[c] = 0.0;
 
-  for (int64_t c0 = 0;; c0 += 64) {
-#pragma unroll
-    for (int s = 0; s < 64; ++s) {
+  for (int64_t c0 = 0; c0 < cnt; c0 += 64) {
+    if (c0 > 0) {
+      C0 = C1;
+      C1 = det_chunk(eu, ei, eq, er, d.begin + c0 + 64 + lane);
+    }
+    const int n = static_cast<int>(min<int64_t>(64, cnt - c0));
+    for (int s = 0; s < n; ++s) {
       const int64_t j = c0 + s;
-      if (j >= cnt) goto done;
-      const int slot = s & 1;
       const uint32_t u = rl(C0.u, s), i = rl(C0.i, s), qf = rl(C0.q, s);
       const double r = rld(C0.r, s);
       const int32_t useq = static_cast<int32_t>(qf & kDetUseqMask);
-      if (!OK[slot]) {  // the ticket was not ready at prefetch time: publish ours, wait, load
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      // (a) prefetch entry j+1, poll entry j+2
+      const bool live1 = j + 1 < cnt;
+      const uint32_t u1 = fld(C0.u, C1.u, s, 1), i1 = fld(C0.i, C1.i, s, 1), q1 = fld(C0.q, C1.q, s, 1);
+      const int32_t okN = live1 && __builtin_amdgcn_readfirstlane(tk1) == static_cast<int32_t>(q1 & kDetUseqMask);
+      const DRow<KPL> PN = ldrow<KPL>(urs, voff, okN ? u1 * rowb : kOOB);
+      const DRow<KPL> QN = ldrow<KPL>(irs, voff, live1 && !(q1 & kDetKeepQ) ? i1 * rowb : kOOB);
+      const int32_t tk2 = poll_issue(j + 2 < cnt ? ticket + fld(C0.u, C1.u, s, 2) : dummy_ticket);
+      // entry j's user row: prefetched, or (rarely) wait for its ticket now
+      if (!okP) {
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): entry j-1's stores landed
         __hip_atomic_store(pend, pend_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         pend = dummy_ticket;
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // bounded wait (100 MHz clock)
@@ -213,49 +226,38 @@ __global__ __launch_bounds__(64) void k_det_sweep(const DetWave* __restrict__ wa
           }
           __builtin_amdgcn_s_sleep(1);
         }
-        PR[slot] = ldrow<KPL>(urs, voff, u * rowb);
-        // wait here, inside the slow path: otherwise the compiler's wait for the row at its use
-        // (after the merge) must cover this youngest load and drains the fast path's prefetches
-        __builtin_amdgcn_s_waitcnt(0x0F70);
+        P = ldrow<KPL>(urs, voff, u * rowb);
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // waited here, so the fast path's waits stay counted
       }
-      double P[KPL];
+      // (b) compute
+      if (!(qf & kDetKeepQ)) {
 #pragma unroll
-      for (int c = 0; c < KPL; ++c) {
-        P[c] = PR[slot].v[c];
-        if (!(qf & kDetKeepQ)) q[c] = QR[slot].v[c];
+        for (int c = 0; c < KPL; ++c) q[c] = Q.v[c];
       }
       const double ru = regU[u], ri = regI[i];  // lambda / omega (read-only in the sweep)
-      double pr[KPL];
+      double pr[KPL], pn[KPL];
 #pragma unroll
-      for (int c = 0; c < KPL; ++c) pr[c] = P[c] * q[c];
+      for (int c = 0; c < KPL; ++c) pr[c] = P.v[c] * q[c];
       const double e = r - seq_dot<KPL>(pr, k, lds, lane);  // :405
-      double pn[KPL];
 #pragma unroll
       for (int c = 0; c < KPL; ++c) {
-        pn[c] = P[c] - eta * (ru * P[c] - e * q[c]);  // :407-408
-        q[c] = q[c] - eta * (ri * q[c] - e * P[c]);   // :409-410 (old p)
+        pn[c] = P.v[c] - eta * (ru * P.v[c] - e * q[c]);  // :407-408
+        q[c] = q[c] - eta * (ri * q[c] - e * P.v[c]);     // :409-410 (old p)
       }
-      wait_vmcnt<2 * KPL + 1>();  // entry j-1's stores have landed
+      // (c) entry j-1's stores have landed: publish its ticket
+      wait_vmcnt<2 * KPL + 1>();
       __hip_atomic_store(pend, pend_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // (d) stores
       strow<KPL>(urs, voff, u * rowb, pn);
       strow<KPL>(irs, voff, (qf & kDetDeferQ) ? kOOB : i * rowb, q);
       pend = ticket + u;
       pend_val = useq + 1;
-      // prefetch entry j+2, poll entry j+3
-      const uint32_t u2 = s + 2 < 64 ? rl(C0.u, s + 2) : rl(C1.u, s + 2 - 64);
-      const uint32_t i2 = s + 2 < 64 ? rl(C0.i, s + 2) : rl(C1.i, s + 2 - 64);
-      const uint32_t q2 = s + 2 < 64 ? rl(C0.q, s + 2) : rl(C1.q, s + 2 - 64);
-      const uint32_t u3 = s + 3 < 64 ? rl(C0.u, s + 3) : rl(C1.u, s + 3 - 64);
-      const bool live2 = j + 2 < cnt;
-      OK[slot] = live2 && __builtin_amdgcn_readfirstlane(TK) == static_cast<int32_t>(q2 & kDetUseqMask);
-      PR[slot] = ldrow<KPL>(urs, voff, OK[slot] ? u2 * rowb : kOOB);
-      QR[slot] = ldrow<KPL>(irs, voff, live2 && !(q2 & kDetKeepQ) ? i2 * rowb : kOOB);
-      TK = poll_issue(j + 3 < cnt ? ticket + u3 : dummy_ticket);
+      P = PN;
+      Q = QN;
+      okP = okN;
+      tk1 = tk2;
     }
-    C0 = C1;
-    C1 = det_chunk(eu, ei, eq, er, d.begin + c0 + 128 + lane);
   }
-done:
   __builtin_amdgcn_s_waitcnt(0x0F70);
   __hip_atomic_store(pend, pend_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
