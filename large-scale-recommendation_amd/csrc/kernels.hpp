@@ -78,7 +78,8 @@ void launch_sweep_pair_sys(hipStream_t st, const SysWave* sw, const WaveDesc* sy
 // set when a wave gave up waiting.  ev0 / ev1 (may be null): dispatch-recorded timing events.
 int det_sweep_capacity(int k);
 // Entry arrays are read in 64-entry chunks up to 192 entries past a wave's end (kDetPad slack).
-// u_bytes / i_bytes: slab sizes (< 4 GiB, 32-bit row offsets); dummy_ticket: a scratch word.
+// u_bytes / i_bytes: slab sizes (< 4 GiB, 32-bit row offsets); dummy_ticket: 16 scratch words
+// per wave (nw * 16 int32).
 constexpr int64_t kDetPad = 256;
 void launch_det_sweep(hipStream_t st, const DetWave* waves, int nw, const uint32_t* eu, const uint32_t* ei,
                       const uint32_t* eq, const double* er, double* U, double* I, uint64_t u_bytes, uint64_t i_bytes,

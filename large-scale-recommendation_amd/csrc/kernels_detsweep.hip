@@ -98,6 +98,11 @@ __device__ __forceinline__ int32_t poll_issue(const int32_t* t) {
   return __hip_atomic_load(t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Lane 0 stores the ticket (one word, one request; the wave's earlier stores have drained).
+__device__ __forceinline__ void publish(int32_t* t, int32_t v, int lane) {
+  if (lane == 0) __hip_atomic_store(t, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t raw_rsrc(const void* base, uint64_t bytes) {
   const uint32_t n = bytes > 0xFFFFF000ull ? 0xFFFFF000u : static_cast<uint32_t>(bytes);
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, n, 0x00020000);
@@ -166,6 +171,7 @@ __global__ __launch_bounds__(64) void k_det_sweep(const DetWave* __restrict__ wa
   const DetWave d = waves[blockIdx.x];
   const int64_t cnt = d.count;
   if (cnt == 0) return;
+  dummy_ticket += 16 * static_cast<int64_t>(blockIdx.x);  // this wave's own scratch line
   const __amdgpu_buffer_rsrc_t urs = raw_rsrc(U, u_bytes), irs = raw_rsrc(I, i_bytes);
   uint32_t voff[KPL];
 #pragma unroll
@@ -215,13 +221,13 @@ __global__ __launch_bounds__(64) void k_det_sweep(const DetWave* __restrict__ wa
       // entry j's user row: prefetched, or (rarely) wait for its ticket now
       if (!okP) {
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): entry j-1's stores landed
-        __hip_atomic_store(pend, pend_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        publish(pend, pend_val, lane);
         pend = dummy_ticket;
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // bounded wait (100 MHz clock)
         while (poll(ticket + u) != useq) {
           if (poll(err) != 0) return;
           if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {  // ~1 s: a producer never ran
-            __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return;
           }
           __builtin_amdgcn_s_sleep(1);
@@ -246,7 +252,7 @@ __global__ __launch_bounds__(64) void k_det_sweep(const DetWave* __restrict__ wa
       }
       // (c) entry j-1's stores have landed: publish its ticket
       wait_vmcnt<2 * KPL + 1>();
-      __hip_atomic_store(pend, pend_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      publish(pend, pend_val, lane);
       // (d) stores
       strow<KPL>(urs, voff, u * rowb, pn);
       strow<KPL>(irs, voff, (qf & kDetDeferQ) ? kOOB : i * rowb, q);
@@ -259,7 +265,7 @@ __global__ __launch_bounds__(64) void k_det_sweep(const DetWave* __restrict__ wa
     }
   }
   __builtin_amdgcn_s_waitcnt(0x0F70);
-  __hip_atomic_store(pend, pend_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  publish(pend, pend_val, lane);
 }
 
 template <int KPL>

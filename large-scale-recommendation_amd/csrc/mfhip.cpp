@@ -89,7 +89,7 @@ struct Shard {
   // deterministic persistent sweep (kernels_detsweep.hip)
   DetSweepLayout det_layout;
   DetBuf det_buf[2];
-  DevBuf det_ticket, det_err;
+  DevBuf det_ticket, det_err, det_scratch;
   int64_t det_n_max = 0, det_nw_max = 0;
   // evaluation scratch
   DevBuf ev_u, ev_i, ev_r, ev_mult, ev_out, ev_part;
@@ -797,7 +797,7 @@ void det_run(mf_ctx* ctx, int64_t count) {
                        reinterpret_cast<const uint32_t*>(dp + o.qf), reinterpret_cast<const double*>(dp + o.r),
                        sh.uf.as<double>(), sh.itf.as<double>(), sh.uf.bytes(), sh.itf.bytes(), sh.regu.as<double>(),
                        sh.regi.as<double>(), k, eta, sh.det_ticket.as<int32_t>(),
-                       sh.det_ticket.as<int32_t>() + ctx->U.rows(), sh.det_err.as<int32_t>(), tm.start(), tm.stop());
+                       sh.det_scratch.as<int32_t>(), sh.det_err.as<int32_t>(), tm.start(), tm.stop());
       MF_HIP(hipGetLastError());
       ctx->stats.updates += db.n;
       ctx->stats.kernel_launches += 1;
@@ -914,7 +914,8 @@ void prepare_det_sweep(mf_ctx* ctx) {
       db.pin.alloc(bytes);
       db.dev.alloc(bytes);
     }
-    s.det_ticket.alloc(static_cast<size_t>(ctx->U.rows() + 1) * 4);  // + the sweep's scratch word
+    s.det_ticket.alloc(static_cast<size_t>(std::max<int64_t>(ctx->U.rows(), 1)) * 4);
+    s.det_scratch.alloc(static_cast<size_t>(s.det_nw_max) * 64);  // one scratch line per wave
     s.det_err.alloc(16);
     MF_HIP(hipMemset(s.det_err.get(), 0, 16));
   }
