@@ -40,6 +40,7 @@ __device__ __forceinline__ double rld(double v, int l) {
   return __longlong_as_double(static_cast<long long>((static_cast<unsigned long long>(hi) << 32) | lo));
 }
 
+__device__ __forceinline__ double uniform(double v) { return rld(v, 0); }
 __device__ __forceinline__ double ld_sc1(const double* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -151,9 +152,9 @@ __device__ __forceinline__ void wait_vmcnt() {
 //   (a) prefetch entry j+1's user row -- if its ticket, polled at entry j-1, was ready; else an
 //       out-of-range offset (zeros, entry j+1 then waits and loads itself) -- and its item row
 //       unless j+1 keeps j's (issued after every earlier store of this wave: a wave reads its own
-//       earlier stores), and poll entry j+2's ticket;
+//       earlier stores), load its two lambda / omega values, and poll entry j+2's ticket;
 //   (b) compute entry j from the rows prefetched at entry j-1 (the sequential dot via LDS);
-//   (c) wait only for entry j-1's stores (vmcnt(2*KPL + 1): (a)'s operations are younger) and
+//   (c) wait only for entry j-1's stores (vmcnt(2*KPL + 3): (a)'s operations are younger) and
 //       publish entry j-1's ticket;
 //   (d) store entry j's user row and its item row unless entry j+1 keeps it.
 // So a row load overlaps one entry's compute and a store drain the next entry's.  A wave blocks
@@ -186,11 +187,14 @@ __global__ __launch_bounds__(64) void k_det_sweep(const DetWave* __restrict__ wa
   // entry 0 read synchronously; entry 1's ticket polled ahead
   DRow<KPL> P, Q;
   int32_t okP;
+  double RU, RI;
   {
     const uint32_t u0 = rl(C0.u, 0), i0 = rl(C0.i, 0), q0 = rl(C0.q, 0);
     okP = poll(ticket + u0) == static_cast<int32_t>(q0 & kDetUseqMask);
     P = ldrow<KPL>(urs, voff, okP ? u0 * rowb : kOOB);
     Q = ldrow<KPL>(irs, voff, i0 * rowb);
+    RU = ld_sc1(regU + u0);
+    RI = ld_sc1(regI + i0);
   }
   int32_t tk1 = poll_issue(cnt > 1 ? ticket + rl(C0.u, 1) : dummy_ticket);
   __builtin_amdgcn_s_waitcnt(0x0F70);
@@ -218,6 +222,9 @@ __global__ __launch_bounds__(64) void k_det_sweep(const DetWave* __restrict__ wa
       const DRow<KPL> PN = ldrow<KPL>(urs, voff, okN ? u1 * rowb : kOOB);
       const DRow<KPL> QN = ldrow<KPL>(irs, voff, live1 && !(q1 & kDetKeepQ) ? i1 * rowb : kOOB);
       const int32_t tk2 = poll_issue(j + 2 < cnt ? ticket + fld(C0.u, C1.u, s, 2) : dummy_ticket);
+      // entry j+1's lambda / omega as vector loads: a scalar load here would be waited for at the
+      // dot's first LDS wait (lgkmcnt also counts SMEM)
+      const double RUN = ld_sc1(regU + (live1 ? u1 : 0u)), RIN = ld_sc1(regI + (live1 ? i1 : 0u));
       // entry j's user row: prefetched, or (rarely) wait for its ticket now
       if (!okP) {
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): entry j-1's stores landed
@@ -240,7 +247,7 @@ __global__ __launch_bounds__(64) void k_det_sweep(const DetWave* __restrict__ wa
 #pragma unroll
         for (int c = 0; c < KPL; ++c) q[c] = Q.v[c];
       }
-      const double ru = regU[u], ri = regI[i];  // lambda / omega (read-only in the sweep)
+      const double ru = uniform(RU), ri = uniform(RI);  // lambda / omega, prefetched with the rows
       double pr[KPL], pn[KPL];
 #pragma unroll
       for (int c = 0; c < KPL; ++c) pr[c] = P.v[c] * q[c];
@@ -251,7 +258,7 @@ __global__ __launch_bounds__(64) void k_det_sweep(const DetWave* __restrict__ wa
         q[c] = q[c] - eta * (ri * q[c] - e * P.v[c]);     // :409-410 (old p)
       }
       // (c) entry j-1's stores have landed: publish its ticket
-      wait_vmcnt<2 * KPL + 1>();
+      wait_vmcnt<2 * KPL + 3>();
       publish(pend, pend_val, lane);
       // (d) stores
       strow<KPL>(urs, voff, u * rowb, pn);
@@ -260,6 +267,8 @@ __global__ __launch_bounds__(64) void k_det_sweep(const DetWave* __restrict__ wa
       pend_val = useq + 1;
       P = PN;
       Q = QN;
+      RU = RUN;
+      RI = RIN;
       okP = okN;
       tk1 = tk2;
     }

@@ -56,6 +56,7 @@ struct DetBuf {
   PinnedBuf pin;
   DevBuf dev;
   hipEvent_t copied = nullptr;  // the H2D from `pin` finished (pin may be rewritten)
+  hipEvent_t swept = nullptr;   // the sweep that read `dev` finished (dev may be rewritten)
   bool pending = false;         // `copied` was recorded and not yet waited for
   int64_t n = 0, nw = 0, keeps = 0, defers = 0;
 };
@@ -64,6 +65,7 @@ struct Shard {
   int device = 0;
   int index = 0;  // global shard index (== rank in rank mode)
   hipStream_t stream = nullptr;
+  hipStream_t copy_stream = nullptr;  // host-to-device staging beside the sweeps (deterministic mode)
   hipEvent_t done = nullptr;  // ring hand-off ordering between in-process shards
   DevBuf uf, itf, regu, regi;
   int64_t cap_u = 0, cap_i = 0;
@@ -185,18 +187,27 @@ void init_shard(Shard& s, int device, int index) {
   s.index = index;
   DeviceGuard g(device);
   MF_HIP(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+  MF_HIP(hipStreamCreateWithFlags(&s.copy_stream, hipStreamNonBlocking));
   MF_HIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+  for (auto& b : s.det_buf) {
+    MF_HIP(hipEventCreateWithFlags(&b.copied, hipEventDisableTiming));
+    MF_HIP(hipEventCreateWithFlags(&b.swept, hipEventDisableTiming));
+  }
 }
 
 void destroy_shard(Shard& s) {
   if (!s.stream) return;
   (void)hipSetDevice(s.device);
   (void)hipStreamSynchronize(s.stream);
+  (void)hipStreamSynchronize(s.copy_stream);
   for (auto e : s.ev) (void)hipEventDestroy(e);
   s.ev.clear();
-  for (auto& b : s.det_buf)
+  for (auto& b : s.det_buf) {
     if (b.copied) (void)hipEventDestroy(b.copied);
+    if (b.swept) (void)hipEventDestroy(b.swept);
+  }
   (void)hipEventDestroy(s.done);
+  (void)hipStreamDestroy(s.copy_stream);
   (void)hipStreamDestroy(s.stream);
   s.stream = nullptr;
 }
@@ -785,11 +796,14 @@ void det_run(mf_ctx* ctx, int64_t count) {
                                                    {o.i, static_cast<size_t>(db.n) * 4},
                                                    {o.qf, static_cast<size_t>(db.n) * 4},
                                                    {o.r, static_cast<size_t>(db.n) * 8}};
+      // staging copy on the copy stream, after the sweep that last read this buffer (s-2), so it
+      // overlaps the sweep of s-1 still running on the compute stream
+      MF_HIP(hipStreamWaitEvent(sh.copy_stream, db.swept, 0));
       for (const auto& rg : regions)
-        MF_HIP(hipMemcpyAsync(dp + rg.first, hp + rg.first, rg.second, hipMemcpyHostToDevice, sh.stream));
-      if (!db.copied) MF_HIP(hipEventCreateWithFlags(&db.copied, hipEventDisableTiming));
-      MF_HIP(hipEventRecord(db.copied, sh.stream));
+        MF_HIP(hipMemcpyAsync(dp + rg.first, hp + rg.first, rg.second, hipMemcpyHostToDevice, sh.copy_stream));
+      MF_HIP(hipEventRecord(db.copied, sh.copy_stream));
       db.pending = true;
+      MF_HIP(hipStreamWaitEvent(sh.stream, db.copied, 0));
       MF_HIP(hipMemsetAsync(sh.det_ticket.get(), 0, sh.det_ticket.bytes(), sh.stream));
       LaunchTimer tm(sh, ctx->profiling, true);
       launch_det_sweep(sh.stream, reinterpret_cast<const DetWave*>(dp + o.waves), static_cast<int>(db.nw),
@@ -799,6 +813,7 @@ void det_run(mf_ctx* ctx, int64_t count) {
                        sh.regi.as<double>(), k, eta, sh.det_ticket.as<int32_t>(),
                        sh.det_scratch.as<int32_t>(), sh.det_err.as<int32_t>(), tm.start(), tm.stop());
       MF_HIP(hipGetLastError());
+      MF_HIP(hipEventRecord(db.swept, sh.stream));
       ctx->stats.updates += db.n;
       ctx->stats.kernel_launches += 1;
       // rows: user in + out per update, item in / out where not kept in registers; per update
