@@ -51,7 +51,10 @@ struct DeviceGuard {
   } while (0)
 
 // Deterministic persistent sweep: one superstep's entries, staged in pinned memory by a host
-// thread while the previous superstep runs, then copied to the device (fixed SoA offsets).
+// thread while earlier supersteps run, then copied to the device (fixed SoA offsets).  A ring of
+// kDetSlots buffers: the host builds supersteps s+1 and s+2 (two builders, each one thread per
+// rating block) while the device runs s.
+constexpr int kDetSlots = 3;
 struct DetBuf {
   PinnedBuf pin;
   DevBuf dev;
@@ -90,7 +93,7 @@ struct Shard {
   std::vector<double> sm_bytes;         // per superstep index (s-1) mod n: bytes the sweep requests
   // deterministic persistent sweep (kernels_detsweep.hip)
   DetSweepLayout det_layout;
-  DetBuf det_buf[2];
+  DetBuf det_buf[kDetSlots];
   DevBuf det_ticket, det_err, det_scratch;
   int64_t det_n_max = 0, det_nw_max = 0;
   // evaluation scratch
@@ -764,23 +767,29 @@ void det_build(mf_ctx* ctx, int64_t superstep, int slot) {
   }
 }
 
-// Deterministic supersteps with the persistent sweep: the host builds superstep s+1's entries
+// Deterministic supersteps with the persistent sweep: the host builds supersteps s+1 and s+2
 // while the device runs superstep s.
 void det_run(mf_ctx* ctx, int64_t count) {
   const int k = ctx->P.num_factors;
   const int64_t s0 = ctx->superstep_done + 1;
-  for (auto& sh : ctx->shards)  // a previous call's last copies may still read the staging buffers
-    for (auto& db : sh.det_buf)
-      if (db.pending) {
-        DeviceGuard g(sh.device);
-        MF_HIP(hipEventSynchronize(db.copied));
-        db.pending = false;
-      }
-  std::future<void> next = std::async(std::launch::async, det_build, ctx, s0, 0);
+  auto reclaim = [&](int slot) {  // the staging copy out of this slot's pinned buffer has finished
+    for (auto& sh : ctx->shards) {
+      DetBuf& db = sh.det_buf[slot];
+      if (!db.pending) continue;
+      DeviceGuard g(sh.device);
+      MF_HIP(hipEventSynchronize(db.copied));
+      db.pending = false;
+    }
+  };
+  for (int slot = 0; slot < kDetSlots; ++slot) reclaim(slot);  // a previous call's last copies
+  std::future<void> builds[kDetSlots];
+  constexpr int kAhead = kDetSlots - 1;  // supersteps built ahead of the one launched
+  for (int64_t x = 0; x < std::min<int64_t>(count, kAhead); ++x)
+    builds[x % kDetSlots] = std::async(std::launch::async, det_build, ctx, s0 + x, static_cast<int>(x % kDetSlots));
   for (int64_t x = 0; x < count; ++x) {
     const int64_t s = s0 + x;
-    const int slot = static_cast<int>(x & 1);
-    next.get();
+    const int slot = static_cast<int>(x % kDetSlots);
+    builds[slot].get();
     const int32_t iteration = static_cast<int32_t>(s / ctx->nb);  // :476
     const double eta = learning_rate(ctx->P.lr_method, ctx->P.learning_rate, iteration + 1, ctx->P.lambda,
                                      ctx->P.lr_arg);  // :383-386
@@ -796,8 +805,8 @@ void det_run(mf_ctx* ctx, int64_t count) {
                                                    {o.i, static_cast<size_t>(db.n) * 4},
                                                    {o.qf, static_cast<size_t>(db.n) * 4},
                                                    {o.r, static_cast<size_t>(db.n) * 8}};
-      // staging copy on the copy stream, after the sweep that last read this buffer (s-2), so it
-      // overlaps the sweep of s-1 still running on the compute stream
+      // staging copy on the copy stream, after the sweep that last read this buffer (s-3), so it
+      // overlaps the sweeps still running on the compute stream
       MF_HIP(hipStreamWaitEvent(sh.copy_stream, db.swept, 0));
       for (const auto& rg : regions)
         MF_HIP(hipMemcpyAsync(dp + rg.first, hp + rg.first, rg.second, hipMemcpyHostToDevice, sh.copy_stream));
@@ -823,17 +832,10 @@ void det_run(mf_ctx* ctx, int64_t count) {
     ring_shift(ctx, s);
     ctx->superstep_done = s;
     ctx->stats.supersteps++;
-    if (x + 1 < count) {
-      const int other = slot ^ 1;  // superstep s-1's staging buffer: its copy must be done
-      for (auto& sh : ctx->shards) {
-        DetBuf& db = sh.det_buf[other];
-        if (db.pending) {
-          DeviceGuard g(sh.device);
-          MF_HIP(hipEventSynchronize(db.copied));
-          db.pending = false;
-        }
-      }
-      next = std::async(std::launch::async, det_build, ctx, s + 1, other);
+    if (x + kAhead < count) {  // superstep s+kAhead goes where s-1 was staged: its copy must be done
+      const int other = static_cast<int>((x + kAhead) % kDetSlots);
+      reclaim(other);
+      builds[other] = std::async(std::launch::async, det_build, ctx, s + kAhead, other);
     }
   }
   ctx->stats.algorithmic_bytes = static_cast<double>(ctx->stats.updates) * bytes_per_update(ctx);
