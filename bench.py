@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--no-profile", action="store_true", help="skip the profiled replay (roofline = null)")
     ap.add_argument("--online-batches", type=int, default=5,
                     help="ONLINE leg (BASELINE config 5): 1M-rating micro-batches applied to the fitted model (0 = off)")
+    ap.add_argument("--det-epochs", type=int, default=2,
+                    help="deterministic-f64 leg (the reference's exact order) on the same data: timed epochs (0 = off)")
     ap.add_argument("--item-split", type=int, default=0,
                     help="fast mode: hot-item replicas, max ratings per item chain per rating block (0 = off)")
     return ap.parse_args()
@@ -153,6 +155,48 @@ def rmse_reference(a, arrays):
         print("[bench] rmse_ref fixture does not match this data (sha256); not used", file=sys.stderr)
         return None
     return rec
+
+
+def det_leg(a, k, nb, train, test, ref):
+    """The deterministic f64 mode on the same data: DSGDforMF.scala:378-418's exact update order
+    (JVM shuffle, F2J ddot fold, no FMA), one persistent sweep per superstep.  Timed epochs after
+    one warmup epoch, then a restarted 10-epoch fit whose held-out RMSE must equal the f64
+    oracle's on this data (tests/golden/rmse_ref.json) to the last bit of its printout."""
+    import mfhip
+    from mfhip import _lib as L
+    p = L.default_params()
+    p.num_factors, p.num_blocks, p.seed, p.has_seed = k, nb, 0, 1
+    p.iterations = 10
+    p.mode = L.MODE_DETERMINISTIC_F64
+    with mfhip.Context(p) as ctx:
+        t0 = time.time()
+        ctx.prepare(*train)
+        ctx.sync()
+        t_prep = time.time() - t0
+        ctx.run(nb)
+        ctx.sync()
+        ctx.reset_stats()
+        t0 = time.perf_counter()
+        ctx.run(a.det_epochs * nb)
+        ctx.sync()
+        el = time.perf_counter() - t0
+        st = ctx.stats()
+        ctx.reset_stats()
+        ctx.set_profiling(True)
+        ctx.run(nb)
+        ctx.sync()
+        ctx.set_profiling(False)
+        sp = ctx.stats()
+        ctx.restart()
+        ctx.run(10 * nb)
+        rmse, _ = ctx.rmse(*test)
+    return {"metric": "SGD rating updates/sec, deterministic f64 (the reference's exact update order)",
+            "value": round(st["updates"] / el, 1), "unit": "updates/s", "dtype": "f64", "epochs": a.det_epochs,
+            "ms_per_step": round(el * 1e3 / a.det_epochs, 3), "kernel": "k_det_sweep",
+            "avg_launch_us": round(sp["kernel_ms"] * 1e3 / max(sp["kernel_launches"], 1), 2),
+            "launches_per_epoch": sp["kernel_launches"], "prepare_s": round(t_prep, 2),
+            "rmse": round(rmse, 9), "rmse_ref": round(ref["oracle_rmse"], 9) if ref else None,
+            "rmse_equal_to_ref": (abs(rmse - ref["oracle_rmse"]) <= 1e-12 * ref["oracle_rmse"]) if ref else None}
 
 
 def online_leg(ctx, synth, nu, ni, a, batch=1_000_000):
@@ -287,6 +331,10 @@ def main():
     online = None
     if D.world == 1 and a.online_batches > 0:
         online = online_leg(ctx, synth, nu, ni, a)
+    det = None
+    if D.world == 1 and a.mode == "fast" and a.det_epochs > 0:
+        ctx.close()  # its HBM is not needed any more
+        det = det_leg(a, k, nb, (tu, ti, tr), (eu, ei, er), ref)
 
     cpu = None
     if D.rank == 0 and D.world == 1 and not a.no_cpu_baseline:
@@ -309,7 +357,7 @@ def main():
             "rmse_rel": round((rmse - ref["oracle_rmse"]) / ref["oracle_rmse"], 5) if ref else None,
             "rmse_ref_source": "tests/golden/rmse_ref.json (tools/rmse_parity.py, oracle f64, same data sha256)"
                                if ref else None,
-            "roofline": roof, "cpu_baseline": cpu, "online": online,
+            "roofline": roof, "cpu_baseline": cpu, "online": online, "deterministic": det,
             "setup_s": {"generate": round(t_gen, 2), "prepare": round(t_prep, 2), "rmse_eval": round(t_eval, 3)},
         }
         print(json.dumps(out), flush=True)
