@@ -355,19 +355,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
 // poll that exceeds ~1 s sets err[0] and the wave gives up (the host then fails loudly).
 template <int KPL, int D>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_sweep_pair_sys(
-    const SysWave* __restrict__ sw, const WaveDesc* __restrict__ sys, int nw, const u4v* __restrict__ recs,
+    const SysWave* __restrict__ sw, const WaveDesc* __restrict__ sys, int nw, int lbase, const u4v* __restrict__ recs,
     float* __restrict__ U, float* __restrict__ I, uint64_t u_bytes, uint64_t i_bytes, float eta,
     int32_t* __restrict__ prog, uint32_t base, int32_t* __restrict__ err, uint64_t* __restrict__ trace) {
   const int lane = threadIdx.x;
   // blocks b and b+8 share an XCD: give each XCD a contiguous range of waves, so most hand-offs
   // (g+1 -> g) stay inside one L2 (speed only; correctness does not depend on it).  XCD x holds
-  // nw/8 blocks, plus one when x < nw%8: a bijection for any nw.
+  // nw/8 blocks, plus one when x < nw%8: a bijection for any nw.  sw = this launch's waves, the
+  // superstep's waves from lbase on (progress words and SysWave::nbr count from the superstep's
+  // first wave).
   const int b = static_cast<int>(blockIdx.x);
   const int x = b % 8, per = nw / 8, extra = nw % 8;
   const int L = x * per + min(x, extra) + b / 8;
   const SysWave w = sw[L];
   const WaveDesc* my = sys + w.cell0;
-  int32_t* my_prog = prog + static_cast<int64_t>(L) * kProgStride;
+  int32_t* my_prog = prog + static_cast<int64_t>(lbase + L) * kProgStride;
   int32_t* nb_prog = prog + static_cast<int64_t>(w.nbr) * kProgStride;
   const __amdgpu_buffer_rsrc_t urs = raw_rsrc(U, u_bytes), irs = raw_rsrc(I, i_bytes);
   for (int t = 0; t < w.G; ++t) {
@@ -409,11 +411,12 @@ void dispatch(hipStream_t st, const WaveDesc* waves, int nwaves, const PairRec* 
 }
 
 template <int KPL>
-void dispatch_sys(hipStream_t st, const SysWave* sw, const WaveDesc* sys, int nw, const PairRec* recs, float* U,
-                  float* I, uint64_t ub, uint64_t ib, float eta, int32_t* prog, uint32_t base, int32_t* err,
+void dispatch_sys(hipStream_t st, const SysWave* sw, const WaveDesc* sys, int nw, int lbase, const PairRec* recs,
+                  float* U, float* I, uint64_t ub, uint64_t ib, float eta, int32_t* prog, uint32_t base, int32_t* err,
                   uint64_t* trace, hipEvent_t ev0, hipEvent_t ev1) {
   hipExtLaunchKernelGGL((k_sweep_pair_sys<KPL, kPairRing>), dim3(static_cast<unsigned>(nw)), dim3(64), 0, st, ev0, ev1,
-                        0, sw, sys, nw, reinterpret_cast<const u4v*>(recs), U, I, ub, ib, eta, prog, base, err, trace);
+                        0, sw, sys, nw, lbase, reinterpret_cast<const u4v*>(recs), U, I, ub, ib, eta, prog, base, err,
+                        trace);
 }
 
 template <int KPL>
@@ -439,16 +442,18 @@ int sweep_pair_sys_capacity(int k) {
   }
 }
 
-void launch_sweep_pair_sys(hipStream_t st, const SysWave* sw, const WaveDesc* sys, int nw, const PairRec* recs,
-                           float* U, float* I, uint64_t u_bytes, uint64_t i_bytes, int k, float eta, int32_t* prog,
-                           uint32_t base, int32_t* err, uint64_t* trace, hipEvent_t ev0, hipEvent_t ev1) {
+void launch_sweep_pair_sys(hipStream_t st, const SysWave* sw, const WaveDesc* sys, int nw, int lbase,
+                           const PairRec* recs, float* U, float* I, uint64_t u_bytes, uint64_t i_bytes, int k, float eta,
+                           int32_t* prog, uint32_t base, int32_t* err, uint64_t* trace, hipEvent_t ev0, hipEvent_t ev1) {
   if (nw <= 0) return;
+#define MF_SYS(KPL) dispatch_sys<KPL>(st, sw, sys, nw, lbase, recs, U, I, u_bytes, i_bytes, eta, prog, base, err, trace, ev0, ev1)
   switch (k) {
-    case 64: dispatch_sys<1>(st, sw, sys, nw, recs, U, I, u_bytes, i_bytes, eta, prog, base, err, trace, ev0, ev1); break;
-    case 128: dispatch_sys<2>(st, sw, sys, nw, recs, U, I, u_bytes, i_bytes, eta, prog, base, err, trace, ev0, ev1); break;
-    case 256: dispatch_sys<4>(st, sw, sys, nw, recs, U, I, u_bytes, i_bytes, eta, prog, base, err, trace, ev0, ev1); break;
+    case 64: MF_SYS(1); break;
+    case 128: MF_SYS(2); break;
+    case 256: MF_SYS(4); break;
     default: break;
   }
+#undef MF_SYS
 }
 
 void launch_sweep_pair(hipStream_t st, const WaveDesc* waves, int nwaves, const PairRec* recs, float* U, float* I,

@@ -69,6 +69,14 @@ struct Shard {
   int index = 0;  // global shard index (== rank in rank mode)
   hipStream_t stream = nullptr;
   hipStream_t copy_stream = nullptr;  // host-to-device staging beside the sweeps (deterministic mode)
+  // ring overlap (c >= 2 user blocks per shard, systolic fast sweep): the shard's last local block
+  // runs on `aux` behind the arriving item block; the leaving block moves on `comm` as soon as
+  // the launch holding the other blocks has finished
+  hipStream_t aux = nullptr, comm = nullptr;
+  hipEvent_t ev_front = nullptr;  // launch A (local blocks 0..c-2) of the latest superstep done
+  hipEvent_t ev_last = nullptr;   // launch B (local block c-1) of the latest superstep done
+  hipEvent_t ev_moved = nullptr;  // the item block this shard sent / received in the latest ring step
+  std::vector<int64_t> st_sys_block_off;  // PairPlan::sys_block_off
   hipEvent_t done = nullptr;  // ring hand-off ordering between in-process shards
   DevBuf uf, itf, regu, regi;
   int64_t cap_u = 0, cap_i = 0;
@@ -129,6 +137,7 @@ struct mf_ctx {
   bool fast_pair = false;         // two updates per step (kernels_pair.hip), k in {64, 128, 256}
   bool fast_sys = false;          // pair cells as one systolic launch per superstep (k_sweep_pair_sys)
   bool det_sweep = false;         // deterministic mode: one persistent k_det_sweep launch per superstep
+  bool ring_overlap = false;      // fast systolic sweep, >1 shard, c >= 2: the ring step overlaps the sweep
   std::vector<int64_t> fast_rb_size;  // per rating block (fast mode)
   mf_stats stats{};
   bool profiling = false;
@@ -191,7 +200,10 @@ void init_shard(Shard& s, int device, int index) {
   DeviceGuard g(device);
   MF_HIP(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
   MF_HIP(hipStreamCreateWithFlags(&s.copy_stream, hipStreamNonBlocking));
+  MF_HIP(hipStreamCreateWithFlags(&s.aux, hipStreamNonBlocking));
+  MF_HIP(hipStreamCreateWithFlags(&s.comm, hipStreamNonBlocking));
   MF_HIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+  for (hipEvent_t* e : {&s.ev_front, &s.ev_last, &s.ev_moved}) MF_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
   for (auto& b : s.det_buf) {
     MF_HIP(hipEventCreateWithFlags(&b.copied, hipEventDisableTiming));
     MF_HIP(hipEventCreateWithFlags(&b.swept, hipEventDisableTiming));
@@ -203,6 +215,12 @@ void destroy_shard(Shard& s) {
   (void)hipSetDevice(s.device);
   (void)hipStreamSynchronize(s.stream);
   (void)hipStreamSynchronize(s.copy_stream);
+  (void)hipStreamSynchronize(s.aux);
+  (void)hipStreamSynchronize(s.comm);
+  for (hipEvent_t e : {s.ev_front, s.ev_last, s.ev_moved})
+    if (e) (void)hipEventDestroy(e);
+  (void)hipStreamDestroy(s.aux);
+  (void)hipStreamDestroy(s.comm);
   for (auto e : s.ev) (void)hipEventDestroy(e);
   s.ev.clear();
   for (auto& b : s.det_buf) {
@@ -393,6 +411,8 @@ void sync_all(mf_ctx* ctx) {
   for (auto& s : ctx->shards) {
     DeviceGuard g(s.device);
     MF_HIP(hipStreamSynchronize(s.stream));
+    MF_HIP(hipStreamSynchronize(s.aux));
+    MF_HIP(hipStreamSynchronize(s.comm));
     for (DevBuf* eb : {&s.fast_err, &s.det_err}) {
       if (!eb->get()) continue;
       int32_t err = 0;
@@ -583,16 +603,31 @@ void fast_superstep(mf_ctx* ctx, Shard& s, int64_t superstep, double eta) {
   launch_split_fork(s.stream, s.st_split.as<SplitItem>() + sp0, nsplit, s.itf.as<float>(), ctx->P.num_factors);
   if (ctx->fast_pair && ctx->fast_sys) {
     const int64_t w0 = s.st_sys_off[smod], nw = s.st_sys_off[smod + 1] - w0;
-    if (nw > 0) {
+    auto sweep = [&](hipStream_t st, int64_t a, int64_t z) {  // waves [a, z) of the superstep
+      if (z <= a) return;
       LaunchTimer tm(s, ctx->profiling, true);
-      launch_sweep_pair_sys(s.stream, s.st_sysw.as<SysWave>() + w0, s.st_sys.as<WaveDesc>(), static_cast<int>(nw),
-                            s.st_recs.as<PairRec>(), s.uf.as<float>(), s.itf.as<float>(), s.uf.bytes(), s.itf.bytes(),
-                            ctx->P.num_factors, static_cast<float>(eta), s.fast_prog.as<int32_t>(), s.sys_base,
-                            s.fast_err.as<int32_t>(), s.st_trace.get() ? s.st_trace.as<uint64_t>() : nullptr,
-                            tm.start(), tm.stop());
-      s.sys_base += s.sys_step;
+      launch_sweep_pair_sys(st, s.st_sysw.as<SysWave>() + w0 + a, s.st_sys.as<WaveDesc>(), static_cast<int>(z - a),
+                            static_cast<int>(a), s.st_recs.as<PairRec>(), s.uf.as<float>(), s.itf.as<float>(),
+                            s.uf.bytes(), s.itf.bytes(), ctx->P.num_factors, static_cast<float>(eta),
+                            s.fast_prog.as<int32_t>(), s.sys_base, s.fast_err.as<int32_t>(),
+                            s.st_trace.get() ? s.st_trace.as<uint64_t>() : nullptr, tm.start(), tm.stop());
       ctx->stats.kernel_launches += 1;
+    };
+    if (ctx->ring_overlap) {
+      // A: local blocks 0..c-2 on the compute stream, behind the previous superstep's block c-1
+      // (its item block is A's last one now); B: block c-1 on aux, behind the item block the
+      // ring step delivered.  Both may run at once (disjoint rows, all waves resident).
+      const int64_t split = s.st_sys_block_off[static_cast<size_t>(smod) * (ctx->c + 1) + ctx->c - 1];
+      MF_HIP(hipStreamWaitEvent(s.stream, s.ev_last, 0));
+      sweep(s.stream, 0, split);
+      MF_HIP(hipEventRecord(s.ev_front, s.stream));
+      MF_HIP(hipStreamWaitEvent(s.aux, s.ev_moved, 0));
+      sweep(s.aux, split, nw);
+      MF_HIP(hipEventRecord(s.ev_last, s.aux));
+    } else {
+      sweep(s.stream, 0, nw);
     }
+    if (nw > 0) s.sys_base += s.sys_step;
   } else if (ctx->fast_pair) {
     for (int32_t t = 0; t < ctx->G_fast; ++t) {
       const int64_t x = smod * ctx->G_fast + t;
@@ -647,9 +682,67 @@ RingStep ring_step(int32_t g, int32_t G, int32_t c, int32_t n, int64_t superstep
   return r;
 }
 
+// The ring step with the overlap of fast_superstep's split launches: the block leaving shard g
+// is the item block of its local block 0, done when launch A is, so it moves on the comm stream
+// behind A while launch B (block c-1) still runs; the arriving block is first needed by the next
+// superstep's launch B, which waits for ev_moved.
+void ring_shift_overlapped(mf_ctx* ctx, int64_t superstep) {
+  const int32_t n = ctx->nb;
+  const size_t k = static_cast<size_t>(ctx->P.num_factors);
+  auto bytes_of = [&](int32_t blk, size_t& off, size_t& bytes) {
+    const int64_t r0 = ctx->I.block_start[blk], cnt = ctx->I.block_start[blk + 1] - r0;
+    off = static_cast<size_t>(r0) * k * ctx->es;
+    bytes = static_cast<size_t>(cnt) * k * ctx->es;
+  };
+  if (ctx->rank_mode) {
+    Shard& s = ctx->shards[0];
+    DeviceGuard g(s.device);
+    const RingStep rs = ring_step(s.index, ctx->G, ctx->c, n, superstep);
+    size_t oo, ob, io, ib;
+    bytes_of(rs.out_blk, oo, ob);
+    bytes_of(rs.in_blk, io, ib);
+    char* base = s.itf.as<char>();
+    MF_HIP(hipStreamWaitEvent(s.comm, s.ev_front, 0));
+    MF_NCCL(ncclGroupStart());
+    if (ob > 0) MF_NCCL(ncclSend(base + oo, ob / ctx->es, ncclFloat32, rs.dst, ctx->comm, s.comm));
+    if (ib > 0) MF_NCCL(ncclRecv(base + io, ib / ctx->es, ncclFloat32, rs.src, ctx->comm, s.comm));
+    MF_NCCL(ncclGroupEnd());
+    MF_HIP(hipEventRecord(s.ev_moved, s.comm));
+  } else {
+    // the sender copies its leaving block into the receiver's slab on its comm stream once its
+    // launch A is done; the receiver's next launch B waits for that copy
+    for (auto& src : ctx->shards) {
+      const RingStep rs = ring_step(src.index, ctx->G, ctx->c, n, superstep);
+      Shard& dst = *local_shard(ctx, rs.dst);
+      size_t off, bytes;
+      bytes_of(rs.out_blk, off, bytes);
+      DeviceGuard g(src.device);
+      MF_HIP(hipStreamWaitEvent(src.comm, src.ev_front, 0));
+      if (bytes > 0)
+        MF_HIP(hipMemcpyPeerAsync(dst.itf.as<char>() + off, dst.device, src.itf.as<char>() + off, src.device, bytes,
+                                  src.comm));
+      MF_HIP(hipEventRecord(src.done, src.comm));
+    }
+    for (auto& dst : ctx->shards) {
+      Shard& src = *local_shard(ctx, ring_step(dst.index, ctx->G, ctx->c, n, superstep).src);
+      DeviceGuard g(dst.device);
+      MF_HIP(hipStreamWaitEvent(dst.comm, src.done, 0));
+      MF_HIP(hipEventRecord(dst.ev_moved, dst.comm));
+    }
+  }
+  for (int32_t g = 0; g < ctx->G; ++g) {
+    const RingStep rs = ring_step(g, ctx->G, ctx->c, n, superstep);
+    ctx->item_loc[rs.out_blk] = rs.dst;
+  }
+}
+
 // nextRatingBlock rotation (:611-619) across shards after superstep s.
 void ring_shift(mf_ctx* ctx, int64_t superstep) {
   if (ctx->G <= 1) return;
+  if (ctx->ring_overlap) {
+    ring_shift_overlapped(ctx, superstep);
+    return;
+  }
   const int32_t n = ctx->nb;
   const size_t k = static_cast<size_t>(ctx->P.num_factors);
   auto rows_of = [&](int32_t blk, int64_t& r0, int64_t& cnt) {
@@ -956,6 +1049,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
   clk.lap("rating blocks");
   const int64_t nb2 = static_cast<int64_t>(ctx->nb) * ctx->nb;
   ctx->det_sweep = false;
+  ctx->ring_overlap = false;
   if (ctx->f64) prepare_det_sweep(ctx);
   clk.lap("deterministic sweep layout");
   if (!ctx->f64) {
@@ -1047,6 +1141,11 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
     }
     ctx->fast_dummy_u = dummy;
     ctx->fast_dummy_i = static_cast<uint32_t>(ctx->I.rows());
+    {
+      const char* ov = std::getenv("MFHIP_RING_OVERLAP");
+      ctx->ring_overlap = ctx->fast_pair && ctx->fast_sys && ctx->G > 1 && ctx->c >= 2 &&
+                          ctx->P.fast_item_split == 0 && !(ov && std::string(ov) == "0");
+    }
     for (auto& s : ctx->shards) {
       ensure_rows(ctx, s, kSideU, ctx->U.rows() + 2);
       ensure_rows(ctx, s, MF_SIDE_ITEM, ctx->I.rows() + 1 + fp.scratch_rows);
@@ -1092,6 +1191,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
             MF_HIP(hipMemcpy(s.st_sysw.get(), pp.sys_waves.data(), pp.sys_waves.size() * sizeof(SysWave),
                              hipMemcpyHostToDevice));
           s.st_sys_off = pp.sys_off;
+          s.st_sys_block_off = pp.sys_block_off;
           s.sys_step = static_cast<uint32_t>(fp.G) + 1u;
           int64_t max_waves = 1;
           for (int32_t sm = 0; sm < ctx->nb; ++sm) max_waves = std::max(max_waves, pp.sys_off[sm + 1] - pp.sys_off[sm]);

@@ -913,6 +913,7 @@ void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, in
   }
   // systolic tables: superstep sm's waves are (j, g), j-major; wave (j, g) owns G_j cells
   pp.sys_off.assign(nb + 1, 0);
+  pp.sys_block_off.assign(static_cast<size_t>(nb) * (c + 1), 0);
   std::vector<std::vector<int64_t>> wave0(nb, std::vector<int64_t>(c, 0));  // sys_waves index of (sm, j, g=0)
   for (int32_t sm = 0; sm < nb; ++sm) {
     pp.sys_off[sm] = static_cast<int64_t>(pp.sys_waves.size());
@@ -922,6 +923,7 @@ void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, in
       const int32_t G = fp.cell_base[b] < 0 ? 0 : fp.Gb[b];
       const int64_t w0 = static_cast<int64_t>(pp.sys_waves.size());
       wave0[sm][j] = w0;
+      pp.sys_block_off[static_cast<size_t>(sm) * (c + 1) + j] = w0 - pp.sys_off[sm];
       for (int32_t g = 0; g < G; ++g) {
         const int32_t nbr = static_cast<int32_t>(w0 - pp.sys_off[sm]) + (g + 1 == G ? 0 : g + 1);
         pp.sys_waves.push_back(SysWave{static_cast<int64_t>(pp.sys.size()), G, nbr});
@@ -930,6 +932,8 @@ void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, in
     }
   }
   pp.sys_off[nb] = static_cast<int64_t>(pp.sys_waves.size());
+  for (int32_t sm = 0; sm < nb; ++sm)
+    pp.sys_block_off[static_cast<size_t>(sm) * (c + 1) + c] = pp.sys_off[sm + 1] - pp.sys_off[sm];
   for (int64_t x = 0; x < nsub; ++x) {
     const int64_t sm = substep_waves ? x / fp.G : x;
     int64_t w = pp.sub_off[x];

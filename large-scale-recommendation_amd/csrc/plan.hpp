@@ -240,6 +240,7 @@ struct PairPlan {
   std::vector<WaveDesc> sys;
   std::vector<SysWave> sys_waves;
   std::vector<int64_t> sys_off;
+  std::vector<int64_t> sys_block_off;  // nb * (c+1): first wave of local block j in superstep sm, relative to sys_off[sm]
   int64_t noop_halves = 0;       // pair halves that are no-ops (planner padding, repeated users)
   std::vector<double> sm_bytes;  // per superstep index: bytes the sweep requests (records + in-range rows)
 };

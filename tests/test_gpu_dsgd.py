@@ -455,3 +455,28 @@ def test_deterministic_persistent_sweep_bit_exact_hot_items(k, nb, shards):
             ids, vecs = ctx.factors(side)
             rids, rvecs = m.factors(side)
             assert np.array_equal(ids, rids) and np.array_equal(vecs, rvecs)
+
+
+@pytest.mark.parametrize("shards,nb", [(2, 4), (2, 8), (4, 8)])
+def test_ring_overlap_split_launches_bitwise(monkeypatch, shards, nb):
+    """c = nb/shards >= 2 user blocks per shard: each superstep runs as launch A (blocks 0..c-2) on
+    the compute stream and launch B (block c-1) on a second stream behind the arriving item block,
+    while the leaving block moves on a third stream as soon as A is done (the north star's ring
+    exchange overlapped with compute).  Scheduling only: factors bitwise equal to the same plan
+    without the overlap and to one shard."""
+    monkeypatch.setenv("MFHIP_PAIR_SYS", "1")
+    monkeypatch.setenv("MFHIP_BLOCK_GROUPS", "0")  # the same uniform G on every path
+    d = hot_item_data(64)
+    big = synth.generate(4000, 900, 120000, seed=31)
+    d.u = np.concatenate([d.u, big.u + 500])
+    d.i = np.concatenate([d.i, big.i + 200])
+    d.r = np.concatenate([d.r, big.r])
+    outs = []
+    for devs, ov in (([0], "1"), ([0] * shards, "0"), ([0] * shards, "1")):
+        monkeypatch.setenv("MFHIP_RING_OVERLAP", ov)
+        with mfhip.Context(params(64, 2, nb, 5, mode=L.MODE_FAST_F32, fast_waves=-8), devices=devs) as ctx:
+            ctx.fit(d.u, d.i, d.r)
+            outs.append((ctx.factors(0)[1], ctx.factors(1)[1], ctx.stats()["kernel_launches"]))
+    for o in outs[1:]:
+        assert np.array_equal(outs[0][0], o[0]) and np.array_equal(outs[0][1], o[1])
+    assert outs[2][2] > outs[1][2]  # the overlapped path really split the launches
