@@ -97,6 +97,14 @@ void launch_predict(hipStream_t st, const int32_t* urow, const int32_t* irow, in
                     const void* U, const void* I, int k, bool f64, double* out, const double* r,
                     const int32_t* mult, double lambda, double* partials);
 
+// DSGD blocking on the device (kernels_block.hip): both SideLayouts (initFactorBlockAndIndices,
+// DSGDforMF.scala:513-588, the reference's seeded blocking) and the rating blocks of user blocks
+// [ub_lo, ub_hi) (:301-327; sort_ui: (user, item) order inside a block), bitwise what
+// build_side + build_rating_blocks (plan.cpp) produce.  Host arrays in, host structures out.
+void device_blocking(hipStream_t st, const int32_t* u, const int32_t* i, const double* r, int64_t n, int32_t nb,
+                     int64_t seed, int32_t ub_lo, int32_t ub_hi, bool sort_ui, SideLayout& U, SideLayout& I,
+                     RatingBlocks& rb);
+
 // Initial factor rows on the device (DSGDforMF.scala:548-549, MatrixFactorization.scala:278-280):
 // row x, factor f = the f-th nextDouble of new Random(ids[x] ^ seed) (xor_seed) or of
 // new Random(ids[x]).  One thread per element: the JVM LCG state after m steps is

@@ -474,11 +474,14 @@ void init_factors(mf_ctx* ctx) {
   }
 }
 
-void build_model(mf_ctx* ctx, const int32_t* u, const int32_t* i, int64_t n) {
+// sides_built: ctx->U / ctx->I already hold the blocking (device_blocking).
+void build_model(mf_ctx* ctx, const int32_t* u, const int32_t* i, int64_t n, bool sides_built) {
   const bool seeded = ctx->P.has_seed != 0;
   const Blocking bl = !ctx->f64 && ctx->P.fast_blocking == MF_BLOCKING_BALANCED ? Blocking::kBalanced : Blocking::kJvm;
-  build_side(ctx->U, u, n, ctx->nb, ctx->P.seed, seeded, bl);
-  build_side(ctx->I, i, n, ctx->nb, ctx->P.seed, seeded, bl);
+  if (!sides_built) {
+    build_side(ctx->U, u, n, ctx->nb, ctx->P.seed, seeded, bl);
+    build_side(ctx->I, i, n, ctx->nb, ctx->P.seed, seeded, bl);
+  }
   for (int side = 0; side < 2; ++side) {
     SideLayout& S = side == kSideU ? ctx->U : ctx->I;
     std::vector<double> reg(S.rows());
@@ -1041,12 +1044,24 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
   ctx->nb = std::max(1, ctx->P.num_blocks);
   MF_REQUIRE(ctx->nb % ctx->G == 0, "num_blocks must be a multiple of the device count");
   ctx->c = ctx->nb / ctx->G;
-  build_model(ctx, u, i, n);
-  clk.lap("blocking + factor init + H2D");
   int32_t lo = 0, hi = ctx->nb;
   if (ctx->rank_mode) { lo = ctx->shards[0].index * ctx->c; hi = lo + ctx->c; }
-  build_rating_blocks(ctx->rb, ctx->U, ctx->I, u, i, r, n, lo, hi, ctx->f64 && ctx->P.has_seed);
-  clk.lap("rating blocks");
+  // the reference's seeded blocking runs on the device (MFHIP_HOST_BLOCKING=1: on the host)
+  const char* hb = std::getenv("MFHIP_HOST_BLOCKING");
+  const bool on_device = ctx->P.has_seed && (ctx->f64 || ctx->P.fast_blocking == MF_BLOCKING_REFERENCE) &&
+                         !(hb && std::string(hb) != "0") && n < (int64_t{1} << 31);
+  if (on_device) {
+    Shard& s0 = ctx->shards[0];
+    DeviceGuard g(s0.device);
+    device_blocking(s0.stream, u, i, r, n, ctx->nb, ctx->P.seed, lo, hi, ctx->f64, ctx->U, ctx->I, ctx->rb);
+    clk.lap("blocking + rating blocks (device)");
+  }
+  build_model(ctx, u, i, n, on_device);
+  clk.lap("factor init + H2D");
+  if (!on_device) {
+    build_rating_blocks(ctx->rb, ctx->U, ctx->I, u, i, r, n, lo, hi, ctx->f64 && ctx->P.has_seed);
+    clk.lap("rating blocks");
+  }
   const int64_t nb2 = static_cast<int64_t>(ctx->nb) * ctx->nb;
   ctx->det_sweep = false;
   ctx->ring_overlap = false;

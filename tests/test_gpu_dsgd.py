@@ -480,3 +480,31 @@ def test_ring_overlap_split_launches_bitwise(monkeypatch, shards, nb):
     for o in outs[1:]:
         assert np.array_equal(outs[0][0], o[0]) and np.array_equal(outs[0][1], o[1])
     assert outs[2][2] > outs[1][2]  # the overlapped path really split the launches
+
+
+@pytest.mark.parametrize("mode,k,nb,seed", [(L.MODE_DETERMINISTIC_F64, 16, 4, 3), (L.MODE_DETERMINISTIC_F64, 8, 7, -9),
+                                            (L.MODE_FAST_F32, 64, 8, 0), (L.MODE_FAST_F32, 128, 3, 11)])
+def test_device_blocking_equals_host_blocking(monkeypatch, mode, k, nb, seed):
+    """Blocking on the GPU (kernels_block.hip: radix sorts, scans, the JVM block draw per id) ==
+    the host's build_side + build_rating_blocks bit for bit: the deterministic fit replays the
+    reference's shuffled order inside each rating block and the fast plan depends on every row's
+    position, so any difference in blocks, rows or in-block order changes the factors.  Data with
+    negative ids, duplicate (user, item) pairs and ids far apart (the host's sparse path)."""
+    d = synth.generate(1500, 400, 40000, seed=nb)
+    u = d.u.copy()
+    u[::53] = -u[::53] - 7
+    u[::211] += 1_500_000_000
+    i = d.i.copy()
+    i[::97] = -i[::97] - 1
+    u = np.concatenate([u, u[:3000]])
+    i = np.concatenate([i, i[:3000]])
+    r = np.concatenate([d.r, d.r[:3000][::-1]])
+    outs = []
+    for host in ("1", "0"):
+        monkeypatch.setenv("MFHIP_HOST_BLOCKING", host)
+        with mfhip.Context(params(k, 2, nb, seed, mode=mode)) as ctx:
+            ctx.fit(u, i, r)
+            outs.append([ctx.factors(s) for s in (0, 1)])
+    for s in (0, 1):
+        assert np.array_equal(outs[0][s][0], outs[1][s][0])
+        assert np.array_equal(outs[0][s][1], outs[1][s][1])
