@@ -2,6 +2,7 @@
 #include "plan.hpp"
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <unordered_map>
@@ -418,6 +419,21 @@ void lpt_groups(const std::vector<int64_t>& load, int32_t G, std::vector<int32_t
   }
 }
 
+// MFHIP_TIMING: build_fast_plan's per-phase thread time (summed over blocks), on stderr
+struct PhaseTimes {
+  std::atomic<int64_t> ns[5];
+  const char* names[5] = {"groups", "keys+sort", "spread", "emit", "other"};
+};
+PhaseTimes g_fp_times;
+struct PhaseTick {
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void lap(int phase) {
+    const auto now = std::chrono::steady_clock::now();
+    g_fp_times.ns[phase] += std::chrono::duration_cast<std::chrono::nanoseconds>(now - t).count();
+    t = now;
+  }
+};
+
 inline uint32_t mix32(uint64_t x) {
   x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;
   return static_cast<uint32_t>(x);
@@ -487,7 +503,9 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
     }
     fp.scratch_rows = cursor;
   }
+  for (auto& x : g_fp_times.ns) x = 0;
   parallel_tasks(nblk, [&](int64_t bx) {
+    PhaseTick tick;
     const int64_t b = blocks[bx];
     const int32_t G = fp.Gb[b];
     const int64_t GG = static_cast<int64_t>(G) * G;
@@ -531,46 +549,67 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
     std::vector<int32_t> gu, gi;
     lpt_groups(lu, G, gu);
     lpt_groups(li, G, gi);
+    tick.lap(0);
+    // Cell-major order: counting sort by cell (stable in x), then (item, tie, x) inside a cell --
+    // the order of sorting the whole block by (cell << 40 | item << 16 | tie, x).
     std::vector<std::pair<uint64_t, int64_t>> key(len);
-    for (int64_t x = 0; x < len; ++x) {
-      const int64_t j = s + x;
-      const uint32_t il = vil[x];
-      const uint32_t ul = rb.urow[j] - static_cast<uint32_t>(ub);
-      const int32_t g = gi[il], h = gu[ul];
-      const int64_t t = ((h - g) % G + G) % G;
-      const uint64_t cell = static_cast<uint64_t>(t * G + g);
-      const uint64_t tie = mix32(order_seed ^ (static_cast<uint64_t>(rb.urow[j]) << 20)) & 0xFFFFu;
-      key[x] = {(cell << 40) | (static_cast<uint64_t>(il) << 16) | tie, x};
+    {
+      std::vector<int32_t> cell_of(len);
+      std::vector<int64_t> cstart(GG + 1, 0);
+      for (int64_t x = 0; x < len; ++x) {
+        const uint32_t ul = rb.urow[s + x] - static_cast<uint32_t>(ub);
+        const int32_t g = gi[vil[x]], h = gu[ul];
+        const int64_t t = ((h - g) % G + G) % G;
+        cell_of[x] = static_cast<int32_t>(t * G + g);
+        cstart[cell_of[x] + 1]++;
+      }
+      for (int64_t c = 0; c < GG; ++c) cstart[c + 1] += cstart[c];
+      std::vector<int64_t> cur(cstart.begin(), cstart.end() - 1);
+      for (int64_t x = 0; x < len; ++x) {
+        const uint64_t cell = static_cast<uint64_t>(cell_of[x]);
+        const uint64_t tie = mix32(order_seed ^ (static_cast<uint64_t>(rb.urow[s + x]) << 20)) & 0xFFFFu;
+        key[cur[cell]++] = {(cell << 40) | (static_cast<uint64_t>(vil[x]) << 16) | tie, x};
+      }
+      for (int64_t c = 0; c < GG; ++c)
+        if (cstart[c + 1] - cstart[c] > 1) std::sort(key.begin() + cstart[c], key.begin() + cstart[c + 1]);
     }
-    std::sort(key.begin(), key.end());
+    tick.lap(1);
     // Repeated (user, item) ratings (frequent in Zipf-distributed data: a heavy user rates a hot
     // item dozens of times) would sit next to each other and force no-op halves into the pair
     // steps (a pair cannot hold one user twice).  Spread them: inside an item run, the m
     // ratings of one user go to the fractional positions (o + h_u) / m, o = 0..m-1, h_u a
     // per-user hash in [0, 1) -- evenly over the whole run, interleaved with everyone else.
+    // Runs are contiguous in key order, so each run is re-sorted on its own by (position, x).
     {
-      struct K { uint64_t run, pos; int64_t x; };
-      std::vector<K> k2(len);
-      std::unordered_map<uint32_t, std::pair<uint32_t, uint32_t>> seen;  // user -> (count, next occurrence)
+      struct K { uint64_t pos; int64_t x; };
+      std::vector<K> k2;
+      std::vector<uint32_t> ucnt(nu, 0), unext(nu, 0);  // per local user in the current run
       for (int64_t y0 = 0; y0 < len;) {
         const uint64_t run = key[y0].first & ~0xFFFFull;  // cell and item
         int64_t y1 = y0;
-        seen.clear();
-        while (y1 < len && (key[y1].first & ~0xFFFFull) == run) seen[rb.urow[s + key[y1].second]].first++, ++y1;
+        while (y1 < len && (key[y1].first & ~0xFFFFull) == run) ucnt[rb.urow[s + key[y1].second] - ub]++, ++y1;
+        if (y1 - y0 > 1) {
+          k2.resize(y1 - y0);
+          for (int64_t y = y0; y < y1; ++y) {
+            const uint32_t urow = rb.urow[s + key[y].second];
+            const uint32_t ul = urow - static_cast<uint32_t>(ub);
+            const double h = static_cast<double>(mix32(order_seed * 0x2545F4914F6CDD1DULL ^ urow)) * (1.0 / 4294967296.0);
+            const double frac = (unext[ul]++ + h) / ucnt[ul];
+            k2[y - y0] = K{(static_cast<uint64_t>(frac * 16777216.0) << 16) | (key[y].first & 0xFFFFull), key[y].second};
+          }
+          std::sort(k2.begin(), k2.end(), [](const K& a, const K& b) { return a.pos != b.pos ? a.pos < b.pos : a.x < b.x; });
+          for (int64_t y = y0; y < y1; ++y) key[y] = {run, k2[y - y0].x};
+        } else {
+          key[y0].first = run;
+        }
         for (int64_t y = y0; y < y1; ++y) {
-          const uint32_t urow = rb.urow[s + key[y].second];
-          auto& e = seen[urow];
-          const double h = static_cast<double>(mix32(order_seed * 0x2545F4914F6CDD1DULL ^ urow)) * (1.0 / 4294967296.0);
-          const double frac = (e.second++ + h) / e.first;
-          k2[y] = K{run, (static_cast<uint64_t>(frac * 16777216.0) << 16) | (key[y].first & 0xFFFFull), key[y].second};
+          const uint32_t ul = rb.urow[s + key[y].second] - static_cast<uint32_t>(ub);
+          ucnt[ul] = unext[ul] = 0;
         }
         y0 = y1;
       }
-      std::sort(k2.begin(), k2.end(), [](const K& a, const K& b) {
-        return a.run != b.run ? a.run < b.run : a.pos != b.pos ? a.pos < b.pos : a.x < b.x;
-      });
-      for (int64_t y = 0; y < len; ++y) key[y] = {k2[y].run, k2[y].x};
     }
+    tick.lap(2);
     // Emit each cell as a sequence the kernel can run with a D-deep prefetch ring: every user
     // and every item row recurs either at the next position (the kernel forwards it in
     // registers: item runs and user runs) or at least kHazardWindow positions later (its
@@ -579,6 +618,8 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
     // item; otherwise start from the item with the most pending ratings whose row and some
     // pending user row are both free; only when nothing qualifies emit a no-op record (zero
     // user row, current item).  last_*[x] = (cell, position) of the row's latest emission.
+    // Groups are flat: an item group is a contiguous range of the cell's entries, a user group a
+    // range of a per-cell CSR list (entries in cell order).
     std::vector<FastRec>& out = outs[bx];
     std::vector<int64_t>& src = srcs[bx];
     std::vector<int32_t>& off = offs[bx];
@@ -588,9 +629,10 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
     std::vector<std::pair<int64_t, int64_t>> last_u(nu, {-1, 0}), last_i(nv, {-1, 0});
     std::vector<std::pair<int64_t, int32_t>> uslot(nu, {-1, 0});
     struct Ent { uint32_t ul, il; int32_t ug, ig; int64_t j; };
-    struct Grp { std::vector<int32_t> e; size_t head = 0; int32_t left = 0; uint32_t row = 0; };
+    struct Grp { int32_t beg = 0, end = 0, head = 0, left = 0; uint32_t row = 0; };  // [beg, end) of its list
     std::vector<Ent> ents;
     std::vector<Grp> igs, ugs;
+    std::vector<int32_t> ulist, ufill;  // user groups' entry lists (CSR over ugs)
     std::vector<uint8_t> taken;
     std::vector<int32_t> iorder;
     int64_t x = 0;
@@ -602,23 +644,35 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
       while (x < len && static_cast<int64_t>(key[x].first >> 40) == c) {
         const int64_t j = s + key[x].second;
         const uint32_t il = vil[key[x].second], ul = rb.urow[j] - static_cast<uint32_t>(ub);
-        if (igs.empty() || ents.back().il != il) { igs.emplace_back(); igs.back().row = il; }
+        const int32_t e = static_cast<int32_t>(ents.size());
+        if (igs.empty() || ents.back().il != il) {
+          igs.emplace_back();
+          igs.back().row = il;
+          igs.back().beg = igs.back().head = e;
+        }
         auto& us = uslot[ul];
         if (us.first != c) { us = {c, static_cast<int32_t>(ugs.size())}; ugs.emplace_back(); }
-        const int32_t e = static_cast<int32_t>(ents.size());
         ents.push_back(Ent{ul, il, us.second, static_cast<int32_t>(igs.size()) - 1, j});
-        igs.back().e.push_back(e);
-        ugs[us.second].e.push_back(e);
+        igs.back().end = e + 1;
+        ugs[us.second].end++;  // count for now
         ++x;
       }
       const int32_t m = static_cast<int32_t>(ents.size());
+      {  // user groups: counts -> CSR ranges, entries in cell order
+        int32_t acc = 0;
+        for (auto& g2 : ugs) { const int32_t n2 = g2.end; g2.beg = g2.head = acc; acc += n2; g2.end = acc; }
+        ulist.resize(m);
+        ufill.resize(ugs.size());
+        for (size_t g2 = 0; g2 < ugs.size(); ++g2) ufill[g2] = ugs[g2].beg;
+        for (int32_t e = 0; e < m; ++e) ulist[ufill[ents[e].ug]++] = e;
+      }
       taken.assign(m, 0);
-      for (auto& g2 : igs) g2.left = static_cast<int32_t>(g2.e.size());
-      for (auto& g2 : ugs) g2.left = static_cast<int32_t>(g2.e.size());
+      for (auto& g2 : igs) g2.left = g2.end - g2.beg;
+      for (auto& g2 : ugs) g2.left = g2.end - g2.beg;
       iorder.resize(igs.size());
       std::iota(iorder.begin(), iorder.end(), 0);
       std::stable_sort(iorder.begin(), iorder.end(), [&](int32_t a2, int32_t b2) {
-        return igs[a2].e.size() > igs[b2].e.size();
+        return igs[a2].end - igs[a2].beg > igs[b2].end - igs[b2].beg;
       });
       size_t iorder_head = 0;
       int32_t prev_ug = -1, prev_ig = -1;
@@ -628,11 +682,12 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
         const int64_t pos = static_cast<int64_t>(out.size()) - cell_begin;
         auto ufree = [&](uint32_t ul) { return last_u[ul].first != c || pos - last_u[ul].second >= kHazardWindow; };
         auto ifree = [&](uint32_t il) { return last_i[il].first != c || pos - last_i[il].second >= kHazardWindow; };
-        auto scan = [&](Grp& g2, auto ok) -> int32_t {
-          while (g2.head < g2.e.size() && taken[g2.e[g2.head]]) ++g2.head;
+        // the first untaken entries of a group's list (at most 4 * window of them) that pass ok
+        auto scan = [&](Grp& g2, const int32_t* list, auto ok) -> int32_t {
+          while (g2.head < g2.end && taken[list ? list[g2.head] : g2.head]) ++g2.head;
           int seen = 0;
-          for (size_t y = g2.head; y < g2.e.size() && seen < 4 * kHazardWindow; ++y) {
-            const int32_t e = g2.e[y];
+          for (int32_t y = g2.head; y < g2.end && seen < 4 * kHazardWindow; ++y) {
+            const int32_t e = list ? list[y] : y;
             if (taken[e]) continue;
             ++seen;
             if (ok(ents[e])) return e;
@@ -641,11 +696,11 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
         };
         auto try_item = [&]() -> int32_t {  // continue the item run
           if (prev_ig < 0 || igs[prev_ig].left == 0) return -1;
-          return scan(igs[prev_ig], [&](const Ent& en) { return en.ug == prev_ug || ufree(en.ul); });
+          return scan(igs[prev_ig], nullptr, [&](const Ent& en) { return en.ug == prev_ug || ufree(en.ul); });
         };
         auto try_user = [&]() -> int32_t {  // continue the user run
           if (prev_ug < 0 || ugs[prev_ug].left == 0) return -1;
-          return scan(ugs[prev_ug], [&](const Ent& en) { return en.ig == prev_ig || ifree(en.il); });
+          return scan(ugs[prev_ug], ulist.data(), [&](const Ent& en) { return en.ig == prev_ig || ifree(en.il); });
         };
         const bool user_first = prev_ug >= 0 && prev_ig >= 0 && ugs[prev_ug].left > igs[prev_ig].left;
         int32_t pick = user_first ? try_user() : try_item();
@@ -658,7 +713,7 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
             if (g2.left == 0) continue;
             ++tried;
             if (!ifree(g2.row)) continue;
-            pick = scan(g2, [&](const Ent& en) { return ufree(en.ul); });
+            pick = scan(g2, nullptr, [&](const Ent& en) { return ufree(en.ul); });
             if (pick >= 0) break;
           }
         }
@@ -691,7 +746,11 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
       }
       off[c + 1] = static_cast<int32_t>(out.size());
     }
+    tick.lap(3);
   });
+  if (std::getenv("MFHIP_TIMING"))
+    for (int ph = 0; ph < 4; ++ph)
+      std::fprintf(stderr, "[mfhip]   fast plan %-10s %8.3f s (thread time)\n", g_fp_times.names[ph], g_fp_times.ns[ph] * 1e-9);
   int64_t total = 0, cells = 0;
   for (int64_t bx = 0; bx < nblk; ++bx) {
     fp.rec_base[blocks[bx]] = total;
@@ -871,17 +930,21 @@ void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, in
       }
       // the lean path prefetches kPairRingSingle pairs ahead: a user row it loads must have
       // been stored by an earlier pair at least that far back
-      if (single) {
-        std::unordered_map<uint32_t, int64_t> stored;
+      if (single) {  // the stores of the previous kPairRingSingle - 1 pairs, as a ring
+        constexpr int kR = kPairRingSingle - 1;
+        uint32_t ring[kR > 0 ? kR : 1][2];
+        for (auto& rr : ring) rr[0] = rr[1] = kOffOOB;
         for (const PairRec* r = first; single && r < out; ++r) {
           const int64_t j = r - first;
           for (uint32_t off : {r->ua, r->ub}) {
             if (off == kOffOOB) continue;
-            const auto it = stored.find(off);
-            if (it != stored.end() && j - it->second < kPairRingSingle) { single = false; why = 6; }
+            for (int y = 0; y < kR; ++y)
+              if (ring[y][0] == off || ring[y][1] == off) { single = false; why = 6; }
           }
-          if (r->sa != kOffOOB) stored[r->sa] = j;
-          if (r->sb != kOffOOB) stored[r->sb] = j;
+          if (kR > 0) {
+            ring[j % kR][0] = r->sa;
+            ring[j % kR][1] = r->sb;
+          }
         }
       }
       if (single) pp.waves[w_this].cells = kWaveSingleRun;

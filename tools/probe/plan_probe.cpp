@@ -58,6 +58,18 @@ int main(int argc, char** argv) {
   build_pair_plan(pp, fp, nb, nb, 0, k, false);
   std::printf("pair plan %.3f s\n", lap());
   std::printf("pads %lld noop halves %lld pairs %zu\n", (long long)fp.pads, (long long)pp.noop_halves, pp.recs.size());
+  {  // fingerprint of the plans (FNV-1a over the records, cell offsets and pair records)
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](const void* p, size_t n) {
+      const unsigned char* c = static_cast<const unsigned char*>(p);
+      for (size_t x = 0; x < n; ++x) { h ^= c[x]; h *= 1099511628211ull; }
+    };
+    mix(fp.recs.data(), fp.recs.size() * sizeof(FastRec));
+    mix(fp.cell_off.data(), fp.cell_off.size() * 4);
+    mix(pp.recs.data(), pp.recs.size() * sizeof(PairRec));
+    mix(pp.sys.data(), pp.sys.size() * sizeof(WaveDesc));
+    std::printf("plan fingerprint %016llx\n", (unsigned long long)h);
+  }
   for (int sm = 0; sm < nb; ++sm) {
     int64_t maxp = 0, maxw = -1, singles = 0, waves_sm = pp.sys_off[sm + 1] - pp.sys_off[sm];
     for (int64_t w = pp.sys_off[sm]; w < pp.sys_off[sm + 1]; ++w) {
