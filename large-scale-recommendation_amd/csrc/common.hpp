@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdlib>
+#include <atomic>
 #include <functional>
 #include <stdexcept>
 #include <string>
@@ -144,15 +145,17 @@ inline void parallel_for(int64_t n, const std::function<void(int64_t, int64_t, i
   for (auto& x : th) x.join();
 }
 
-// parallel over independent tasks 0..n-1 (dynamic: task t -> worker t % w).
+// parallel over independent tasks 0..n-1, dynamically: each worker takes the next task index
+// (tasks of very different sizes -- rating blocks -- then balance).
 inline void parallel_tasks(int64_t n, const std::function<void(int64_t)>& fn, int max_workers = 0) {
   if (n <= 0) return;
   int w = max_workers > 0 ? max_workers : host_threads();
   w = static_cast<int>(std::min<int64_t>(w, n));
   if (w <= 1) { for (int64_t t = 0; t < n; ++t) fn(t); return; }
+  std::atomic<int64_t> next{0};
   std::vector<std::thread> th;
   for (int t = 0; t < w; ++t)
-    th.emplace_back([&, t] { for (int64_t x = t; x < n; x += w) fn(x); });
+    th.emplace_back([&] { for (int64_t x; (x = next.fetch_add(1)) < n;) fn(x); });
   for (auto& x : th) x.join();
 }
 
