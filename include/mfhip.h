@@ -250,6 +250,18 @@ int mf_debug_fast_split(const int32_t* users, const int32_t* items, int64_t n, i
                         int64_t seed, int32_t groups, int32_t blocking, int32_t window, int32_t item_split,
                         int32_t* block_out, int32_t* substep_out, int32_t* group_out, int64_t* pos_out,
                         int32_t* replica_out);
+/* mf_debug_fast_stream: the stream sweep's plan (k_sweep_stream; reference blocking) with G = groups
+   item groups and ustride * G user groups per rating block: rating j is in sub-step substep_out[j]
+   (0 .. ustride*G-1) of item group group_out[j], at pos_out[j] inside its cell.  Applying the
+   ratings sequentially in (sub-step, block, group, pos) order is what the sweep computes. */
+int mf_debug_fast_stream(const int32_t* users, const int32_t* items, int64_t n, int32_t n_blocks, int64_t seed,
+                         int32_t groups, int32_t ustride, int32_t window, int32_t* block_out, int32_t* substep_out,
+                         int32_t* group_out, int64_t* pos_out);
+/* mf_debug_stream_protocol: builds the stream sweep's plan exactly as mf_dsgd_prepare does on one
+   device (k, groups, ustride) and replays the kernel's hand-off protocol on the host:
+   *stuck_out = the supersteps whose waves could not all finish (0 = deadlock-free). */
+int mf_debug_stream_protocol(const int32_t* users, const int32_t* items, int64_t n, int32_t n_blocks, int64_t seed,
+                             int32_t groups, int32_t ustride, int32_t k, int64_t* stuck_out);
 /* mf_debug_ring_schedule: the item-block ring step ring_shift runs after superstep `superstep`
    (1-based) on rank `rank` of `world` with n blocks (n = c * world): the item block it sends
    (*out_blk) to rank *dst and the one it receives (*in_blk) from rank *src -- nextRatingBlock

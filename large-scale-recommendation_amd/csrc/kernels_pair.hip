@@ -35,145 +35,7 @@
 namespace mfhip {
 namespace {
 
-typedef float f2 __attribute__((ext_vector_type(2)));
-typedef uint32_t u4v __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ uint32_t rl(uint32_t v, int l) {
-  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), l));
-}
-__device__ __forceinline__ float rlf(float v, int l) { return __uint_as_float(rl(__float_as_uint(v), l)); }
-
-template <int CTRL>
-__device__ __forceinline__ float dpp(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-
-__device__ __forceinline__ float u2f(uint32_t v) { return __uint_as_float(v); }
-__device__ __forceinline__ uint32_t f2u(float v) { return __float_as_uint(v); }
-
-// Three 64-lane sums at once, uniform results.  gfx950's half swaps fold the three values into
-// one register first (v_permlane32_swap: x | y halves; v_permlane16_swap: rows of x, z, y, z),
-// so only one 16-lane butterfly remains: 10 VALU operations instead of 18 interleaved DPP adds
-// (measured equal per step: a swap costs ~14 cycles against ~4.6 for an interleaved DPP add).
-__device__ __forceinline__ void wave_sum3(float& x, float& y, float& z) {
-  const auto xy = __builtin_amdgcn_permlane32_swap(f2u(x), f2u(y), false, false);  // [x_lo y_lo], [x_hi y_hi]
-  const auto zz = __builtin_amdgcn_permlane32_swap(f2u(z), f2u(z), false, false);  // [z_lo z_lo], [z_hi z_hi]
-  const float v = u2f(xy[0]) + u2f(xy[1]);  // lanes 0-31: x halves summed, 32-63: y
-  const float w = u2f(zz[0]) + u2f(zz[1]);  // z halves summed (both halves)
-  const auto vw = __builtin_amdgcn_permlane16_swap(f2u(v), f2u(w), false, false);
-  float s = u2f(vw[0]) + u2f(vw[1]);  // row 0: x, row 1: z, row 2: y, row 3: z (16-lane partials)
-  s += dpp<0xB1>(s);
-  s += dpp<0x4E>(s);
-  s += dpp<0x141>(s);
-  s += dpp<0x140>(s);
-  x = rlf(s, 0);
-  z = rlf(s, 16);
-  y = rlf(s, 32);
-}
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t raw_rsrc(const void* base, uint64_t bytes) {
-  const uint32_t n = bytes > 0xFFFFF000ull ? 0xFFFFF000u : static_cast<uint32_t>(bytes);
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, n, 0x00020000);
-}
-
-// A lane holds floats [lane*KPL, (lane+1)*KPL) of a row, as NV float pairs.
-template <int KPL>
-struct Row {
-  static constexpr int NV = KPL == 1 ? 1 : KPL / 2;
-  f2 v[NV];
-};
-
-// Cache policy of a row access: 0 = plain; kSC1 = sc1 (L1 bypass on loads, write-through and
-// dropped from the XCD's L2 on stores), used for user rows handed between waves of the
-// systolic sweep (MI355X_MICROARCH.md, inter-workgroup visibility, valid forms).
-constexpr int kSC1 = 16;
-
-template <int KPL, int POL = 0>
-__device__ __forceinline__ Row<KPL> ld(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t off) {
-  Row<KPL> r;
-  if constexpr (KPL == 1) {
-    r.v[0] = f2{__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, voff, off, POL)), 0.f};
-  } else if constexpr (KPL == 2) {
-    const auto x = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, off, POL);
-    r.v[0] = f2{__uint_as_float(x[0]), __uint_as_float(x[1])};
-  } else {
-#pragma unroll
-    for (int c = 0; c < KPL / 4; ++c) {
-      const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 16u * c, off, POL);
-      r.v[2 * c] = f2{__uint_as_float(x[0]), __uint_as_float(x[1])};
-      r.v[2 * c + 1] = f2{__uint_as_float(x[2]), __uint_as_float(x[3])};
-    }
-  }
-  return r;
-}
-
-template <int KPL, int POL = 0>
-__device__ __forceinline__ void st(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t off, const Row<KPL>& r) {
-  if constexpr (KPL == 1) {
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.v[0].x), rs, voff, off, POL);
-  } else if constexpr (KPL == 2) {
-    using u2 = uint32_t __attribute__((ext_vector_type(2)));
-    __builtin_amdgcn_raw_buffer_store_b64(u2{__float_as_uint(r.v[0].x), __float_as_uint(r.v[0].y)}, rs, voff, off, POL);
-  } else {
-#pragma unroll
-    for (int c = 0; c < KPL / 4; ++c)
-      __builtin_amdgcn_raw_buffer_store_b128(u4v{__float_as_uint(r.v[2 * c].x), __float_as_uint(r.v[2 * c].y),
-                                                 __float_as_uint(r.v[2 * c + 1].x), __float_as_uint(r.v[2 * c + 1].y)},
-                                             rs, voff + 16u * c, off, POL);
-  }
-}
-
-template <int KPL>
-__device__ __forceinline__ float dot_part(const Row<KPL>& a, const Row<KPL>& b) {
-  f2 acc = a.v[0] * b.v[0];
-#pragma unroll
-  for (int e = 1; e < Row<KPL>::NV; ++e) acc = a.v[e] * b.v[e] + acc;
-  return KPL == 1 ? acc.x : acc.x + acc.y;
-}
-
-// CH consecutive pair records of the cell, pair y in lane y (index clamped to the cell).
-struct Chunk {
-  uint32_t ua, ub, ia, ib;  // loads (byte offsets)
-  uint32_t sa, sb, sia, si; // stores
-  uint32_t flags;
-  float era, erb;           // eta * r
-  float aa, ab, ba, bb;     // 1 - eta * ri, 1 - eta * ru (1 for no-op records)
-};
-
-// A chunk's records as loaded (raw words, one pair per lane).  The next chunk is loaded a whole
-// chunk ahead and only converted (eta folded in) when it becomes current, so nothing reads a
-// just-loaded register at the chunk boundary and the factor-row ring keeps running across it
-// (converting at load time made every chunk boundary wait for its own record loads).
-// s_waitcnt vmcnt(0) the compiler can see (gfx9 encoding: expcnt 7, lgkmcnt 15).  Issued once
-// after a wave's initial prefetch: otherwise the loop header inherits the preheader's "just
-// loaded" ring rows and the compiler drains the ring at EVERY chunk boundary (vmcnt(0) in the
-// header, i.e. once per 56 pairs).
-__device__ __forceinline__ void drain_vmem() { __builtin_amdgcn_s_waitcnt(0x0F70); }
-
-struct ChunkRaw {
-  u4v w0, w1, w2, w3;
-};
-
-__device__ __forceinline__ ChunkRaw chunk_load(const u4v* __restrict__ R, int c, int npairs, int lane) {
-  const int64_t x = min(c * kPairChunk + lane, npairs - 1);
-  // records are read once: non-temporal, so they do not push factor rows out of L2 / MALL
-  return ChunkRaw{__builtin_nontemporal_load(R + 4 * x), __builtin_nontemporal_load(R + 4 * x + 1),
-                  __builtin_nontemporal_load(R + 4 * x + 2), __builtin_nontemporal_load(R + 4 * x + 3)};
-}
-
-__device__ __forceinline__ Chunk chunk_convert(const ChunkRaw& r, float eta) {
-  Chunk ch;
-  ch.ua = r.w0[0]; ch.ub = r.w0[1]; ch.ia = r.w0[2]; ch.ib = r.w0[3];
-  ch.sa = r.w1[0]; ch.sb = r.w1[1]; ch.sia = r.w1[2]; ch.si = r.w1[3];
-  ch.flags = r.w2[0];
-  ch.era = eta * __uint_as_float(r.w2[1]);
-  ch.erb = eta * __uint_as_float(r.w2[2]);
-  ch.ba = fmaf(-eta, __uint_as_float(r.w2[3]), 1.f);
-  ch.bb = fmaf(-eta, __uint_as_float(r.w3[0]), 1.f);
-  ch.aa = fmaf(-eta, __uint_as_float(r.w3[1]), 1.f);
-  ch.ab = fmaf(-eta, __uint_as_float(r.w3[2]), 1.f);
-  return ch;
-}
+#include "pair_device.hpp"
 
 // One cell (WaveDesc d) of the pair schedule, swept by the calling wave.  UP = cache policy of
 // the user-row loads and stores.

@@ -96,7 +96,8 @@ EXPORTS = [
     "mf_reset_stats", "mf_jvm_shuffle", "mf_jvm_block_of", "mf_jvm_random_factors",
     "mf_learning_rate", "mf_debug_levels", "mf_debug_fast_schedule", "mf_debug_fast_split", "mf_fast_plan_window",
     "mf_fast_kernel_name", "mf_get_params", "mf_read_ratings", "mf_save_model", "mf_load_model",
-    "mf_dsgd_restart", "mf_online_update_out", "mf_debug_ring_schedule",
+    "mf_dsgd_restart", "mf_online_update_out", "mf_debug_ring_schedule", "mf_debug_fast_stream",
+    "mf_debug_stream_protocol",
 ]
 
 _i32p = C.POINTER(C.c_int32)
@@ -156,6 +157,10 @@ def lib() -> C.CDLL:
                                              C.c_int32, _i32p, _i32p, _i32p, _i64p]),
         "mf_debug_fast_split": (C.c_int, [_i32p, _i32p, C.c_int64, C.c_int32, C.c_int64, C.c_int32, C.c_int32,
                                           C.c_int32, C.c_int32, _i32p, _i32p, _i32p, _i64p, _i32p]),
+        "mf_debug_fast_stream": (C.c_int, [_i32p, _i32p, C.c_int64, C.c_int32, C.c_int64, C.c_int32, C.c_int32,
+                                           C.c_int32, _i32p, _i32p, _i32p, _i64p]),
+        "mf_debug_stream_protocol": (C.c_int, [_i32p, _i32p, C.c_int64, C.c_int32, C.c_int64, C.c_int32, C.c_int32,
+                                               C.c_int32, _i64p]),
         "mf_fast_plan_window": (C.c_int, [C.c_int32, _i32p]),
         "mf_fast_kernel_name": (C.c_char_p, [C.c_int32]),
         "mf_get_params": (C.c_int, [C.c_void_p, C.POINTER(mf_params)]),
