@@ -718,7 +718,9 @@ void fast_superstep(mf_ctx* ctx, Shard& s, int64_t superstep, double eta) {
     }
     ctx->stats.kernel_launches += ctx->G_fast;
   }
-  launch_split_join(s.stream, s.st_split.as<SplitItem>() + sp0, nsplit, s.itf.as<float>(), ctx->P.num_factors);
+  static const bool keep_join = [] { const char* v = std::getenv("MFHIP_SPLIT_JOIN"); return v && std::string(v) == "keep"; }();
+  if (!keep_join)  // MFHIP_SPLIT_JOIN=keep: the item keeps replica 0's chain (the others are dropped)
+    launch_split_join(s.stream, s.st_split.as<SplitItem>() + sp0, nsplit, s.itf.as<float>(), ctx->P.num_factors);
   MF_HIP(hipGetLastError());
   ctx->stats.updates += ups;
   if (!s.sm_bytes.empty()) ctx->stats.moved_bytes += s.sm_bytes[smod];
