@@ -436,6 +436,8 @@ struct PhaseTick {
   }
 };
 
+// one rating of a block while its fast plan is built: index in the block, local user, virtual item
+struct PlanEnt { uint32_t x, ul, vil; float r; };
 inline uint32_t mix32(uint64_t x) {
   x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;
   return static_cast<uint32_t>(x);
@@ -472,9 +474,6 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
   for (int64_t b = 0; b < nb2; ++b)
     if (rb.size(b) > 0) blocks.push_back(b);
   const int64_t nblk = static_cast<int64_t>(blocks.size());
-  std::vector<std::vector<FastRec>> outs(nblk);
-  std::vector<std::vector<int64_t>> srcs(nblk);
-  std::vector<std::vector<int32_t>> offs(nblk);
   std::vector<int64_t> pads(nblk, 0);
   // hot-item replicas: per block, the items with more than split_run ratings and their R
   std::vector<std::vector<std::pair<uint32_t, int32_t>>> hot(nblk);
@@ -509,8 +508,20 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
     fp.scratch_rows = cursor;
   }
   for (auto& x : g_fp_times.ns) x = 0;
+  // Phase 1, per block: virtual items, LPT groups, cell-major order and the spreading of
+  // repeated users.  Its result (the block's entries in final cell order, as flat arrays) feeds
+  // phase 2, which emits cells in independent chunks.
+  struct BlockWork {
+    int64_t len = 0, nu = 0, nv = 0, ub = 0, GG = 0, T = 0;
+    std::vector<int64_t> cstart;   // GG + 1 cell starts in the arrays below
+    std::vector<PlanEnt> e;        // the block's ratings in cell order
+    std::vector<uint32_t> vrow;    // virtual item -> physical row
+    std::vector<float> regu, regi; // lambda / omega (f32) per local user / virtual item
+  };
+  std::vector<BlockWork> work(nblk);
   parallel_tasks(nblk, [&](int64_t bx) {
     PhaseTick tick;
+    BlockWork& W = work[bx];
     const int64_t b = blocks[bx];
     const int32_t G = fp.Gb[b];
     const int64_t T = static_cast<int64_t>(K) * G;  // sub-steps = user groups
@@ -550,72 +561,128 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
         vil[x] = r == 0 ? il : static_cast<uint32_t>(vbase[h] + r - 1);
       }
     }
+    std::vector<uint32_t> ulx(len);  // local user of every rating (x order)
+    for (int64_t x = 0; x < len; ++x) ulx[x] = rb.urow[s + x] - static_cast<uint32_t>(ub);
     std::vector<int64_t> lu(nu, 0), li(nv, 0);
-    for (int64_t x = 0; x < len; ++x) { lu[rb.urow[s + x] - ub]++; li[vil[x]]++; }
+    for (int64_t x = 0; x < len; ++x) { lu[ulx[x]]++; li[vil[x]]++; }
     std::vector<int32_t> gu, gi;
     lpt_groups(lu, static_cast<int32_t>(T), gu);
     lpt_groups(li, G, gi);
     tick.lap(0);
-    // Cell-major order: counting sort by cell (stable in x), then (item, tie, x) inside a cell --
-    // the order of sorting the whole block by (cell << 40 | item << 16 | tie, x).
-    std::vector<std::pair<uint64_t, int64_t>> key(len);
+    // Cell-major order (cell, item, x): two stable counting sorts, by item and then by cell.  The
+    // spreading below depends only on each user's ratings of a run in x order, so this is the
+    // plan of sorting the block by (cell, item, per-user hash, x).  The entries are gathered into
+    // flat arrays in that order, so everything after reads them sequentially.
+    W.cstart.assign(GG + 1, 0);
+    std::vector<int64_t>& cstart = W.cstart;
+    std::vector<PlanEnt>& E = W.e;
+    E.resize(len);
     {
       std::vector<int32_t> cell_of(len);
-      std::vector<int64_t> cstart(GG + 1, 0);
       for (int64_t x = 0; x < len; ++x) {
-        const uint32_t ul = rb.urow[s + x] - static_cast<uint32_t>(ub);
-        const int32_t g = gi[vil[x]], h = gu[ul];
-        const int64_t t = ((h - static_cast<int64_t>(K) * g) % T + T) % T;
+        const int32_t g = gi[vil[x]], h = gu[ulx[x]];
+        const int64_t d = h - static_cast<int64_t>(K) * g;  // in (-T, T): h < T, K*g < K*G = T
+        const int64_t t = d < 0 ? d + T : d;
         cell_of[x] = static_cast<int32_t>(gmajor ? g * T + t : t * G + g);
         cstart[cell_of[x] + 1]++;
       }
       for (int64_t c = 0; c < GG; ++c) cstart[c + 1] += cstart[c];
       std::vector<int64_t> cur(cstart.begin(), cstart.end() - 1);
-      for (int64_t x = 0; x < len; ++x) {
-        const uint64_t cell = static_cast<uint64_t>(cell_of[x]);
-        const uint64_t tie = mix32(order_seed ^ (static_cast<uint64_t>(rb.urow[s + x]) << 20)) & 0xFFFFu;
-        key[cur[cell]++] = {(cell << 40) | (static_cast<uint64_t>(vil[x]) << 16) | tie, x};
+      for (int64_t x = 0; x < len; ++x)
+        E[cur[cell_of[x]]++] = PlanEnt{static_cast<uint32_t>(x), ulx[x], vil[x], static_cast<float>(rb.r[s + x])};
+      // inside a cell: by item, x order kept (entries arrive in x order).  A cell's items all
+      // belong to its item group, so this is a counting sort over the group's items, ranked by id.
+      std::vector<int32_t> irank(nv), gsize(G, 0);
+      for (int64_t v = 0; v < nv; ++v) irank[v] = gsize[gi[v]]++;
+      const int32_t gmax = *std::max_element(gsize.begin(), gsize.end());
+      std::vector<int32_t> bucket(gmax + 1);
+      std::vector<PlanEnt> tmp;
+      for (int64_t c = 0; c < GG; ++c) {
+        const int64_t c0 = cstart[c], m = cstart[c + 1] - c0;
+        if (m < 2) continue;
+        const int32_t g = static_cast<int32_t>(gmajor ? c / T : c % G), ng = gsize[g];
+        std::fill(bucket.begin(), bucket.begin() + ng + 1, 0);
+        for (int64_t y = c0; y < c0 + m; ++y) bucket[irank[E[y].vil] + 1]++;
+        for (int32_t r = 0; r < ng; ++r) bucket[r + 1] += bucket[r];
+        tmp.assign(E.begin() + c0, E.begin() + c0 + m);
+        for (const PlanEnt& e : tmp) E[c0 + bucket[irank[e.vil]]++] = e;
       }
-      for (int64_t c = 0; c < GG; ++c)
-        if (cstart[c + 1] - cstart[c] > 1) std::sort(key.begin() + cstart[c], key.begin() + cstart[c + 1]);
     }
     tick.lap(1);
     // Repeated (user, item) ratings (frequent in Zipf-distributed data: a heavy user rates a hot
     // item dozens of times) would sit next to each other and force no-op halves into the pair
     // steps (a pair cannot hold one user twice).  Spread them: inside an item run, the m
     // ratings of one user go to the fractional positions (o + h_u) / m, o = 0..m-1, h_u a
-    // per-user hash in [0, 1) -- evenly over the whole run, interleaved with everyone else.
-    // Runs are contiguous in key order, so each run is re-sorted on its own by (position, x).
+    // per-user hash in [0, 1) -- evenly over the whole run, interleaved with everyone else;
+    // ties by a second per-user hash, then x.
     {
-      struct K { uint64_t pos; int64_t x; };
-      std::vector<K> k2;
+      struct K2 { uint64_t pos; PlanEnt e; };
+      std::vector<K2> k2;
       std::vector<uint32_t> ucnt(nu, 0), unext(nu, 0);  // per local user in the current run
-      for (int64_t y0 = 0; y0 < len;) {
-        const uint64_t run = key[y0].first & ~0xFFFFull;  // cell and item
-        int64_t y1 = y0;
-        while (y1 < len && (key[y1].first & ~0xFFFFull) == run) ucnt[rb.urow[s + key[y1].second] - ub]++, ++y1;
-        if (y1 - y0 > 1) {
-          k2.resize(y1 - y0);
-          for (int64_t y = y0; y < y1; ++y) {
-            const uint32_t urow = rb.urow[s + key[y].second];
-            const uint32_t ul = urow - static_cast<uint32_t>(ub);
-            const double h = static_cast<double>(mix32(order_seed * 0x2545F4914F6CDD1DULL ^ urow)) * (1.0 / 4294967296.0);
-            const double frac = (unext[ul]++ + h) / ucnt[ul];
-            k2[y - y0] = K{(static_cast<uint64_t>(frac * 16777216.0) << 16) | (key[y].first & 0xFFFFull), key[y].second};
+      for (int64_t c = 0; c < GG; ++c)
+        for (int64_t y0 = cstart[c], ye = cstart[c + 1]; y0 < ye;) {
+          const uint32_t v0 = E[y0].vil;
+          int64_t y1 = y0;
+          while (y1 < ye && E[y1].vil == v0) ucnt[E[y1].ul]++, ++y1;
+          if (y1 - y0 > 1) {
+            k2.resize(y1 - y0);
+            for (int64_t y = y0; y < y1; ++y) {
+              const uint32_t ul = E[y].ul;
+              const uint32_t urow = ul + static_cast<uint32_t>(ub);
+              const double h = static_cast<double>(mix32(order_seed * 0x2545F4914F6CDD1DULL ^ urow)) * (1.0 / 4294967296.0);
+              const double frac = (unext[ul]++ + h) / ucnt[ul];
+              const uint64_t tie = mix32(order_seed ^ (static_cast<uint64_t>(urow) << 20)) & 0xFFFFu;
+              k2[y - y0] = K2{(static_cast<uint64_t>(frac * 16777216.0) << 16) | tie, E[y]};
+            }
+            std::sort(k2.begin(), k2.end(), [](const K2& a2, const K2& b2) { return a2.pos != b2.pos ? a2.pos < b2.pos : a2.e.x < b2.e.x; });
+            for (int64_t y = y0; y < y1; ++y) E[y] = k2[y - y0].e;
           }
-          std::sort(k2.begin(), k2.end(), [](const K& a, const K& b) { return a.pos != b.pos ? a.pos < b.pos : a.x < b.x; });
-          for (int64_t y = y0; y < y1; ++y) key[y] = {run, k2[y - y0].x};
-        } else {
-          key[y0].first = run;
+          for (int64_t y = y0; y < y1; ++y) ucnt[E[y].ul] = unext[E[y].ul] = 0;
+          y0 = y1;
         }
-        for (int64_t y = y0; y < y1; ++y) {
-          const uint32_t ul = rb.urow[s + key[y].second] - static_cast<uint32_t>(ub);
-          ucnt[ul] = unext[ul] = 0;
-        }
-        y0 = y1;
-      }
     }
+    W.regu.resize(nu);
+    W.regi.resize(nv);
+    for (int64_t ul = 0; ul < nu; ++ul) W.regu[ul] = static_cast<float>(lambda / static_cast<double>(U.omega[ub + ul]));
+    for (int64_t il = 0; il < nv; ++il) W.regi[il] = static_cast<float>(lambda / static_cast<double>(I.omega[vreal[il]]));
+    W.vrow = std::move(vrow);
+    W.len = len; W.nu = nu; W.nv = nv; W.ub = ub; W.GG = GG; W.T = T;
     tick.lap(2);
+  });
+  // Phase 2: emit.  Streams (a cell, or with gmajor one wave's K*G cells) are independent, so a
+  // block's cells are cut into chunks of whole streams of about kChunk entries, emitted in
+  // parallel and concatenated in cell order.
+  struct Chunk2 { int64_t bx, c0, c1; std::vector<FastRec> out; std::vector<int64_t> src; std::vector<int32_t> off; int64_t pads = 0; };
+  std::vector<Chunk2> chunks;
+  {
+    constexpr int64_t kChunk = 1 << 17;
+    for (int64_t bx = 0; bx < nblk; ++bx) {
+      const BlockWork& W = work[bx];
+      const int64_t per = fp.gmajor ? W.T : 1;  // cells per stream
+      int64_t c0 = 0;
+      for (int64_t c = per; c <= W.GG; c += per)
+        if (c == W.GG || W.cstart[c] - W.cstart[c0] >= kChunk) {
+          chunks.push_back(Chunk2{bx, c0, c, {}, {}, {}, 0});
+          c0 = c;
+        }
+    }
+  }
+  // largest first, so the tail of the task list is short
+  std::vector<int64_t> corder(chunks.size());
+  std::iota(corder.begin(), corder.end(), 0);
+  std::stable_sort(corder.begin(), corder.end(), [&](int64_t a2, int64_t b2) {
+    const BlockWork &A = work[chunks[a2].bx], &B = work[chunks[b2].bx];
+    return A.cstart[chunks[a2].c1] - A.cstart[chunks[a2].c0] > B.cstart[chunks[b2].c1] - B.cstart[chunks[b2].c0];
+  });
+  parallel_tasks(static_cast<int64_t>(chunks.size()), [&](int64_t cx) {
+    PhaseTick tick;
+    Chunk2& ck = chunks[corder[cx]];
+    const BlockWork& W = work[ck.bx];
+    const int64_t b = blocks[ck.bx];
+    const int64_t s = rb.start[b];
+    const int32_t G = fp.Gb[b];
+    const int64_t T = W.T;
+    const uint32_t ub = static_cast<uint32_t>(W.ub);
     // Emit each cell as a sequence the kernel can run with a D-deep prefetch ring: every user
     // and every item row recurs either at the next position (the kernel forwards it in
     // registers: item runs and user runs) or at least kHazardWindow positions later (its
@@ -623,31 +690,37 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
     // item run, or the current user run when that user has more pending ratings than the
     // item; otherwise start from the item with the most pending ratings whose row and some
     // pending user row are both free; only when nothing qualifies emit a no-op record (zero
-    // user row, current item).  last_*[x] = (cell, position) of the row's latest emission.
+    // user row, current item).  last_*[x] = (stream, position) of the row's latest emission.
     // Groups are flat: an item group is a contiguous range of the cell's entries, a user group a
     // range of a per-cell CSR list (entries in cell order).
-    std::vector<FastRec>& out = outs[bx];
-    std::vector<int64_t>& src = srcs[bx];
-    std::vector<int32_t>& off = offs[bx];
-    out.reserve(len + len / 8 + 16);
-    if (rec_src) src.reserve(len + len / 8 + 16);
-    off.assign(GG + 1, 0);
-    std::vector<std::pair<int64_t, int64_t>> last_u(nu, {-1, 0}), last_i(nv, {-1, 0});
-    std::vector<std::pair<int64_t, int32_t>> uslot(nu, {-1, 0});
-    struct Ent { uint32_t ul, il; int32_t ug, ig; int64_t j; };
+    (void)G;
+    std::vector<FastRec>& out = ck.out;
+    std::vector<int64_t>& src = ck.src;
+    std::vector<int32_t>& off = ck.off;
+    const int64_t n_in = W.cstart[ck.c1] - W.cstart[ck.c0];
+    out.reserve(n_in + n_in / 8 + 16);
+    if (rec_src) src.reserve(n_in + n_in / 8 + 16);
+    off.assign(ck.c1 - ck.c0, 0);  // end of each cell, relative to the chunk
+    struct Last { int32_t sid, pos; };
+    // a stream that is one cell keeps its state per cell-local user / item slot (small, hot
+    // arrays); streams of several cells (gmajor) index it by local user / virtual item
+    const bool local = !gmajor;
+    std::vector<Last> last_u(local ? 0 : W.nu, Last{-1, 0}), last_i(local ? 0 : W.nv, Last{-1, 0});
+    std::vector<std::pair<int32_t, int32_t>> uslot(W.nu, {-1, 0});
+    struct Ent { uint32_t ul, il; int32_t ug, ig; int64_t y; };
     struct Grp { int32_t beg = 0, end = 0, head = 0, left = 0; uint32_t row = 0; };  // [beg, end) of its list
     std::vector<Ent> ents;
     std::vector<Grp> igs, ugs;
     std::vector<int32_t> ulist, ufill;  // user groups' entry lists (CSR over ugs)
     std::vector<uint8_t> taken;
     std::vector<int32_t> iorder;
-    int64_t x = 0;
     // a stream (sid) is one cell, or with gmajor one wave's K*G cells in order: positions and the
     // window count along the stream, and the last item of a cell is carried into the next one
-    int64_t cur_sid = -1, stream_begin = 0;
+    int32_t cur_sid = -1;
+    int64_t stream_begin = 0;
     uint32_t carry_il = UINT32_MAX, prev_irow = 0;
-    for (int64_t c = 0; c < GG; ++c) {
-      const int64_t sid = gmajor ? c / T : c;
+    for (int64_t c = ck.c0; c < ck.c1; ++c) {
+      const int32_t sid = static_cast<int32_t>(gmajor ? c / T : c);
       if (sid != cur_sid) {
         cur_sid = sid;
         stream_begin = static_cast<int64_t>(out.size());
@@ -657,9 +730,8 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
       ents.clear();
       igs.clear();
       ugs.clear();
-      while (x < len && static_cast<int64_t>(key[x].first >> 40) == c) {
-        const int64_t j = s + key[x].second;
-        const uint32_t il = vil[key[x].second], ul = rb.urow[j] - static_cast<uint32_t>(ub);
+      for (int64_t y = W.cstart[c]; y < W.cstart[c + 1]; ++y) {
+        const uint32_t il = W.e[y].vil, ul = W.e[y].ul;
         const int32_t e = static_cast<int32_t>(ents.size());
         if (igs.empty() || ents.back().il != il) {
           igs.emplace_back();
@@ -667,13 +739,16 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
           igs.back().beg = igs.back().head = e;
         }
         auto& us = uslot[ul];
-        if (us.first != c) { us = {c, static_cast<int32_t>(ugs.size())}; ugs.emplace_back(); }
-        ents.push_back(Ent{ul, il, us.second, static_cast<int32_t>(igs.size()) - 1, j});
+        if (us.first != c) { us = {static_cast<int32_t>(c), static_cast<int32_t>(ugs.size())}; ugs.emplace_back(); }
+        ents.push_back(Ent{ul, il, us.second, static_cast<int32_t>(igs.size()) - 1, y});
         igs.back().end = e + 1;
         ugs[us.second].end++;  // count for now
-        ++x;
       }
       const int32_t m = static_cast<int32_t>(ents.size());
+      if (local) {  // slots of this cell start free
+        last_u.assign(ugs.size(), Last{-1, 0});
+        last_i.assign(igs.size(), Last{-1, 0});
+      }
       {  // user groups: counts -> CSR ranges, entries in cell order
         int32_t acc = 0;
         for (auto& g2 : ugs) { const int32_t n2 = g2.end; g2.beg = g2.head = acc; acc += n2; g2.end = acc; }
@@ -697,9 +772,10 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
           if (igs[g2].row == carry_il) { prev_ig = static_cast<int32_t>(g2); break; }
       int32_t left = m;
       while (left > 0) {
-        const int64_t pos = static_cast<int64_t>(out.size()) - stream_begin;
-        auto ufree = [&](uint32_t ul) { return last_u[ul].first != sid || pos - last_u[ul].second >= kHazardWindow; };
-        auto ifree = [&](uint32_t il) { return last_i[il].first != sid || pos - last_i[il].second >= kHazardWindow; };
+        const int32_t pos = static_cast<int32_t>(static_cast<int64_t>(out.size()) - stream_begin);
+        auto free_at = [&](const Last& L) { return L.sid != sid || pos - L.pos >= kHazardWindow; };
+        auto ufree = [&](const Ent& en) { return free_at(local ? last_u[en.ug] : last_u[en.ul]); };
+        auto ifree = [&](int32_t ig, uint32_t il) { return free_at(local ? last_i[ig] : last_i[il]); };
         // the first untaken entries of a group's list (at most 4 * window of them) that pass ok
         auto scan = [&](Grp& g2, const int32_t* list, auto ok) -> int32_t {
           while (g2.head < g2.end && taken[list ? list[g2.head] : g2.head]) ++g2.head;
@@ -714,11 +790,11 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
         };
         auto try_item = [&]() -> int32_t {  // continue the item run
           if (prev_ig < 0 || igs[prev_ig].left == 0) return -1;
-          return scan(igs[prev_ig], nullptr, [&](const Ent& en) { return en.ug == prev_ug || ufree(en.ul); });
+          return scan(igs[prev_ig], nullptr, [&](const Ent& en) { return en.ug == prev_ug || ufree(en); });
         };
         auto try_user = [&]() -> int32_t {  // continue the user run
           if (prev_ug < 0 || ugs[prev_ug].left == 0) return -1;
-          return scan(ugs[prev_ug], ulist.data(), [&](const Ent& en) { return en.ig == prev_ig || ifree(en.il); });
+          return scan(ugs[prev_ug], ulist.data(), [&](const Ent& en) { return en.ig == prev_ig || ifree(en.ig, en.il); });
         };
         const bool user_first = prev_ug >= 0 && prev_ig >= 0 && ugs[prev_ug].left > igs[prev_ig].left;
         int32_t pick = user_first ? try_user() : try_item();
@@ -730,8 +806,8 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
             Grp& g2 = igs[iorder[z]];
             if (g2.left == 0) continue;
             ++tried;
-            if (!ifree(g2.row)) continue;
-            pick = scan(g2, nullptr, [&](const Ent& en) { return ufree(en.ul); });
+            if (!ifree(iorder[z], g2.row)) continue;
+            pick = scan(g2, nullptr, [&](const Ent& en) { return ufree(en); });
             if (pick >= 0) break;
           }
         }
@@ -739,9 +815,9 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
           out.push_back(FastRec{dummy_row * row_bytes, prev_irow * row_bytes, 0.f, 0.f, 0.f, dummy_row,
                                 prev_irow | kPadBit, 0});
           if (rec_src) src.push_back(-1);
-          pads[bx]++;
-          if (prev_ig >= 0) last_i[igs[prev_ig].row] = {sid, pos};
-          else if (carry_il != UINT32_MAX) last_i[carry_il] = {sid, pos};
+          ck.pads++;
+          if (prev_ig >= 0) (local ? last_i[prev_ig] : last_i[igs[prev_ig].row]) = Last{sid, pos};
+          else if (carry_il != UINT32_MAX && !local) last_i[carry_il] = Last{sid, pos};
           prev_ug = -1;
           continue;
         }
@@ -750,44 +826,51 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
         --left;
         igs[en.ig].left--;
         ugs[en.ug].left--;
-        last_u[en.ul] = {sid, pos};
-        last_i[en.il] = {sid, pos};
+        (local ? last_u[en.ug] : last_u[en.ul]) = Last{sid, pos};
+        (local ? last_i[en.ig] : last_i[en.il]) = Last{sid, pos};
         prev_ug = en.ug;
         prev_ig = en.ig;
         carry_il = en.il;
-        const int64_t j = en.j;
-        const uint32_t urow = rb.urow[j];
-        prev_irow = vrow[en.il];
-        out.push_back(FastRec{urow * row_bytes, prev_irow * row_bytes, static_cast<float>(rb.r[j]),
-                              static_cast<float>(lambda / static_cast<double>(U.omega[urow])),
-                              static_cast<float>(lambda / static_cast<double>(I.omega[vreal[en.il]])), urow,
+        const uint32_t urow = en.ul + ub;
+        prev_irow = W.vrow[en.il];
+        out.push_back(FastRec{urow * row_bytes, prev_irow * row_bytes, W.e[en.y].r, W.regu[en.ul], W.regi[en.il], urow,
                               prev_irow, 0});
-        if (rec_src) src.push_back(j);
+        if (rec_src) src.push_back(s + W.e[en.y].x);
       }
-      off[c + 1] = static_cast<int32_t>(out.size());
+      off[c - ck.c0] = static_cast<int32_t>(out.size());
     }
     tick.lap(3);
   });
   if (std::getenv("MFHIP_TIMING"))
     for (int ph = 0; ph < 4; ++ph)
       std::fprintf(stderr, "[mfhip]   fast plan %-10s %8.3f s (thread time)\n", g_fp_times.names[ph], g_fp_times.ns[ph] * 1e-9);
+  // concatenate: chunks are in block order, and in cell order inside a block
+  std::vector<int64_t> blk_total(nblk, 0), ck_base(chunks.size());
+  for (size_t x = 0; x < chunks.size(); ++x) {
+    ck_base[x] = blk_total[chunks[x].bx];
+    blk_total[chunks[x].bx] += static_cast<int64_t>(chunks[x].out.size());
+    pads[chunks[x].bx] += chunks[x].pads;
+  }
   int64_t total = 0, cells = 0;
   for (int64_t bx = 0; bx < nblk; ++bx) {
     fp.rec_base[blocks[bx]] = total;
     fp.cell_base[blocks[bx]] = cells;
-    total += static_cast<int64_t>(outs[bx].size());
+    total += blk_total[bx];
     cells += static_cast<int64_t>(K) * fp.Gb[blocks[bx]] * fp.Gb[blocks[bx]] + 1;
     fp.pads += pads[bx];
   }
   fp.recs.resize(total);
-  fp.cell_off.resize(cells);
+  fp.cell_off.assign(cells, 0);
   if (rec_src) rec_src->resize(total);
-  parallel_tasks(nblk, [&](int64_t bx) {
-    const int64_t b = blocks[bx];
-    std::copy(outs[bx].begin(), outs[bx].end(), fp.recs.begin() + fp.rec_base[b]);
-    std::copy(offs[bx].begin(), offs[bx].end(), fp.cell_off.begin() + fp.cell_base[b]);
-    if (rec_src) std::copy(srcs[bx].begin(), srcs[bx].end(), rec_src->begin() + fp.rec_base[b]);
-    std::vector<FastRec>().swap(outs[bx]);
+  parallel_tasks(static_cast<int64_t>(chunks.size()), [&](int64_t x) {
+    Chunk2& ck = chunks[x];
+    const int64_t b = blocks[ck.bx];
+    std::copy(ck.out.begin(), ck.out.end(), fp.recs.begin() + fp.rec_base[b] + ck_base[x]);
+    if (rec_src) std::copy(ck.src.begin(), ck.src.end(), rec_src->begin() + fp.rec_base[b] + ck_base[x]);
+    for (int64_t c = ck.c0; c < ck.c1; ++c)
+      fp.cell_off[fp.cell_base[b] + c + 1] = static_cast<int32_t>(ck_base[x] + ck.off[c - ck.c0]);
+    std::vector<FastRec>().swap(ck.out);
+    std::vector<int64_t>().swap(ck.src);
   });
 }
 
@@ -863,27 +946,39 @@ void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, in
     for (int64_t x = 0; x < len; ++n) x += (x + 1 < len && f[x + 1].u != f[x].u) ? 2 : 1;
     return n;
   };
-  std::vector<std::vector<int32_t>> npair(nsub);
-  parallel_tasks(nsub, [&](int64_t x) {
-    for (const Cell& cl : subs[x]) npair[x].push_back(pairs_of(fp.recs.data() + cl.beg, cl.len));
-  });
+  // cells in wave order (sub-step / superstep major) and their sub-step; the work below runs
+  // over chunks of cells
   pp.sub_off.assign(nsub + 1, 0);
-  int64_t total = 0;
-  for (int64_t x = 0; x < nsub; ++x) {
-    pp.sub_off[x + 1] = pp.sub_off[x] + static_cast<int64_t>(subs[x].size());
+  for (int64_t x = 0; x < nsub; ++x) pp.sub_off[x + 1] = pp.sub_off[x] + static_cast<int64_t>(subs[x].size());
+  const int64_t ncells = pp.sub_off[nsub];
+  std::vector<const Cell*> cellv(ncells);
+  std::vector<int32_t> cell_sx(ncells);
+  for (int64_t x = 0; x < nsub; ++x)
     for (size_t y = 0; y < subs[x].size(); ++y) {
-      pp.waves.push_back(WaveDesc{total, npair[x][y], kWaveGeneric});
-      total += npair[x][y];
+      cellv[pp.sub_off[x] + y] = &subs[x][y];
+      cell_sx[pp.sub_off[x] + y] = static_cast<int32_t>(x);
     }
+  constexpr int64_t kCellChunk = 2048;
+  const int64_t nchunks = (ncells + kCellChunk - 1) / kCellChunk;
+  std::vector<int32_t> npair(ncells);
+  parallel_tasks(nchunks, [&](int64_t ch) {
+    for (int64_t y = ch * kCellChunk; y < std::min(ncells, (ch + 1) * kCellChunk); ++y)
+      npair[y] = pairs_of(fp.recs.data() + cellv[y]->beg, cellv[y]->len);
+  });
+  pp.waves.resize(ncells);
+  int64_t total = 0;
+  for (int64_t y = 0; y < ncells; ++y) {
+    pp.waves[y] = WaveDesc{total, npair[y], kWaveGeneric};
+    total += npair[y];
   }
   pp.recs.resize(total);
-  std::vector<int64_t> noops(nsub, 0);
-  std::vector<double> sub_bytes(nsub, 0.0);  // bytes the kernel requests for the cells of sx
+  std::vector<int64_t> cell_noops(ncells, 0);
+  std::vector<double> cell_bytes(ncells, 0.0);  // bytes the kernel requests for each cell
   const double row_bytes = 4.0 * k;
-  parallel_tasks(nsub, [&](int64_t sx) {
-    int64_t w = pp.sub_off[sx];
-    for (const Cell& cl : subs[sx]) {
-      const int64_t w_this = w++;
+  parallel_tasks(nchunks, [&](int64_t ch) {
+    for (int64_t w_this = ch * kCellChunk; w_this < std::min(ncells, (ch + 1) * kCellChunk); ++w_this) {
+      const Cell& cl = *cellv[w_this];
+      int64_t& noop = cell_noops[w_this];
       PairRec* const first = pp.recs.data() + pp.waves[w_this].base;
       PairRec* out = first;
       const FastRec* f = fp.recs.data() + cl.beg;
@@ -905,7 +1000,7 @@ void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, in
         pr.ra = a.r;
         pr.rua = a.ru;
         pr.ria = a.ri;
-        if (a_pad) noops[sx]++;
+        if (a_pad) noop++;
         pr.ib = pr.ub = pr.sb = pr.sia = kOffOOB;
         // the item row whose run may end after this step: B's if B exists, else A's
         const FastRec* tail = &a;
@@ -923,10 +1018,10 @@ void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, in
             pr.rub = b.ru;
             pr.rib = b.ri;
           } else {
-            noops[sx]++;
+            noop++;
           }
         } else {
-          noops[sx]++;
+          noop++;
         }
         pr.si = (nx >= len || item_of(f[nx]) != item_of(*tail)) ? tail->i_off : kOffOOB;
         pr.flags = flags;
@@ -981,10 +1076,14 @@ void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, in
         }
       }
       if (single && out > first) rows += 2;
-      sub_bytes[sx] += 64.0 * static_cast<double>(out - first) + row_bytes * static_cast<double>(rows);
+      cell_bytes[w_this] = 64.0 * static_cast<double>(out - first) + row_bytes * static_cast<double>(rows);
     }
   });
-  for (int64_t x = 0; x < nsub; ++x) pp.noop_halves += noops[x];
+  std::vector<double> sub_bytes(nsub, 0.0);  // per sub-step, summed in cell order
+  for (int64_t y = 0; y < ncells; ++y) {
+    pp.noop_halves += cell_noops[y];
+    sub_bytes[cell_sx[y]] += cell_bytes[y];
+  }
   pp.sm_bytes.assign(nb, 0.0);
   for (int64_t x = 0; x < nsub; ++x) pp.sm_bytes[substep_waves ? x / fp.G : x] += sub_bytes[x];
   if (g_plan_debug) {

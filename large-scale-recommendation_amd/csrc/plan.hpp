@@ -10,12 +10,28 @@
 //                     in-flight update owns its user and item row (conflict-free batching)
 #pragma once
 #include <cstdint>
+#include <memory>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "id_index.hpp"
 
 namespace mfhip {
+
+// Allocator whose resize() leaves trivially constructible elements uninitialised: the multi-GB
+// record tables are filled by parallel writers, which then also take the first-touch page faults
+// (a value-initialising resize zeroes them on one thread first).
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+  template <class U> struct rebind { using other = NoInitAlloc<U>; };
+  NoInitAlloc() = default;
+  template <class U> NoInitAlloc(const NoInitAlloc<U>&) noexcept {}
+  template <class U> void construct(U* p) noexcept { ::new (static_cast<void*>(p)) U; }
+  template <class U, class... A> void construct(U* p, A&&... a) { ::new (static_cast<void*>(p)) U(std::forward<A>(a)...); }
+};
+template <class T>
+using RecVec = std::vector<T, NoInitAlloc<T>>;
 
 struct SideLayout {
   int32_t n_blocks = 1;
@@ -175,7 +191,7 @@ struct FastPlan {
   int32_t K = 1;                       // user groups per item group: a block has G item x K*G user groups
   bool gmajor = false;                 // cell index g*(K*G) + t (stream order) instead of t*G + g
   std::vector<int32_t> Gb;             // per rating block (n*n): its rotation groups
-  std::vector<FastRec> recs;           // all rating blocks of this shard, cell-major per block
+  RecVec<FastRec> recs;                // all rating blocks of this shard, cell-major per block
   std::vector<int64_t> rec_base;       // per rating block (n*n), -1 if not on this shard
   std::vector<int32_t> cell_off;       // per included rating block: K*Gb*Gb+1 relative offsets
   std::vector<int64_t> cell_base;      // per rating block: index into cell_off (-1 if absent)
@@ -256,7 +272,7 @@ struct StreamWave {
 static_assert(sizeof(StreamWave) == 16, "StreamWave is one 16-B word");
 
 struct PairPlan {
-  std::vector<PairRec> recs;
+  RecVec<PairRec> recs;
   std::vector<WaveDesc> waves;   // one per non-empty cell (steps = pairs), every (sm, t), sm-major
   std::vector<int64_t> sub_off;  // nb*G + 1
   // Systolic tables (k_sweep_pair_sys): the waves of superstep sm are
