@@ -159,4 +159,21 @@ inline void parallel_tasks(int64_t n, const std::function<void(int64_t)>& fn, in
   for (auto& x : th) x.join();
 }
 
+// Releases large host buffers on background threads: returning a touched multi-GB allocation
+// to the OS costs seconds (page freeing), which would otherwise sit inside mf_dsgd_prepare.
+// Joined when the owner is destroyed (mf_destroy) or before the next prepare.
+struct Reaper {
+  std::vector<std::thread> th;
+  template <class V>
+  void drop(V& v) {
+    th.emplace_back([x = std::move(v)]() mutable { std::decay_t<V>().swap(x); });
+    v = std::decay_t<V>();
+  }
+  void join() {
+    for (auto& t : th) t.join();
+    th.clear();
+  }
+  ~Reaper() { join(); }
+};
+
 }  // namespace mfhip

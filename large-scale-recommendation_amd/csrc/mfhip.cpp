@@ -116,6 +116,7 @@ struct Shard {
 }  // namespace mfhip
 
 struct mf_ctx {
+  Reaper reaper;  // host plan buffers being released in the background (first member: joined last)
   mf_params P{};
   bool f64 = true;
   size_t es = 8;  // bytes per factor element
@@ -1098,6 +1099,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
   ctx->failed.clear();
   sync_all(ctx);
   PhaseClock clk;
+  ctx->reaper.join();
   ctx->nb = std::max(1, ctx->P.num_blocks);
   MF_REQUIRE(ctx->nb % ctx->G == 0, "num_blocks must be a multiple of the device count");
   ctx->c = ctx->nb / ctx->G;
@@ -1307,6 +1309,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
         s.fast_err.alloc(16 + 32 * static_cast<size_t>(max_waves));  // flag + per-slot diagnostics and wait stats
         MF_HIP(hipMemset(s.fast_err.get(), 0, s.fast_err.bytes()));
         clk.lap("stream plan + H2D");
+        ctx->reaper.drop(pp.recs);
         continue;
       }
       if (ctx->fast_pair) {
@@ -1342,6 +1345,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
           MF_HIP(hipMemset(s.fast_err.get(), 0, 16));
         }
         clk.lap("pair plan + H2D");
+        ctx->reaper.drop(pp.recs);
         if (std::getenv("MFHIP_WAVE_TRACE")) {
           const size_t n = ctx->fast_sys ? pp.sys.size() : pp.waves.size();
           s.st_trace.alloc(std::max<size_t>(n, 1) * 16);
@@ -1393,9 +1397,16 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
       s.fast_blks.alloc(blks.size() * sizeof(FastBlk));
       MF_HIP(hipMemcpy(s.fast_blks.get(), blks.data(), blks.size() * sizeof(FastBlk), hipMemcpyHostToDevice));
     }
-    ctx->rb = RatingBlocks();  // the device holds the schedule; free the host copy
+    clk.lap("device tables");
+    // the device holds the schedule; release the host copies in the background
+    ctx->reaper.drop(fp.recs);
+    ctx->reaper.drop(ctx->rb.urow);
+    ctx->reaper.drop(ctx->rb.irow);
+    ctx->reaper.drop(ctx->rb.r);
+    ctx->rb = RatingBlocks();
     ctx->rb.n_blocks = ctx->nb;
   }
+  clk.lap("release host blocks");
   ctx->superstep_done = 0;
   reset_item_loc(ctx);
   ctx->prepared = true;

@@ -519,6 +519,8 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
     std::vector<float> regu, regi; // lambda / omega (f32) per local user / virtual item
   };
   std::vector<BlockWork> work(nblk);
+  const auto wall0 = std::chrono::steady_clock::now();
+  auto wall = [&] { return std::chrono::duration<double>(std::chrono::steady_clock::now() - wall0).count(); };
   parallel_tasks(nblk, [&](int64_t bx) {
     PhaseTick tick;
     BlockWork& W = work[bx];
@@ -649,6 +651,7 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
     W.len = len; W.nu = nu; W.nv = nv; W.ub = ub; W.GG = GG; W.T = T;
     tick.lap(2);
   });
+  const double wall_p1 = wall();
   // Phase 2: emit.  Streams (a cell, or with gmajor one wave's K*G cells) are independent, so a
   // block's cells are cut into chunks of whole streams of about kChunk entries, emitted in
   // parallel and concatenated in cell order.
@@ -841,6 +844,7 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
     }
     tick.lap(3);
   });
+  const double wall_p2 = wall();
   if (std::getenv("MFHIP_TIMING"))
     for (int ph = 0; ph < 4; ++ph)
       std::fprintf(stderr, "[mfhip]   fast plan %-10s %8.3f s (thread time)\n", g_fp_times.names[ph], g_fp_times.ns[ph] * 1e-9);
@@ -872,6 +876,10 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
     std::vector<FastRec>().swap(ck.out);
     std::vector<int64_t>().swap(ck.src);
   });
+  parallel_tasks(nblk, [&](int64_t bx) { BlockWork().e.swap(work[bx].e); });  // freed in parallel
+  if (std::getenv("MFHIP_TIMING"))
+    std::fprintf(stderr, "[mfhip]   fast plan wall: blocks %.3f s, emit %.3f s, gather %.3f s (%zu emit chunks)\n", wall_p1,
+                 wall_p2 - wall_p1, wall() - wall_p2, chunks.size());
 }
 
 namespace {
