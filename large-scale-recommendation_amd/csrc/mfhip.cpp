@@ -116,7 +116,7 @@ struct Shard {
 }  // namespace mfhip
 
 struct mf_ctx {
-  Reaper reaper;  // host plan buffers being released in the background (first member: joined last)
+  mfhip::Reaper reaper;  // host plan buffers being released in the background (first member: joined last)
   mf_params P{};
   bool f64 = true;
   size_t es = 8;  // bytes per factor element
