@@ -7,6 +7,7 @@
 #include <cstdlib>
 #include <atomic>
 #include <functional>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -159,19 +160,28 @@ inline void parallel_tasks(int64_t n, const std::function<void(int64_t)>& fn, in
   for (auto& x : th) x.join();
 }
 
-// Releases large host buffers on background threads: returning a touched multi-GB allocation
+// Releases large host buffers on a background thread: returning a touched multi-GB allocation
 // to the OS costs seconds (page freeing), which would otherwise sit inside mf_dsgd_prepare.
+// drop() only takes the buffer over; release() hands everything taken to ONE thread (the unmaps
+// hold the process's mmap lock, so a second thread's stack mmap would wait behind the first).
 // Joined when the owner is destroyed (mf_destroy) or before the next prepare.
 struct Reaper {
-  std::vector<std::thread> th;
+  std::vector<std::shared_ptr<void>> held;
+  std::thread th;
   template <class V>
   void drop(V& v) {
-    th.emplace_back([x = std::move(v)]() mutable { std::decay_t<V>().swap(x); });
-    v = std::decay_t<V>();
+    using T = std::decay_t<V>;
+    held.emplace_back(new T(std::move(v)), [](void* p) { delete static_cast<T*>(p); });
+    v = T();
+  }
+  void release() {
+    join();
+    if (held.empty()) return;
+    th = std::thread([h = std::move(held)]() mutable { h.clear(); });
+    held.clear();
   }
   void join() {
-    for (auto& t : th) t.join();
-    th.clear();
+    if (th.joinable()) th.join();
   }
   ~Reaper() { join(); }
 };

@@ -129,6 +129,19 @@ __global__ void k_gather_f64(const int32_t* __restrict__ perm, const double* __r
     dst[x] = src[perm[x]];
 }
 
+// start[b] = lower_bound(keys, b) over the sorted rating-block keys, b = 0..nb2 (one thread each)
+__global__ void k_block_starts(const uint32_t* __restrict__ keys, int64_t n, int64_t nb2, int64_t* __restrict__ start) {
+  const int64_t b = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  if (b > nb2) return;
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = lo + (hi - lo) / 2;
+    if (keys[mid] < static_cast<uint32_t>(b)) lo = mid + 1;
+    else hi = mid;
+  }
+  start[b] = lo;
+}
+
 int bits_for(uint64_t maxval) {
   int b = 1;
   while (b < 64 && (maxval >> b) != 0) ++b;
@@ -291,12 +304,14 @@ void device_blocking(hipStream_t st, const int32_t* u, const int32_t* i, const d
   hipLaunchKernelGGL(k_gather_f64, dim3(grid_for(n)), dim3(kThreads), 0, st, perm.as<int32_t>(), dr.as<double>(), n,
                      gr.as<double>());
   MF_HIP(hipGetLastError());
-  std::vector<uint32_t> keys(n);
-  MF_HIP(hipMemcpyAsync(keys.data(), sorted_keys, n * 4, hipMemcpyDeviceToHost, st));
-  MF_HIP(hipStreamSynchronize(st));
   // keys are sorted: block b spans [lower_bound(b), lower_bound(b+1)); n*n (other ranks) last
-  for (int64_t b = 0; b <= nb2; ++b)
-    rb.start[b] = std::lower_bound(keys.begin(), keys.end(), static_cast<uint32_t>(b)) - keys.begin();
+  DevBuf dstart;
+  dstart.alloc(static_cast<size_t>(nb2 + 1) * 8);
+  hipLaunchKernelGGL(k_block_starts, dim3(static_cast<unsigned>((nb2 + 1 + kThreads - 1) / kThreads)), dim3(kThreads), 0, st,
+                     sorted_keys, n, nb2, dstart.as<int64_t>());
+  MF_HIP(hipGetLastError());
+  MF_HIP(hipMemcpyAsync(rb.start.data(), dstart.get(), static_cast<size_t>(nb2 + 1) * 8, hipMemcpyDeviceToHost, st));
+  MF_HIP(hipStreamSynchronize(st));
   const int64_t total = rb.start[nb2];
   rb.urow.resize(total);
   rb.irow.resize(total);

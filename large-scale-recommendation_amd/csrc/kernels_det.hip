@@ -193,7 +193,8 @@ __global__ __launch_bounds__(256) void k_predict(const int32_t* __restrict__ uro
     }
   }
   if (!partials) return;
-  // fixed-order reduction: lanes in order, then the 4 waves
+  // fixed-order reduction: an XOR butterfly over the 64 lanes (deterministic, not a sequential
+  // left fold), then the 4 waves in order
   for (int l = 1; l < 64; l <<= 1) {
     sse += __shfl_xor(sse, l);
     cnt += __shfl_xor(cnt, l);

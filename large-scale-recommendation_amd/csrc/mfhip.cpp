@@ -1230,6 +1230,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
     MF_REQUIRE(static_cast<uint64_t>(ctx->I.rows() + 1 + fp.scratch_rows) * k * 4 < (1ull << 32),
                "hot-item replica rows exceed the 32-bit item slab offsets");
     ctx->stats.pads = fp.pads;
+    ctx->reaper.drop(fp.scratch);
     clk.lap("cell plan");
     {  // priority threshold: 3x the mean non-empty cell length
       int64_t cells = 0, recs = 0;
@@ -1405,6 +1406,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
     ctx->reaper.drop(ctx->rb.r);
     ctx->rb = RatingBlocks();
     ctx->rb.n_blocks = ctx->nb;
+    ctx->reaper.release();
   }
   clk.lap("release host blocks");
   ctx->superstep_done = 0;

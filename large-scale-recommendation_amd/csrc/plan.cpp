@@ -876,7 +876,8 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
     std::vector<FastRec>().swap(ck.out);
     std::vector<int64_t>().swap(ck.src);
   });
-  parallel_tasks(nblk, [&](int64_t bx) { BlockWork().e.swap(work[bx].e); });  // freed in parallel
+  using Works = std::vector<BlockWork>;
+  fp.scratch = std::shared_ptr<void>(new Works(std::move(work)), [](void* p) { delete static_cast<Works*>(p); });
   if (std::getenv("MFHIP_TIMING"))
     std::fprintf(stderr, "[mfhip]   fast plan wall: blocks %.3f s, emit %.3f s, gather %.3f s (%zu emit chunks)\n", wall_p1,
                  wall_p2 - wall_p1, wall() - wall_p2, chunks.size());

@@ -66,9 +66,9 @@ void lookup_rows(const SideLayout& s, const int32_t* ids, int64_t n, std::vector
 struct RatingBlocks {
   int32_t n_blocks = 1;
   std::vector<int64_t> start;   // n*n + 1, block b = ub*n + ib
-  std::vector<uint32_t> urow;   // global user row
-  std::vector<uint32_t> irow;   // global item row
-  std::vector<double> r;
+  RecVec<uint32_t> urow;        // global user row
+  RecVec<uint32_t> irow;        // global item row
+  RecVec<double> r;
   std::vector<int64_t> src;     // input index per position (only when requested)
   int64_t size(int64_t b) const { return start[b + 1] - start[b]; }
 };
@@ -198,6 +198,7 @@ struct FastPlan {
   int64_t pads = 0;                    // padding records inserted
   std::vector<SplitItem> splits;       // hot-item replicas, grouped by rating block
   std::vector<int64_t> split_off;      // n*n + 1: rating block b owns splits [split_off[b], split_off[b+1])
+  std::shared_ptr<void> scratch;       // the builder's per-block working arrays (the caller may free them late)
   uint32_t scratch_rows = 0;           // scratch item rows used from scratch_base on
 };
 
