@@ -313,9 +313,9 @@ void device_blocking(hipStream_t st, const int32_t* u, const int32_t* i, const d
   MF_HIP(hipMemcpyAsync(rb.start.data(), dstart.get(), static_cast<size_t>(nb2 + 1) * 8, hipMemcpyDeviceToHost, st));
   MF_HIP(hipStreamSynchronize(st));
   const int64_t total = rb.start[nb2];
-  rb.urow.resize(total);
-  rb.irow.resize(total);
-  rb.r.resize(total);
+  resize_huge(rb.urow, total);
+  resize_huge(rb.irow, total);
+  resize_huge(rb.r, total);
   if (total > 0) {
     MF_HIP(hipMemcpyAsync(rb.urow.data(), gu.get(), total * 4, hipMemcpyDeviceToHost, st));
     MF_HIP(hipMemcpyAsync(rb.irow.data(), gi.get(), total * 4, hipMemcpyDeviceToHost, st));

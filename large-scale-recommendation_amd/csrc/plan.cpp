@@ -1,6 +1,8 @@
 // plan.cpp -- host-side DSGD blocking and device schedules (see plan.hpp).
 #include "plan.hpp"
 
+#include <sys/mman.h>
+
 #include <algorithm>
 #include <array>
 #include <chrono>
@@ -398,6 +400,13 @@ int32_t choose_groups(int64_t avg_block_ratings, int32_t blocks_per_device, int3
   return static_cast<int32_t>(std::clamp<int64_t>(g, 4, 1024));
 }
 
+void hugepage_hint(void* p, size_t bytes) {
+  constexpr uintptr_t kHuge = uintptr_t{1} << 21;
+  const uintptr_t a = (reinterpret_cast<uintptr_t>(p) + kHuge - 1) & ~(kHuge - 1);
+  const uintptr_t e = (reinterpret_cast<uintptr_t>(p) + bytes) & ~(kHuge - 1);
+  if (e > a) madvise(reinterpret_cast<void*>(a), e - a, MADV_HUGEPAGE);
+}
+
 namespace {
 // Longest-processing-time greedy: heaviest rows first into the least-loaded group.
 void lpt_groups(const std::vector<int64_t>& load, int32_t G, std::vector<int32_t>& group) {
@@ -514,7 +523,7 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
   struct BlockWork {
     int64_t len = 0, nu = 0, nv = 0, ub = 0, GG = 0, T = 0;
     std::vector<int64_t> cstart;   // GG + 1 cell starts in the arrays below
-    std::vector<PlanEnt> e;        // the block's ratings in cell order
+    RecVec<PlanEnt> e;             // the block's ratings in cell order
     std::vector<uint32_t> vrow;    // virtual item -> physical row
     std::vector<float> regu, regi; // lambda / omega (f32) per local user / virtual item
   };
@@ -577,8 +586,8 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
     // flat arrays in that order, so everything after reads them sequentially.
     W.cstart.assign(GG + 1, 0);
     std::vector<int64_t>& cstart = W.cstart;
-    std::vector<PlanEnt>& E = W.e;
-    E.resize(len);
+    RecVec<PlanEnt>& E = W.e;
+    resize_huge(E, len);
     {
       std::vector<int32_t> cell_of(len);
       for (int64_t x = 0; x < len; ++x) {
@@ -863,7 +872,7 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
     cells += static_cast<int64_t>(K) * fp.Gb[blocks[bx]] * fp.Gb[blocks[bx]] + 1;
     fp.pads += pads[bx];
   }
-  fp.recs.resize(total);
+  resize_huge(fp.recs, total);
   fp.cell_off.assign(cells, 0);
   if (rec_src) rec_src->resize(total);
   parallel_tasks(static_cast<int64_t>(chunks.size()), [&](int64_t x) {
@@ -980,7 +989,7 @@ void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, in
     pp.waves[y] = WaveDesc{total, npair[y], kWaveGeneric};
     total += npair[y];
   }
-  pp.recs.resize(total);
+  resize_huge(pp.recs, total);
   std::vector<int64_t> cell_noops(ncells, 0);
   std::vector<double> cell_bytes(ncells, 0.0);  // bytes the kernel requests for each cell
   const double row_bytes = 4.0 * k;
@@ -1211,7 +1220,7 @@ void build_stream_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, 
     total += np;
     pp.max_pairs = std::max<int64_t>(pp.max_pairs, np);
   }
-  pp.recs.resize(total);
+  resize_huge(pp.recs, total);
   std::vector<int64_t> noops(nw, 0);
   std::vector<double> wbytes(nw, 0.0);
   const double row_bytes = 4.0 * k;

@@ -33,6 +33,15 @@ struct NoInitAlloc : std::allocator<T> {
 template <class T>
 using RecVec = std::vector<T, NoInitAlloc<T>>;
 
+// Asks for transparent huge pages on a large, not yet touched buffer (first-touch faults then come
+// 2 MB at a time instead of 4 KB: seconds on the multi-GB record tables).  Only a hint.
+void hugepage_hint(void* p, size_t bytes);
+template <class V>
+void resize_huge(V& v, size_t n) {
+  v.resize(n);
+  hugepage_hint(v.data(), n * sizeof(typename V::value_type));
+}
+
 struct SideLayout {
   int32_t n_blocks = 1;
   std::vector<int32_t> row_id;       // row -> id; rows grouped by block, ids ascending in a block
