@@ -1222,6 +1222,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
       ctx->fast_sys = fits;
       if (!fits) block_groups.clear();
     }
+    clk.lap("schedule model (groups)");
     build_fast_plan(fp, ctx->rb, ctx->U, ctx->I, ctx->G_fast, k, ctx->P.lambda,
                     static_cast<uint64_t>(ctx->P.seed) * 0x9E3779B97F4A7C15ULL + 1, dummy, nullptr,
                     ctx->fast_stream ? 2 * ctx->stream_ring : ctx->fast_pair ? 2 * kPairRing : kHazardWindow,
