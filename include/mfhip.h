@@ -268,6 +268,11 @@ int mf_debug_stream_protocol(const int32_t* users, const int32_t* items, int64_t
    (DSGDforMF.scala:611-619) over ranks. */
 int mf_debug_ring_schedule(int32_t rank, int32_t world, int32_t n_blocks, int64_t superstep, int32_t* out_blk,
                            int32_t* in_blk, int32_t* dst, int32_t* src);
+/* mf_debug_plan_digest: after mf_dsgd_prepare of a fast-mode fit on one shard, an FNV-1a digest
+   of the device schedule -- the pair records, the wave table and (systolic) the per-wave cell
+   tables -- and the pair-record count: out[0] = digest, out[1] = records.  Compares the device-
+   built plan (kernels_plan.hip) with the host-built one (MFHIP_DEVICE_PLAN=0). */
+int mf_debug_plan_digest(mf_ctx* ctx, uint64_t out[2]);
 /* The plan window (records between two uses of a row inside a cell unless adjacent) the fast
    sweep uses at rank k: the prefetch distance of the kernel selected for k. */
 int mf_fast_plan_window(int32_t k, int32_t* window_out);

@@ -118,6 +118,15 @@ void device_blocking(hipStream_t st, const int32_t* u, const int32_t* i, const d
                      int64_t seed, int32_t ub_lo, int32_t ub_hi, bool sort_ui, SideLayout& U, SideLayout& I,
                      RatingBlocks& rb);
 
+// The fast pair schedule's per-cell work on the device (kernels_plan.hip): the greedy emission of
+// every cell of `work` (build_fast_plan's phase-1 output, blocks in ascending order) and the pair
+// records of every wave, bitwise the host build_fast_plan + build_pair_plan.  Fills fp's cell /
+// record offsets and pads, pp's tables and stats (pp.recs stays empty) and d_pairs (device).
+class DevBuf;
+void device_pair_schedule(hipStream_t st, std::vector<FastBlockWork>& work, FastPlan& fp, int32_t nb, int32_t c,
+                          int32_t shard, int32_t k, uint32_t dummy_row, int32_t window, bool substep_waves,
+                          PairPlan& pp, DevBuf& d_pairs);
+
 // Initial factor rows on the device (DSGDforMF.scala:548-549, MatrixFactorization.scala:278-280):
 // row x, factor f = the f-th nextDouble of new Random(ids[x] ^ seed) (xor_seed) or of
 // new Random(ids[x]).  One thread per element: the JVM LCG state after m steps is

@@ -87,6 +87,7 @@ struct Shard {
   DevBuf fast_recs, fast_cells, fast_blks;
   DevBuf fast_prog, fast_err;  // persistent sweep: progress words + timeout flag
   DevBuf st_recs, st_waves;    // stream schedule (kernels_stream.hip)
+  int64_t st_nrecs = 0;        // pair records in st_recs
   std::vector<int64_t> st_sub_off;
   std::vector<WaveDesc> st_waves_host;  // kept only when tracing
   DevBuf st_sys, st_sysw;               // systolic pair tables (PairPlan::sys, sys_waves)
@@ -1223,16 +1224,33 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
       if (!fits) block_groups.clear();
     }
     clk.lap("schedule model (groups)");
+    // the per-cell emission and the pair records on the device (kernels_plan.hip) for the default
+    // systolic pair sweep of one shard; MFHIP_DEVICE_PLAN=0 keeps them on the host
+    const char* dpv = std::getenv("MFHIP_DEVICE_PLAN");
+    const bool dev_plan = ctx->fast_pair && ctx->fast_sys && !ctx->fast_stream && ctx->P.fast_item_split == 0 &&
+                          ctx->shards.size() == 1 && !(dpv && std::string(dpv) == "0");
+    std::vector<FastBlockWork> entries;
     build_fast_plan(fp, ctx->rb, ctx->U, ctx->I, ctx->G_fast, k, ctx->P.lambda,
                     static_cast<uint64_t>(ctx->P.seed) * 0x9E3779B97F4A7C15ULL + 1, dummy, nullptr,
                     ctx->fast_stream ? 2 * ctx->stream_ring : ctx->fast_pair ? 2 * kPairRing : kHazardWindow,
                     block_groups.empty() ? nullptr : &block_groups, ctx->P.fast_item_split,
-                    static_cast<uint32_t>(ctx->I.rows() + 1), ctx->fast_stream ? stream_K : 1, ctx->fast_stream);
+                    static_cast<uint32_t>(ctx->I.rows() + 1), ctx->fast_stream ? stream_K : 1, ctx->fast_stream,
+                    dev_plan ? &entries : nullptr);
     MF_REQUIRE(static_cast<uint64_t>(ctx->I.rows() + 1 + fp.scratch_rows) * k * 4 < (1ull << 32),
                "hot-item replica rows exceed the 32-bit item slab offsets");
+    PairPlan dev_pp;
+    DevBuf dev_pairs;
+    if (dev_plan) {
+      Shard& s0 = ctx->shards[0];
+      DeviceGuard g(s0.device);
+      clk.lap("cell order (host)");
+      device_pair_schedule(s0.stream, entries, fp, ctx->nb, ctx->c, s0.index, k, dummy, 2 * kPairRing, false, dev_pp,
+                           dev_pairs);
+      ctx->reaper.drop(entries);
+    }
     ctx->stats.pads = fp.pads;
     ctx->reaper.drop(fp.scratch);
-    clk.lap("cell plan");
+    clk.lap(dev_plan ? "cell emission + pairs (device)" : "cell plan");
     {  // priority threshold: 3x the mean non-empty cell length
       int64_t cells = 0, recs = 0;
       for (int64_t b = 0; b < nb2; ++b)
@@ -1316,10 +1334,17 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
       }
       if (ctx->fast_pair) {
         PairPlan pp;
-        build_pair_plan(pp, fp, ctx->nb, ctx->c, s.index, k, !ctx->fast_sys);
+        if (dev_plan) {
+          pp = std::move(dev_pp);
+          s.st_recs = std::move(dev_pairs);
+        } else {
+          build_pair_plan(pp, fp, ctx->nb, ctx->c, s.index, k, !ctx->fast_sys);
+        }
         ctx->stats.pads += pp.noop_halves - fp.pads;  // run padding on top of the planner's
         s.sm_bytes = pp.sm_bytes;
-        s.st_recs.alloc(std::max<size_t>(pp.recs.size(), 1) * sizeof(PairRec));
+        s.st_nrecs = 0;
+        for (const WaveDesc& wd : pp.waves) s.st_nrecs = std::max<int64_t>(s.st_nrecs, wd.base + wd.steps);
+        if (!dev_plan) s.st_recs.alloc(std::max<size_t>(pp.recs.size(), 1) * sizeof(PairRec));
         s.st_waves.alloc(std::max<size_t>(pp.waves.size(), 1) * sizeof(WaveDesc));
         if (!pp.recs.empty())
           MF_HIP(hipMemcpy(s.st_recs.get(), pp.recs.data(), pp.recs.size() * sizeof(PairRec), hipMemcpyHostToDevice));
@@ -2261,6 +2286,31 @@ const char* mf_fast_kernel_name(int32_t k) {
     case FastKernel::kPersistent: return "k_fast_superstep";
     default: return "k_fast_substep";
   }
+}
+
+int mf_debug_plan_digest(mf_ctx* ctx, uint64_t out[2]) {
+  return guarded([&] {
+    MF_REQUIRE(ctx && out, "null argument");
+    MF_REQUIRE(ctx->prepared && !ctx->f64 && ctx->fast_pair && ctx->shards.size() == 1,
+               "mf_debug_plan_digest needs a prepared fast-mode pair fit on one shard");
+    sync_all(ctx);
+    Shard& s = ctx->shards[0];
+    DeviceGuard g(s.device);
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](const DevBuf& d, size_t bytes) {
+      std::vector<unsigned char> v(bytes);
+      if (bytes) MF_HIP(hipMemcpy(v.data(), d.get(), bytes, hipMemcpyDeviceToHost));
+      for (unsigned char c : v) { h ^= c; h *= 1099511628211ull; }
+    };
+    mix(s.st_recs, static_cast<size_t>(s.st_nrecs) * sizeof(PairRec));
+    mix(s.st_waves, s.st_sub_off.empty() ? 0 : static_cast<size_t>(s.st_sub_off.back()) * sizeof(WaveDesc));
+    if (ctx->fast_sys) {
+      mix(s.st_sys, s.st_sys.bytes());
+      mix(s.st_sysw, s.st_sysw.bytes());
+    }
+    out[0] = h;
+    out[1] = static_cast<uint64_t>(s.st_nrecs);
+  });
 }
 
 int mf_debug_ring_schedule(int32_t rank, int32_t world, int32_t n_blocks, int64_t superstep, int32_t* out_blk,

@@ -445,8 +445,6 @@ struct PhaseTick {
   }
 };
 
-// one rating of a block while its fast plan is built: index in the block, local user, virtual item
-struct PlanEnt { uint32_t x, ul, vil; float r; };
 inline uint32_t mix32(uint64_t x) {
   x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;
   return static_cast<uint32_t>(x);
@@ -462,7 +460,8 @@ inline uint32_t mix32(uint64_t x) {
 void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, const SideLayout& I,
                      int32_t G0, int32_t k, double lambda, uint64_t order_seed, uint32_t dummy_row,
                      std::vector<int64_t>* rec_src, int32_t window, const std::vector<int32_t>* block_groups,
-                     int32_t split_run, uint32_t scratch_base, int32_t ustride, bool gmajor) {
+                     int32_t split_run, uint32_t scratch_base, int32_t ustride, bool gmajor,
+                     std::vector<FastBlockWork>* entries_out) {
   const int64_t kHazardWindow = window;  // shadows the default for this plan
   const int32_t K = std::max(ustride, 1);
   const uint32_t row_bytes = static_cast<uint32_t>(k) * 4u;
@@ -520,13 +519,7 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
   // Phase 1, per block: virtual items, LPT groups, cell-major order and the spreading of
   // repeated users.  Its result (the block's entries in final cell order, as flat arrays) feeds
   // phase 2, which emits cells in independent chunks.
-  struct BlockWork {
-    int64_t len = 0, nu = 0, nv = 0, ub = 0, GG = 0, T = 0;
-    std::vector<int64_t> cstart;   // GG + 1 cell starts in the arrays below
-    RecVec<PlanEnt> e;             // the block's ratings in cell order
-    std::vector<uint32_t> vrow;    // virtual item -> physical row
-    std::vector<float> regu, regi; // lambda / omega (f32) per local user / virtual item
-  };
+  using BlockWork = FastBlockWork;
   std::vector<BlockWork> work(nblk);
   const auto wall0 = std::chrono::steady_clock::now();
   auto wall = [&] { return std::chrono::duration<double>(std::chrono::steady_clock::now() - wall0).count(); };
@@ -657,10 +650,16 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
     for (int64_t ul = 0; ul < nu; ++ul) W.regu[ul] = static_cast<float>(lambda / static_cast<double>(U.omega[ub + ul]));
     for (int64_t il = 0; il < nv; ++il) W.regi[il] = static_cast<float>(lambda / static_cast<double>(I.omega[vreal[il]]));
     W.vrow = std::move(vrow);
-    W.len = len; W.nu = nu; W.nv = nv; W.ub = ub; W.GG = GG; W.T = T;
+    W.b = b; W.len = len; W.nu = nu; W.nv = nv; W.ub = ub; W.GG = GG; W.T = T;
     tick.lap(2);
   });
   const double wall_p1 = wall();
+  if (entries_out) {  // the caller emits (kernels_plan.hip); fp keeps the groups and the splits
+    if (std::getenv("MFHIP_TIMING"))
+      std::fprintf(stderr, "[mfhip]   fast plan wall: blocks %.3f s (emission on the device)\n", wall_p1);
+    *entries_out = std::move(work);
+    return;
+  }
   // Phase 2: emit.  Streams (a cell, or with gmajor one wave's K*G cells) are independent, so a
   // block's cells are cut into chunks of whole streams of about kChunk entries, emitted in
   // parallel and concatenated in cell order.
@@ -952,7 +951,7 @@ std::vector<std::vector<SubCell>> collect_supersteps(const FastPlan& fp, int32_t
 // and how A's user row is forwarded: from the previous step's A or B when that was the
 // record just before A.
 void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, int32_t shard, int32_t k,
-                     bool substep_waves) {
+                     bool substep_waves, const std::vector<int32_t>* cell_pairs) {
   using Cell = SubCell;
   pp = PairPlan();
   const auto subs = substep_waves ? collect_subs(fp, nb, c, shard) : collect_supersteps(fp, nb, c, shard);
@@ -978,22 +977,34 @@ void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, in
     }
   constexpr int64_t kCellChunk = 2048;
   const int64_t nchunks = (ncells + kCellChunk - 1) / kCellChunk;
+  // each wave's cell, indexed like fp.cell_off
+  pp.wave_cell.resize(ncells);
+  for (int64_t y = 0; y < ncells; ++y) {
+    const Cell& cl = *cellv[y];
+    const int64_t sm = substep_waves ? cell_sx[y] / fp.G : cell_sx[y];
+    const int32_t p = shard * c + cl.j;
+    const int64_t b = static_cast<int64_t>(p) * nb + (p + sm) % nb;
+    pp.wave_cell[y] = fp.cell_base[b] + static_cast<int64_t>(cl.t) * fp.Gb[b] + cl.g;
+  }
   std::vector<int32_t> npair(ncells);
-  parallel_tasks(nchunks, [&](int64_t ch) {
-    for (int64_t y = ch * kCellChunk; y < std::min(ncells, (ch + 1) * kCellChunk); ++y)
-      npair[y] = pairs_of(fp.recs.data() + cellv[y]->beg, cellv[y]->len);
-  });
+  if (cell_pairs)
+    for (int64_t y = 0; y < ncells; ++y) npair[y] = (*cell_pairs)[pp.wave_cell[y]];
+  else
+    parallel_tasks(nchunks, [&](int64_t ch) {
+      for (int64_t y = ch * kCellChunk; y < std::min(ncells, (ch + 1) * kCellChunk); ++y)
+        npair[y] = pairs_of(fp.recs.data() + cellv[y]->beg, cellv[y]->len);
+    });
   pp.waves.resize(ncells);
   int64_t total = 0;
   for (int64_t y = 0; y < ncells; ++y) {
     pp.waves[y] = WaveDesc{total, npair[y], kWaveGeneric};
     total += npair[y];
   }
-  resize_huge(pp.recs, total);
+  if (!cell_pairs) resize_huge(pp.recs, total);
   std::vector<int64_t> cell_noops(ncells, 0);
   std::vector<double> cell_bytes(ncells, 0.0);  // bytes the kernel requests for each cell
   const double row_bytes = 4.0 * k;
-  parallel_tasks(nchunks, [&](int64_t ch) {
+  parallel_tasks(cell_pairs ? 0 : nchunks, [&](int64_t ch) {
     for (int64_t w_this = ch * kCellChunk; w_this < std::min(ncells, (ch + 1) * kCellChunk); ++w_this) {
       const Cell& cl = *cellv[w_this];
       int64_t& noop = cell_noops[w_this];
@@ -1134,11 +1145,13 @@ void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, in
   pp.sys_off[nb] = static_cast<int64_t>(pp.sys_waves.size());
   for (int32_t sm = 0; sm < nb; ++sm)
     pp.sys_block_off[static_cast<size_t>(sm) * (c + 1) + c] = pp.sys_off[sm + 1] - pp.sys_off[sm];
+  pp.wave_sys.assign(ncells, -1);
   for (int64_t x = 0; x < nsub; ++x) {
     const int64_t sm = substep_waves ? x / fp.G : x;
     int64_t w = pp.sub_off[x];
     for (const Cell& cl : subs[x]) {
       const SysWave& sw = pp.sys_waves[wave0[sm][cl.j] + cl.g];
+      pp.wave_sys[w] = sw.cell0 + cl.t;
       pp.sys[sw.cell0 + cl.t] = pp.waves[w++];
     }
   }

@@ -195,6 +195,21 @@ struct SplitItem {
   int32_t R;
 };
 
+// One rating of a block while its fast plan is built: index in the block, local user, local
+// (virtual) item, rating.
+struct PlanEnt { uint32_t x, ul, vil; float r; };
+
+// A block after phase 1 of build_fast_plan (LPT groups, cell-major order, spreading): its
+// entries in final cell order, ready for the greedy emission (host, or kernels_plan.hip).
+struct FastBlockWork {
+  int64_t b = 0;                       // rating block
+  int64_t len = 0, nu = 0, nv = 0, ub = 0, GG = 0, T = 0;
+  std::vector<int64_t> cstart;         // GG + 1 cell starts in e
+  RecVec<PlanEnt> e;                   // the block's ratings in cell order
+  std::vector<uint32_t> vrow;          // virtual item -> physical row
+  std::vector<float> regu, regi;       // lambda / omega (f32) per local user / virtual item
+};
+
 struct FastPlan {
   int32_t G = 4;                       // rotation groups per rating block (the largest when per-block)
   int32_t K = 1;                       // user groups per item group: a block has G item x K*G user groups
@@ -283,6 +298,8 @@ static_assert(sizeof(StreamWave) == 16, "StreamWave is one 16-B word");
 
 struct PairPlan {
   RecVec<PairRec> recs;
+  std::vector<int64_t> wave_cell;  // per wave: its cell, indexed like FastPlan::cell_off (cell_base[b] + cell)
+  std::vector<int64_t> wave_sys;   // per wave: its slot in sys (-1: none)
   std::vector<WaveDesc> waves;   // one per non-empty cell (steps = pairs), every (sm, t), sm-major
   std::vector<int64_t> sub_off;  // nb*G + 1
   // Systolic tables (k_sweep_pair_sys): the waves of superstep sm are
@@ -304,8 +321,10 @@ struct PairPlan {
 // pp.waves / sub_off) per sub-step (sm, t), longest first, for the per-sub-step launches (needs a
 // uniform G); otherwise per superstep, and only the systolic tables are meaningful.
 // fp.gmajor: the stream tables instead (build_stream_plan).
+// cell_pairs (tables only): the pair count of every cell, indexed like fp.cell_off; the records
+// are then built elsewhere (kernels_plan.hip) and pp.recs stays empty, pp.waves[].cells generic.
 void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, int32_t shard, int32_t k,
-                     bool substep_waves = true);
+                     bool substep_waves = true, const std::vector<int32_t>* cell_pairs = nullptr);
 // ring: the kernel's prefetch depth (kStreamRing or another depth k_sweep_stream is built for; the
 // fast plan's window must be 2 * ring).
 void build_stream_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, int32_t shard, int32_t k,
@@ -330,7 +349,8 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
                      int32_t G, int32_t k, double lambda, uint64_t order_seed, uint32_t dummy_row,
                      std::vector<int64_t>* rec_src = nullptr, int32_t window = kHazardWindow,
                      const std::vector<int32_t>* block_groups = nullptr, int32_t split_run = 0,
-                     uint32_t scratch_base = 0, int32_t ustride = 1, bool gmajor = false);
+                     uint32_t scratch_base = 0, int32_t ustride = 1, bool gmajor = false,
+                     std::vector<FastBlockWork>* entries_out = nullptr);
 
 // Rotation groups per rating block for the systolic sweep, where every rating block of a
 // superstep is its own G_j x G_j grid and only the superstep's longest wave matters.  For each

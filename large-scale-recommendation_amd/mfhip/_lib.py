@@ -97,7 +97,7 @@ EXPORTS = [
     "mf_learning_rate", "mf_debug_levels", "mf_debug_fast_schedule", "mf_debug_fast_split", "mf_fast_plan_window",
     "mf_fast_kernel_name", "mf_get_params", "mf_read_ratings", "mf_save_model", "mf_load_model",
     "mf_dsgd_restart", "mf_online_update_out", "mf_debug_ring_schedule", "mf_debug_fast_stream",
-    "mf_debug_stream_protocol",
+    "mf_debug_stream_protocol", "mf_debug_plan_digest",
 ]
 
 _i32p = C.POINTER(C.c_int32)
@@ -171,6 +171,7 @@ def lib() -> C.CDLL:
         "mf_online_update_out": (C.c_int, [_ctxp, _i32p, _i32p, _f64p, C.c_int64, C.c_int, C.c_int, _i64p, _i64p,
                                            _f64p, _f64p]),
         "mf_debug_ring_schedule": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int64, _i32p, _i32p, _i32p, _i32p]),
+        "mf_debug_plan_digest": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -185,6 +185,12 @@ class Context:
         check(L.lib().mf_get_stats(self._h, C.byref(s)))
         return {f: getattr(s, f) for f, _ in L.mf_stats._fields_ if not f.startswith("reserved")}
 
+    def plan_digest(self) -> tuple:
+        """(FNV digest of the device schedule, pair records) after prepare (mf_debug_plan_digest)."""
+        out = (C.c_uint64 * 2)()
+        check(L.lib().mf_debug_plan_digest(self._h, out))
+        return int(out[0]), int(out[1])
+
     def reset_stats(self) -> None:
         check(L.lib().mf_reset_stats(self._h))
 
