@@ -72,7 +72,8 @@ def main():
         print(f"world={world} mode={a.mode} rmse rank={rm:.6f} single={rrm:.6f} matched {cnt}/{rcnt} "
               f"max|dU|={du:.3g} max|dI|={di:.3g}", flush=True)
         if a.mode == "det" or a.fast_waves < 0:
-            assert du == 0.0 and di == 0.0 and rm == rrm, "rank mode is not bit-exact"
+            # factors bitwise; the RMSE's SSE is all-reduced over ranks (another summation order)
+            assert du == 0.0 and di == 0.0 and abs(rm - rrm) <= 1e-12 * rrm, "rank mode is not bit-exact"
         else:
             assert abs(rm - rrm) / rrm < 5e-3, "rank-mode RMSE off"
         print("RANK_CHECK_OK", flush=True)
