@@ -91,6 +91,12 @@ class DevBuf {
   size_t bytes_ = 0;
 };
 
+// Rating blocks on the device (kernels_block.hip device_blocking's output, rb order).
+struct DevRatingBlocks {
+  DevBuf urow, irow, r;  // u32, u32, f64
+  int64_t total = 0;
+};
+
 // Pinned host staging buffer.
 class PinnedBuf {
  public:

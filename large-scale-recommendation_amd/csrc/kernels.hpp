@@ -114,17 +114,27 @@ void launch_predict(hipStream_t st, const int32_t* urow, const int32_t* irow, in
 // DSGDforMF.scala:513-588, the reference's seeded blocking) and the rating blocks of user blocks
 // [ub_lo, ub_hi) (:301-327; sort_ui: (user, item) order inside a block), bitwise what
 // build_side + build_rating_blocks (plan.cpp) produce.  Host arrays in, host structures out.
+class DevBuf;
+// keep (optional): the rating blocks' device arrays (urow u32, irow u32, r f64, rb order, the
+// first rb.start[n*n] entries valid) are handed over instead of freed.
+struct DevRatingBlocks;
 void device_blocking(hipStream_t st, const int32_t* u, const int32_t* i, const double* r, int64_t n, int32_t nb,
                      int64_t seed, int32_t ub_lo, int32_t ub_hi, bool sort_ui, SideLayout& U, SideLayout& I,
-                     RatingBlocks& rb);
+                     RatingBlocks& rb, DevRatingBlocks* keep = nullptr);
 
 // The fast pair schedule's per-cell work on the device (kernels_plan.hip): the greedy emission of
 // every cell of `work` (build_fast_plan's phase-1 output, blocks in ascending order) and the pair
 // records of every wave, bitwise the host build_fast_plan + build_pair_plan.  Fills fp's cell /
 // record offsets and pads, pp's tables and stats (pp.recs stays empty) and d_pairs (device).
-class DevBuf;
 void device_pair_schedule(hipStream_t st, std::vector<FastBlockWork>& work, FastPlan& fp, int32_t nb, int32_t c,
                           int32_t shard, int32_t k, uint32_t dummy_row, int32_t window, bool substep_waves,
+                          PairPlan& pp, DevBuf& d_pairs);
+// The whole fast schedule from the device rating blocks (kernels_plan.hip): phase 1 as device
+// sorts (cell-major order, spreading) around host LPT groups from device histograms, then the
+// emission and pair records as above.  Gb: the rotation groups of every rating block.
+void device_fast_schedule(hipStream_t st, const DevRatingBlocks& dr, const RatingBlocks& rb, const SideLayout& U,
+                          const SideLayout& I, const std::vector<int32_t>& Gb, double lambda, uint64_t order_seed,
+                          FastPlan& fp, int32_t c, int32_t shard, int32_t k, uint32_t dummy_row, int32_t window,
                           PairPlan& pp, DevBuf& d_pairs);
 
 // Initial factor rows on the device (DSGDforMF.scala:548-549, MatrixFactorization.scala:278-280):

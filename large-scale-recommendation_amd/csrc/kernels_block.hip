@@ -236,7 +236,7 @@ void block_side(hipStream_t st, Temp& tmp, const int32_t* d_ids, int64_t n, int3
 
 void device_blocking(hipStream_t st, const int32_t* u, const int32_t* i, const double* r, int64_t n, int32_t nb,
                      int64_t seed, int32_t ub_lo, int32_t ub_hi, bool sort_ui, SideLayout& U, SideLayout& I,
-                     RatingBlocks& rb) {
+                     RatingBlocks& rb, DevRatingBlocks* keep) {
   MF_REQUIRE(n < (int64_t{1} << 31), "device blocking sorts with 32-bit indices (< 2^31 ratings)");
   const int64_t nb2 = static_cast<int64_t>(nb) * nb;
   Temp tmp;
@@ -322,6 +322,12 @@ void device_blocking(hipStream_t st, const int32_t* u, const int32_t* i, const d
     MF_HIP(hipMemcpyAsync(rb.r.data(), gr.get(), total * 8, hipMemcpyDeviceToHost, st));
   }
   MF_HIP(hipStreamSynchronize(st));
+  if (keep) {
+    keep->urow = std::move(gu);
+    keep->irow = std::move(gi);
+    keep->r = std::move(gr);
+    keep->total = total;
+  }
 }
 
 }  // namespace mfhip

@@ -12,6 +12,10 @@
 // memory at the cell's entry range.  Integer work, latency-bound: no MFMA, no LDS staging.
 #include <hip/hip_runtime.h>
 
+#include <hipcub/device/device_radix_sort.hpp>
+#include <hipcub/device/device_scan.hpp>
+
+#include <algorithm>
 #include <climits>
 #include <vector>
 
@@ -366,59 +370,186 @@ T* upload(DevBuf& d, const T* h, size_t n, hipStream_t st) {
   return d.as<T>();
 }
 
-}  // namespace
+// ---------------------------------------------------------------------------------------------
+// Phase 1 on the device (build_fast_plan's per-block work for the default plan: no hot-item
+// replicas, K = 1, per-cell streams).  Ratings stay in the rating blocks' device order (x).
 
-void device_pair_schedule(hipStream_t st, std::vector<FastBlockWork>& work, FastPlan& fp, int32_t nb, int32_t c,
-                          int32_t shard, int32_t k, uint32_t dummy_row, int32_t window, bool substep_waves,
-                          PairPlan& pp, DevBuf& d_pairs) {
-  const int64_t nb2 = static_cast<int64_t>(nb) * nb;
-  const int64_t nblk = static_cast<int64_t>(work.size());
-  // cells indexed like fp.cell_off: per block GG cells + one empty slot
-  std::vector<int64_t> eoff(nblk + 1, 0), coff(nblk + 1, 0), vitoff(nblk + 1, 0), uoff(nblk + 1, 0);
-  for (int64_t bx = 0; bx < nblk; ++bx) {
-    eoff[bx + 1] = eoff[bx] + work[bx].len;
-    coff[bx + 1] = coff[bx] + work[bx].GG + 1;
-    vitoff[bx + 1] = vitoff[bx] + work[bx].nv;
-    uoff[bx + 1] = uoff[bx] + work[bx].nu;
+inline int bits_of(uint64_t maxval) {
+  int b = 1;
+  while (b < 64 && (maxval >> b) != 0) ++b;
+  return b;
+}
+
+__device__ __forceinline__ uint32_t mix32d(uint64_t x) {
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;
+  return static_cast<uint32_t>(x);
+}
+
+// per rating: its block, local user / item, and the per-block user / item histograms
+__global__ void k_p1_local(const uint32_t* __restrict__ urow, const uint32_t* __restrict__ irow, int64_t n,
+                           const int64_t* __restrict__ bstart, int64_t nb2, int32_t nb, const int64_t* __restrict__ ubs,
+                           const int64_t* __restrict__ ibs, const int64_t* __restrict__ uoff,
+                           const int64_t* __restrict__ ioff, int32_t* __restrict__ blk, uint32_t* __restrict__ ul,
+                           uint32_t* __restrict__ il, int32_t* __restrict__ ucnt, int32_t* __restrict__ icnt) {
+  for (int64_t x = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; x < n;
+       x += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    int64_t lo = 0, hi = nb2;  // block b: bstart[b] <= x < bstart[b+1]
+    while (hi - lo > 1) {
+      const int64_t mid = (lo + hi) / 2;
+      if (bstart[mid] <= x) lo = mid;
+      else hi = mid;
+    }
+    const int32_t b = static_cast<int32_t>(lo), p = b / nb, q = b % nb;
+    const uint32_t u = urow[x] - static_cast<uint32_t>(ubs[p]), i = irow[x] - static_cast<uint32_t>(ibs[q]);
+    blk[x] = b;
+    ul[x] = u;
+    il[x] = i;
+    atomicAdd(ucnt + uoff[b] + u, 1);
+    atomicAdd(icnt + ioff[b] + i, 1);
   }
-  const int64_t total = eoff[nblk], ncells = coff[nblk];
-  std::vector<int64_t> cstart(ncells + 1);
+}
+
+// cell-major key (cell, item rank in the cell's item group), stable in x by the sort
+__global__ void k_p1_cellkey(const int32_t* __restrict__ blk, const uint32_t* __restrict__ ul,
+                             const uint32_t* __restrict__ il, int64_t n, const int32_t* __restrict__ Gb,
+                             const int64_t* __restrict__ cbase, const int64_t* __restrict__ uoff,
+                             const int64_t* __restrict__ ioff, const int32_t* __restrict__ gu,
+                             const int32_t* __restrict__ gi, const int32_t* __restrict__ irank, uint64_t R,
+                             uint64_t* __restrict__ key, int32_t* __restrict__ val, int32_t* __restrict__ ccount) {
+  for (int64_t x = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; x < n;
+       x += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int32_t b = blk[x], G = Gb[b];
+    const int32_t g = gi[ioff[b] + il[x]], h = gu[uoff[b] + ul[x]];
+    const int32_t d = h - g;
+    const int64_t gc = cbase[b] + static_cast<int64_t>(d < 0 ? d + G : d) * G + g;
+    key[x] = static_cast<uint64_t>(gc) * R + static_cast<uint64_t>(irank[ioff[b] + il[x]]);
+    val[x] = static_cast<int32_t>(x);
+    atomicAdd(ccount + gc, 1);
+  }
+}
+
+__global__ void k_p1_heads64(const uint64_t* __restrict__ k, int64_t n, int32_t* __restrict__ head) {
+  for (int64_t y = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; y < n;
+       y += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    head[y] = (y == 0 || k[y] != k[y - 1]) ? 1 : 0;
+}
+
+// (run, local user) key of position y of the cell-major order
+__global__ void k_p1_runuser(const int32_t* __restrict__ runid1, const int32_t* __restrict__ O1,
+                             const uint32_t* __restrict__ ul, int64_t n, uint64_t NU, uint64_t* __restrict__ key,
+                             int32_t* __restrict__ val) {
+  for (int64_t y = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; y < n;
+       y += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    key[y] = static_cast<uint64_t>(runid1[y] - 1) * NU + ul[O1[y]];
+    val[y] = static_cast<int32_t>(y);
+  }
+}
+
+__global__ void k_p1_segstart(const int32_t* __restrict__ head, const int32_t* __restrict__ segid1, int64_t n,
+                              int64_t* __restrict__ segstart) {
+  for (int64_t z = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; z < n;
+       z += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    if (head[z]) segstart[segid1[z] - 1] = z;
+}
+
+// spreading key of position y: the o-th of a user's m ratings in its item run goes to
+// (o + h_u) / m (24 bits), ties by a second per-user hash (16 bits); x breaks the rest (stable)
+__global__ void k_p1_pos(const int32_t* __restrict__ segid1, const int64_t* __restrict__ segstart,
+                         const int32_t* __restrict__ P2, const int32_t* __restrict__ O1,
+                         const uint32_t* __restrict__ urow, int64_t n, uint64_t order_seed,
+                         uint64_t* __restrict__ pos, int32_t* __restrict__ val) {
+  for (int64_t z = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; z < n;
+       z += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t sg = segid1[z] - 1;
+    const int64_t s0 = segstart[sg], m = segstart[sg + 1] - s0, o = z - s0;
+    const int32_t y = P2[z];
+    const uint32_t u = urow[O1[y]];
+    const double h = static_cast<double>(mix32d(order_seed * 0x2545F4914F6CDD1DULL ^ u)) * (1.0 / 4294967296.0);
+    const double frac = (static_cast<double>(o) + h) / static_cast<double>(m);
+    const uint64_t tie = mix32d(order_seed ^ (static_cast<uint64_t>(u) << 20)) & 0xFFFFu;
+    pos[y] = (static_cast<uint64_t>(frac * 16777216.0) << 16) | tie;
+    val[y] = y;
+  }
+}
+
+__global__ void k_p1_runkey(const int32_t* __restrict__ Q1, const int32_t* __restrict__ runid1, int64_t n,
+                            uint32_t* __restrict__ key) {
+  for (int64_t w = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; w < n;
+       w += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    key[w] = static_cast<uint32_t>(runid1[Q1[w]] - 1);
+}
+
+__global__ void k_p1_gather(const int32_t* __restrict__ F, const int32_t* __restrict__ O1,
+                            const int32_t* __restrict__ blk, const int64_t* __restrict__ bstart,
+                            const uint32_t* __restrict__ ul, const uint32_t* __restrict__ il,
+                            const double* __restrict__ r, int64_t n, PlanEnt* __restrict__ E) {
+  for (int64_t w = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; w < n;
+       w += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int32_t x = O1[F[w]];
+    E[w] = PlanEnt{static_cast<uint32_t>(x - bstart[blk[x]]), ul[x], il[x], static_cast<float>(r[x])};
+  }
+}
+
+struct SortTemp {
+  DevBuf buf;
+  void* get(size_t bytes) {
+    buf.alloc(std::max<size_t>(bytes, 256));
+    return buf.get();
+  }
+};
+
+template <class K>
+void sort_pairs(hipStream_t st, SortTemp& tmp, const K* kin, K* kout, const int32_t* vin, int32_t* vout, int64_t n,
+                int bits) {
+  size_t tb = 0;
+  MF_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kin, kout, vin, vout, static_cast<int>(n), 0, bits, st));
+  MF_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.get(tb), tb, kin, kout, vin, vout, static_cast<int>(n), 0, bits, st));
+}
+
+void inclusive_sum(hipStream_t st, SortTemp& tmp, const int32_t* in, int32_t* out, int64_t n) {
+  size_t tb = 0;
+  MF_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tb, in, out, static_cast<int>(n), st));
+  MF_HIP(hipcub::DeviceScan::InclusiveSum(tmp.get(tb), tb, in, out, static_cast<int>(n), st));
+}
+
+// Per-block host metadata of the plan (blocks with ratings, ascending b) and the device inputs
+// of the emission: the entries in cell order and the cell starts (cells indexed like
+// fp.cell_off: GG cells + one empty slot per block).
+struct PlanBlocks {
+  std::vector<int64_t> b, GG, nu, nv, len;
+  std::vector<uint32_t> ub;
+  std::vector<int64_t> uoff, voff;  // nblk + 1: offsets into regu / regi, vrow
+  std::vector<float> regu, regi;
+  std::vector<uint32_t> vrow;
+  int64_t total = 0;
+};
+
+void emit_and_pair(hipStream_t st, const PlanBlocks& pb, DevBuf& dE, DevBuf& dcs, FastPlan& fp, int32_t nb, int32_t c,
+                   int32_t shard, int32_t k, uint32_t dummy_row, int32_t window, bool substep_waves, PairPlan& pp,
+                   DevBuf& d_pairs) {
+  const int64_t nb2 = static_cast<int64_t>(nb) * nb;
+  const int64_t nblk = static_cast<int64_t>(pb.b.size());
+  std::vector<int64_t> coff(nblk + 1, 0);
+  for (int64_t bx = 0; bx < nblk; ++bx) coff[bx + 1] = coff[bx] + pb.GG[bx] + 1;
+  const int64_t total = pb.total, ncells = coff[nblk];
   std::vector<int32_t> cblk(ncells);
-  std::vector<uint32_t> bub(nblk);
-  std::vector<float> regu(uoff[nblk]), regi(vitoff[nblk]);
-  std::vector<uint32_t> vrow(vitoff[nblk]);
   fp.cell_base.assign(nb2, -1);
   fp.rec_base.assign(nb2, -1);
   for (int64_t bx = 0; bx < nblk; ++bx) {
-    const FastBlockWork& W = work[bx];
-    fp.cell_base[W.b] = coff[bx];
-    for (int64_t cc = 0; cc <= W.GG; ++cc) {
-      cstart[coff[bx] + cc] = eoff[bx] + W.cstart[cc];
-      if (cc < W.GG) cblk[coff[bx] + cc] = static_cast<int32_t>(bx);
-    }
-    cblk[coff[bx] + W.GG] = static_cast<int32_t>(bx);
-    bub[bx] = static_cast<uint32_t>(W.ub);
-    std::copy(W.regu.begin(), W.regu.end(), regu.begin() + uoff[bx]);
-    std::copy(W.regi.begin(), W.regi.end(), regi.begin() + vitoff[bx]);
-    std::copy(W.vrow.begin(), W.vrow.end(), vrow.begin() + vitoff[bx]);
+    fp.cell_base[pb.b[bx]] = coff[bx];
+    for (int64_t cc = 0; cc <= pb.GG[bx]; ++cc) cblk[coff[bx] + cc] = static_cast<int32_t>(bx);
   }
-  cstart[ncells] = total;
-  DevBuf dE, dcs, dcb, dbub, dbregu, dbvit, dregu, dregi, dvrow;
-  dE.alloc(std::max<int64_t>(total, 1) * sizeof(PlanEnt));
-  for (int64_t bx = 0; bx < nblk; ++bx)
-    if (work[bx].len)
-      MF_HIP(hipMemcpyAsync(dE.as<PlanEnt>() + eoff[bx], work[bx].e.data(), work[bx].len * sizeof(PlanEnt),
-                            hipMemcpyHostToDevice, st));
+  DevBuf dcb, dbub, dbregu, dbvit, dregu, dregi, dvrow;
   EmitArgs A{};
   A.E = dE.as<PlanEnt>();
-  A.cstart = upload(dcs, cstart.data(), cstart.size(), st);
+  A.cstart = dcs.as<int64_t>();
   A.cblk = upload(dcb, cblk.data(), cblk.size(), st);
-  A.bub = upload(dbub, bub.data(), bub.size(), st);
-  A.bregu = upload(dbregu, uoff.data(), static_cast<size_t>(nblk), st);
-  A.bvit = upload(dbvit, vitoff.data(), static_cast<size_t>(nblk), st);
-  A.regu = upload(dregu, regu.data(), regu.size(), st);
-  A.regi = upload(dregi, regi.data(), regi.size(), st);
-  A.vrow = upload(dvrow, vrow.data(), vrow.size(), st);
+  A.bub = upload(dbub, pb.ub.data(), pb.ub.size(), st);
+  A.bregu = upload(dbregu, pb.uoff.data(), static_cast<size_t>(nblk), st);
+  A.bvit = upload(dbvit, pb.voff.data(), static_cast<size_t>(nblk), st);
+  A.regu = upload(dregu, pb.regu.data(), pb.regu.size(), st);
+  A.regi = upload(dregi, pb.regi.data(), pb.regi.size(), st);
+  A.vrow = upload(dvrow, pb.vrow.data(), pb.vrow.size(), st);
   const size_t ne = static_cast<size_t>(std::max<int64_t>(total, 1));
   DevBuf s_ug, s_ig, s_ul, s_io, s_tk, s_igB, s_igE, s_igH, s_igL, s_igR, s_ugB, s_ugE, s_ugH, s_ugL, s_lu, s_li, s_hk, s_hv;
   auto i32 = [&](DevBuf& d) { d.alloc(ne * 4); return d.as<int32_t>(); };
@@ -434,12 +565,11 @@ void device_pair_schedule(hipStream_t st, std::vector<FastBlockWork>& work, Fast
   A.window = window;
   A.row_bytes = static_cast<uint32_t>(k) * 4u;
   A.dummy = dummy_row;
-  DevBuf dnrec, dnpads, dnpairs, drecbase, drecs;
-  dnrec.alloc(static_cast<size_t>(ncells) * 4);
-  dnpads.alloc(static_cast<size_t>(ncells) * 4);
+  DevBuf dnrec, dnpads, dnpairs, drecbase, drecs, derr;
+  dnrec.alloc(static_cast<size_t>(std::max<int64_t>(ncells, 1)) * 4);
+  dnpads.alloc(static_cast<size_t>(std::max<int64_t>(ncells, 1)) * 4);
   A.nrec = dnrec.as<int32_t>();
   A.npads = dnpads.as<int32_t>();
-  DevBuf derr;
   derr.alloc(4);
   MF_HIP(hipMemsetAsync(derr.get(), 0, 4, st));
   A.err = derr.as<int32_t>();
@@ -458,9 +588,9 @@ void device_pair_schedule(hipStream_t st, std::vector<FastBlockWork>& work, Fast
   fp.pads = 0;
   int64_t nrecs = 0;
   for (int64_t bx = 0; bx < nblk; ++bx) {
-    fp.rec_base[work[bx].b] = nrecs;
+    fp.rec_base[pb.b[bx]] = nrecs;
     int64_t acc = 0;
-    for (int64_t cc = 0; cc <= work[bx].GG; ++cc) {
+    for (int64_t cc = 0; cc <= pb.GG[bx]; ++cc) {
       const int64_t gc = coff[bx] + cc;
       recbase[gc] = nrecs + acc;
       fp.cell_off[gc] = static_cast<int32_t>(acc);
@@ -472,7 +602,7 @@ void device_pair_schedule(hipStream_t st, std::vector<FastBlockWork>& work, Fast
   A.recbase = upload(drecbase, recbase.data(), recbase.size(), st);
   drecs.alloc(static_cast<size_t>(std::max<int64_t>(nrecs, 1)) * sizeof(FastRec));
   A.recs = drecs.as<FastRec>();
-  dnpairs.alloc(static_cast<size_t>(ncells) * 4);
+  dnpairs.alloc(static_cast<size_t>(std::max<int64_t>(ncells, 1)) * 4);
   A.npairs = dnpairs.as<int32_t>();
   hipLaunchKernelGGL(k_emit_cells, dim3(plan_grid(ncells)), dim3(kPlanThreads), 0, st, A);
   MF_HIP(hipGetLastError());
@@ -534,6 +664,243 @@ void device_pair_schedule(hipStream_t st, std::vector<FastBlockWork>& work, Fast
     }
   pp.sm_bytes.assign(nb, 0.0);
   for (int64_t x = 0; x < nsub; ++x) pp.sm_bytes[substep_waves ? x / fp.G : x] += sub_bytes[x];
+}
+
+}  // namespace
+
+void device_pair_schedule(hipStream_t st, std::vector<FastBlockWork>& work, FastPlan& fp, int32_t nb, int32_t c,
+                          int32_t shard, int32_t k, uint32_t dummy_row, int32_t window, bool substep_waves,
+                          PairPlan& pp, DevBuf& d_pairs) {
+  const int64_t nblk = static_cast<int64_t>(work.size());
+  PlanBlocks pb;
+  pb.uoff.assign(nblk + 1, 0);
+  pb.voff.assign(nblk + 1, 0);
+  std::vector<int64_t> eoff(nblk + 1, 0);
+  for (int64_t bx = 0; bx < nblk; ++bx) {
+    const FastBlockWork& W = work[bx];
+    pb.b.push_back(W.b);
+    pb.GG.push_back(W.GG);
+    pb.nu.push_back(W.nu);
+    pb.nv.push_back(W.nv);
+    pb.len.push_back(W.len);
+    pb.ub.push_back(static_cast<uint32_t>(W.ub));
+    pb.uoff[bx + 1] = pb.uoff[bx] + W.nu;
+    pb.voff[bx + 1] = pb.voff[bx] + W.nv;
+    eoff[bx + 1] = eoff[bx] + W.len;
+    pb.regu.insert(pb.regu.end(), W.regu.begin(), W.regu.end());
+    pb.regi.insert(pb.regi.end(), W.regi.begin(), W.regi.end());
+    pb.vrow.insert(pb.vrow.end(), W.vrow.begin(), W.vrow.end());
+  }
+  pb.total = eoff[nblk];
+  std::vector<int64_t> cstart;
+  for (int64_t bx = 0; bx < nblk; ++bx)
+    for (int64_t cc = 0; cc <= work[bx].GG; ++cc) cstart.push_back(eoff[bx] + work[bx].cstart[cc]);
+  cstart.push_back(pb.total);
+  DevBuf dE, dcs;
+  dE.alloc(std::max<int64_t>(pb.total, 1) * sizeof(PlanEnt));
+  for (int64_t bx = 0; bx < nblk; ++bx)
+    if (work[bx].len)
+      MF_HIP(hipMemcpyAsync(dE.as<PlanEnt>() + eoff[bx], work[bx].e.data(), work[bx].len * sizeof(PlanEnt),
+                            hipMemcpyHostToDevice, st));
+  upload(dcs, cstart.data(), cstart.size(), st);
+  emit_and_pair(st, pb, dE, dcs, fp, nb, c, shard, k, dummy_row, window, substep_waves, pp, d_pairs);
+}
+
+void device_fast_schedule(hipStream_t st, const DevRatingBlocks& dr, const RatingBlocks& rb, const SideLayout& U,
+                          const SideLayout& I, const std::vector<int32_t>& Gb, double lambda, uint64_t order_seed,
+                          FastPlan& fp, int32_t c, int32_t shard, int32_t k, uint32_t dummy_row, int32_t window,
+                          PairPlan& pp, DevBuf& d_pairs) {
+  const int32_t nb = rb.n_blocks;
+  const int64_t nb2 = static_cast<int64_t>(nb) * nb;
+  const int64_t n = dr.total;
+  MF_REQUIRE(n == rb.start[nb2] && n < (int64_t{1} << 31), "device schedule: rating blocks do not match");
+  PlanBlocks pb;
+  std::vector<int64_t> uoffb(nb2, 0), ioffb(nb2, 0), cbase(nb2, 0);
+  std::vector<int32_t> Gblk(nb2, 1);
+  int64_t usum = 0, isum = 0, csum = 0;
+  for (int64_t b = 0; b < nb2; ++b) {
+    if (rb.size(b) == 0) continue;
+    const int32_t p = static_cast<int32_t>(b / nb), q = static_cast<int32_t>(b % nb);
+    const int64_t nu = U.block_start[p + 1] - U.block_start[p], ni = I.block_start[q + 1] - I.block_start[q];
+    const int64_t G = Gb[b];
+    pb.b.push_back(b);
+    pb.GG.push_back(G * G);
+    pb.nu.push_back(nu);
+    pb.nv.push_back(ni);
+    pb.len.push_back(rb.size(b));
+    pb.ub.push_back(static_cast<uint32_t>(U.block_start[p]));
+    uoffb[b] = usum;
+    ioffb[b] = isum;
+    cbase[b] = csum;
+    Gblk[b] = static_cast<int32_t>(G);
+    usum += nu;
+    isum += ni;
+    csum += G * G + 1;
+  }
+  const int64_t nblk = static_cast<int64_t>(pb.b.size());
+  pb.total = n;
+  // 1. local rows and the per-block histograms
+  DevBuf dbs, dubs, dibs, duo, dio, dblk, dul, dil, ducnt, dicnt;
+  upload(dbs, rb.start.data(), rb.start.size(), st);
+  upload(dubs, U.block_start.data(), U.block_start.size(), st);
+  upload(dibs, I.block_start.data(), I.block_start.size(), st);
+  upload(duo, uoffb.data(), uoffb.size(), st);
+  upload(dio, ioffb.data(), ioffb.size(), st);
+  const size_t nn = static_cast<size_t>(std::max<int64_t>(n, 1));
+  dblk.alloc(nn * 4);
+  dul.alloc(nn * 4);
+  dil.alloc(nn * 4);
+  ducnt.alloc(static_cast<size_t>(std::max<int64_t>(usum, 1)) * 4);
+  dicnt.alloc(static_cast<size_t>(std::max<int64_t>(isum, 1)) * 4);
+  MF_HIP(hipMemsetAsync(ducnt.get(), 0, ducnt.bytes(), st));
+  MF_HIP(hipMemsetAsync(dicnt.get(), 0, dicnt.bytes(), st));
+  hipLaunchKernelGGL(k_p1_local, dim3(plan_grid(n)), dim3(256), 0, st, dr.urow.as<uint32_t>(), dr.irow.as<uint32_t>(), n,
+                     dbs.as<int64_t>(), nb2, nb, dubs.as<int64_t>(), dibs.as<int64_t>(), duo.as<int64_t>(),
+                     dio.as<int64_t>(), dblk.as<int32_t>(), dul.as<uint32_t>(), dil.as<uint32_t>(), ducnt.as<int32_t>(),
+                     dicnt.as<int32_t>());
+  MF_HIP(hipGetLastError());
+  std::vector<int32_t> ucnt(usum), icnt(isum);
+  if (usum) MF_HIP(hipMemcpyAsync(ucnt.data(), ducnt.get(), usum * 4, hipMemcpyDeviceToHost, st));
+  if (isum) MF_HIP(hipMemcpyAsync(icnt.data(), dicnt.get(), isum * 4, hipMemcpyDeviceToHost, st));
+  MF_HIP(hipStreamSynchronize(st));
+  // 2. LPT groups per block on the host (build_fast_plan phase 1), item ranks inside a group
+  std::vector<int32_t> gu(usum), gi(isum), irank(isum);
+  std::vector<int32_t> gmax(nblk, 0);
+  pb.uoff.assign(nblk + 1, 0);
+  pb.voff.assign(nblk + 1, 0);
+  for (int64_t bx = 0; bx < nblk; ++bx) {
+    pb.uoff[bx + 1] = pb.uoff[bx] + pb.nu[bx];
+    pb.voff[bx + 1] = pb.voff[bx] + pb.nv[bx];
+  }
+  pb.regu.resize(usum);
+  pb.regi.resize(isum);
+  pb.vrow.resize(isum);
+  parallel_tasks(nblk, [&](int64_t bx) {
+    const int64_t b = pb.b[bx];
+    const int32_t G = Gblk[b];
+    const int32_t p = static_cast<int32_t>(b / nb), q = static_cast<int32_t>(b % nb);
+    const int64_t nu = pb.nu[bx], ni = pb.nv[bx];
+    std::vector<int64_t> lu(ucnt.begin() + uoffb[b], ucnt.begin() + uoffb[b] + nu);
+    std::vector<int64_t> li(icnt.begin() + ioffb[b], icnt.begin() + ioffb[b] + ni);
+    std::vector<int32_t> g1, g2;
+    lpt_assign(lu, G, g1);
+    lpt_assign(li, G, g2);
+    std::copy(g1.begin(), g1.end(), gu.begin() + uoffb[b]);
+    std::copy(g2.begin(), g2.end(), gi.begin() + ioffb[b]);
+    std::vector<int32_t> gsize(G, 0);
+    for (int64_t il = 0; il < ni; ++il) irank[ioffb[b] + il] = gsize[g2[il]]++;
+    gmax[bx] = *std::max_element(gsize.begin(), gsize.end());
+    const int64_t ub = U.block_start[p], ib = I.block_start[q];
+    for (int64_t ul = 0; ul < nu; ++ul)
+      pb.regu[pb.uoff[bx] + ul] = static_cast<float>(lambda / static_cast<double>(U.omega[ub + ul]));
+    for (int64_t il = 0; il < ni; ++il) {
+      pb.regi[pb.voff[bx] + il] = static_cast<float>(lambda / static_cast<double>(I.omega[ib + il]));
+      pb.vrow[pb.voff[bx] + il] = static_cast<uint32_t>(ib + il);
+    }
+  });
+  int32_t R = 1;
+  for (int32_t g : gmax) R = std::max(R, g + 1);
+  const int64_t ncells = csum;
+  // 3. cell-major order (cell, item rank, x)
+  DevBuf dGb, dcb, dgu, dgi, dir, dk1, dk1s, dv1, dO1, dcc, dcs;
+  upload(dGb, Gblk.data(), Gblk.size(), st);
+  upload(dcb, cbase.data(), cbase.size(), st);
+  upload(dgu, gu.data(), gu.size(), st);
+  upload(dgi, gi.data(), gi.size(), st);
+  upload(dir, irank.data(), irank.size(), st);
+  dk1.alloc(nn * 8);
+  dk1s.alloc(nn * 8);
+  dv1.alloc(nn * 4);
+  dO1.alloc(nn * 4);
+  dcc.alloc(static_cast<size_t>(ncells + 1) * 4);
+  MF_HIP(hipMemsetAsync(dcc.get(), 0, dcc.bytes(), st));
+  hipLaunchKernelGGL(k_p1_cellkey, dim3(plan_grid(n)), dim3(256), 0, st, dblk.as<int32_t>(), dul.as<uint32_t>(),
+                     dil.as<uint32_t>(), n, dGb.as<int32_t>(), dcb.as<int64_t>(), duo.as<int64_t>(), dio.as<int64_t>(),
+                     dgu.as<int32_t>(), dgi.as<int32_t>(), dir.as<int32_t>(), static_cast<uint64_t>(R),
+                     dk1.as<uint64_t>(), dv1.as<int32_t>(), dcc.as<int32_t>());
+  MF_HIP(hipGetLastError());
+  SortTemp tmp;
+  sort_pairs<uint64_t>(st, tmp, dk1.as<uint64_t>(), dk1s.as<uint64_t>(), dv1.as<int32_t>(), dO1.as<int32_t>(), n,
+                       bits_of(static_cast<uint64_t>(ncells) * R));
+  // cell starts: inclusive scan of the cell counts (one extra zero slot at the end)
+  std::vector<int64_t> cstart(ncells + 1, 0);
+  {
+    DevBuf incl;
+    incl.alloc(static_cast<size_t>(ncells + 1) * 4);
+    inclusive_sum(st, tmp, dcc.as<int32_t>(), incl.as<int32_t>(), ncells + 1);
+    std::vector<int32_t> h(ncells + 1);
+    MF_HIP(hipMemcpyAsync(h.data(), incl.get(), (ncells + 1) * 4, hipMemcpyDeviceToHost, st));
+    MF_HIP(hipStreamSynchronize(st));
+    for (int64_t gc = 0; gc < ncells; ++gc) cstart[gc + 1] = h[gc];
+  }
+  upload(dcs, cstart.data(), cstart.size(), st);
+  // 4. runs (cell, item) of that order; within a run each user's ratings counted (o of m)
+  DevBuf dhead, drun, dk2, dk2s, dv2, dP2, dseg, dsegs;
+  dhead.alloc(nn * 4);
+  drun.alloc(nn * 4);
+  hipLaunchKernelGGL(k_p1_heads64, dim3(plan_grid(n)), dim3(256), 0, st, dk1s.as<uint64_t>(), n, dhead.as<int32_t>());
+  inclusive_sum(st, tmp, dhead.as<int32_t>(), drun.as<int32_t>(), n);
+  int32_t nruns = 0;
+  MF_HIP(hipMemcpyAsync(&nruns, drun.as<int32_t>() + n - 1, 4, hipMemcpyDeviceToHost, st));
+  int64_t numax = 1;
+  for (int64_t bx = 0; bx < nblk; ++bx) numax = std::max(numax, pb.nu[bx] + 1);
+  MF_HIP(hipStreamSynchronize(st));
+  dk1.release();
+  dk2.alloc(nn * 8);
+  dk2s.alloc(nn * 8);
+  dv2.alloc(nn * 4);
+  dP2.alloc(nn * 4);
+  hipLaunchKernelGGL(k_p1_runuser, dim3(plan_grid(n)), dim3(256), 0, st, drun.as<int32_t>(), dO1.as<int32_t>(),
+                     dul.as<uint32_t>(), n, static_cast<uint64_t>(numax), dk2.as<uint64_t>(), dv2.as<int32_t>());
+  sort_pairs<uint64_t>(st, tmp, dk2.as<uint64_t>(), dk2s.as<uint64_t>(), dv2.as<int32_t>(), dP2.as<int32_t>(), n,
+                       bits_of(static_cast<uint64_t>(nruns) * numax));
+  hipLaunchKernelGGL(k_p1_heads64, dim3(plan_grid(n)), dim3(256), 0, st, dk2s.as<uint64_t>(), n, dhead.as<int32_t>());
+  dseg.alloc(nn * 4);
+  inclusive_sum(st, tmp, dhead.as<int32_t>(), dseg.as<int32_t>(), n);
+  int32_t nseg = 0;
+  MF_HIP(hipMemcpyAsync(&nseg, dseg.as<int32_t>() + n - 1, 4, hipMemcpyDeviceToHost, st));
+  MF_HIP(hipStreamSynchronize(st));
+  dsegs.alloc(static_cast<size_t>(nseg + 1) * 8);
+  hipLaunchKernelGGL(k_p1_segstart, dim3(plan_grid(n)), dim3(256), 0, st, dhead.as<int32_t>(), dseg.as<int32_t>(), n,
+                     dsegs.as<int64_t>());
+  const int64_t nend = n;
+  MF_HIP(hipMemcpyAsync(dsegs.as<int64_t>() + nseg, &nend, 8, hipMemcpyHostToDevice, st));
+  // 5. spreading positions, then the final order: by position, then (stably) by run
+  DevBuf dpos, dposs, dv3, dQ1, dk3, dk3s, dF;
+  dpos.alloc(nn * 8);
+  dposs.alloc(nn * 8);
+  dv3.alloc(nn * 4);
+  dQ1.alloc(nn * 4);
+  hipLaunchKernelGGL(k_p1_pos, dim3(plan_grid(n)), dim3(256), 0, st, dseg.as<int32_t>(), dsegs.as<int64_t>(),
+                     dP2.as<int32_t>(), dO1.as<int32_t>(), dr.urow.as<uint32_t>(), n, order_seed, dpos.as<uint64_t>(),
+                     dv3.as<int32_t>());
+  MF_HIP(hipGetLastError());
+  sort_pairs<uint64_t>(st, tmp, dpos.as<uint64_t>(), dposs.as<uint64_t>(), dv3.as<int32_t>(), dQ1.as<int32_t>(), n, 40);
+  dk3.alloc(nn * 4);
+  dk3s.alloc(nn * 4);
+  dF.alloc(nn * 4);
+  hipLaunchKernelGGL(k_p1_runkey, dim3(plan_grid(n)), dim3(256), 0, st, dQ1.as<int32_t>(), drun.as<int32_t>(), n,
+                     dk3.as<uint32_t>());
+  sort_pairs<uint32_t>(st, tmp, dk3.as<uint32_t>(), dk3s.as<uint32_t>(), dQ1.as<int32_t>(), dF.as<int32_t>(), n,
+                       bits_of(static_cast<uint64_t>(nruns)));
+  DevBuf dE;
+  dE.alloc(nn * sizeof(PlanEnt));
+  hipLaunchKernelGGL(k_p1_gather, dim3(plan_grid(n)), dim3(256), 0, st, dF.as<int32_t>(), dO1.as<int32_t>(),
+                     dblk.as<int32_t>(), dbs.as<int64_t>(), dul.as<uint32_t>(), dil.as<uint32_t>(), dr.r.as<double>(), n,
+                     dE.as<PlanEnt>());
+  MF_HIP(hipGetLastError());
+  MF_HIP(hipStreamSynchronize(st));
+  for (DevBuf* d : {&dk1s, &dv1, &dO1, &dhead, &drun, &dk2, &dk2s, &dv2, &dP2, &dseg, &dsegs, &dpos, &dposs, &dv3, &dQ1,
+                    &dk3, &dk3s, &dF, &dblk, &dul, &dil, &dcc})
+    d->release();
+  fp.K = 1;
+  fp.gmajor = false;
+  fp.Gb.assign(Gblk.begin(), Gblk.end());
+  fp.G = *std::max_element(fp.Gb.begin(), fp.Gb.end());
+  fp.split_off.assign(nb2 + 1, 0);
+  fp.splits.clear();
+  fp.scratch_rows = 0;
+  emit_and_pair(st, pb, dE, dcs, fp, nb, c, shard, k, dummy_row, window, false, pp, d_pairs);
 }
 
 }  // namespace mfhip

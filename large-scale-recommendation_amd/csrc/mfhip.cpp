@@ -1101,6 +1101,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
   sync_all(ctx);
   PhaseClock clk;
   ctx->reaper.join();
+  DevRatingBlocks dev_rb;  // the device copy of the rating blocks (full device schedule only)
   ctx->nb = std::max(1, ctx->P.num_blocks);
   MF_REQUIRE(ctx->nb % ctx->G == 0, "num_blocks must be a multiple of the device count");
   ctx->c = ctx->nb / ctx->G;
@@ -1113,7 +1114,12 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
   if (on_device) {
     Shard& s0 = ctx->shards[0];
     DeviceGuard g(s0.device);
-    device_blocking(s0.stream, u, i, r, n, ctx->nb, ctx->P.seed, lo, hi, ctx->f64, ctx->U, ctx->I, ctx->rb);
+    const char* dpv0 = std::getenv("MFHIP_DEVICE_PLAN");
+    const bool keep = !ctx->f64 && ctx->shards.size() == 1 && ctx->P.fast_item_split == 0 &&
+                      choose_fast_kernel(ctx->P.num_factors) == FastKernel::kPair && !want_stream() &&
+                      !(dpv0 && (std::string(dpv0) == "0" || std::string(dpv0) == "1"));
+    device_blocking(s0.stream, u, i, r, n, ctx->nb, ctx->P.seed, lo, hi, ctx->f64, ctx->U, ctx->I, ctx->rb,
+                    keep ? &dev_rb : nullptr);
     clk.lap("blocking + rating blocks (device)");
   }
   build_model(ctx, u, i, n, on_device);
@@ -1230,17 +1236,32 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
     const bool dev_plan = ctx->fast_pair && ctx->fast_sys && !ctx->fast_stream && ctx->P.fast_item_split == 0 &&
                           ctx->shards.size() == 1 && !(dpv && std::string(dpv) == "0");
     std::vector<FastBlockWork> entries;
-    build_fast_plan(fp, ctx->rb, ctx->U, ctx->I, ctx->G_fast, k, ctx->P.lambda,
-                    static_cast<uint64_t>(ctx->P.seed) * 0x9E3779B97F4A7C15ULL + 1, dummy, nullptr,
-                    ctx->fast_stream ? 2 * ctx->stream_ring : ctx->fast_pair ? 2 * kPairRing : kHazardWindow,
-                    block_groups.empty() ? nullptr : &block_groups, ctx->P.fast_item_split,
-                    static_cast<uint32_t>(ctx->I.rows() + 1), ctx->fast_stream ? stream_K : 1, ctx->fast_stream,
-                    dev_plan ? &entries : nullptr);
-    MF_REQUIRE(static_cast<uint64_t>(ctx->I.rows() + 1 + fp.scratch_rows) * k * 4 < (1ull << 32),
-               "hot-item replica rows exceed the 32-bit item slab offsets");
     PairPlan dev_pp;
     DevBuf dev_pairs;
-    if (dev_plan) {
+    // MFHIP_DEVICE_PLAN: unset / 2 = the whole schedule on the device, 1 = host phase 1 + device
+    // emission, 0 = host
+    const bool dev_full = dev_plan && dev_rb.total == ctx->rb.start[nb2] && dev_rb.urow.get();
+    if (dev_full) {
+      std::vector<int32_t> Gb(nb2, ctx->G_fast);
+      if (!block_groups.empty())
+        for (int64_t b = 0; b < nb2; ++b) Gb[b] = block_groups[b] > 0 ? block_groups[b] : ctx->G_fast;
+      Shard& s0 = ctx->shards[0];
+      DeviceGuard g(s0.device);
+      device_fast_schedule(s0.stream, dev_rb, ctx->rb, ctx->U, ctx->I, Gb, ctx->P.lambda,
+                           static_cast<uint64_t>(ctx->P.seed) * 0x9E3779B97F4A7C15ULL + 1, fp, ctx->c, s0.index, k,
+                           dummy, 2 * kPairRing, dev_pp, dev_pairs);
+      dev_rb = DevRatingBlocks();
+    } else {
+      build_fast_plan(fp, ctx->rb, ctx->U, ctx->I, ctx->G_fast, k, ctx->P.lambda,
+                      static_cast<uint64_t>(ctx->P.seed) * 0x9E3779B97F4A7C15ULL + 1, dummy, nullptr,
+                      ctx->fast_stream ? 2 * ctx->stream_ring : ctx->fast_pair ? 2 * kPairRing : kHazardWindow,
+                      block_groups.empty() ? nullptr : &block_groups, ctx->P.fast_item_split,
+                      static_cast<uint32_t>(ctx->I.rows() + 1), ctx->fast_stream ? stream_K : 1, ctx->fast_stream,
+                      dev_plan ? &entries : nullptr);
+    }
+    MF_REQUIRE(static_cast<uint64_t>(ctx->I.rows() + 1 + fp.scratch_rows) * k * 4 < (1ull << 32),
+               "hot-item replica rows exceed the 32-bit item slab offsets");
+    if (dev_plan && !dev_full) {
       Shard& s0 = ctx->shards[0];
       DeviceGuard g(s0.device);
       clk.lap("cell order (host)");
@@ -1250,7 +1271,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
     }
     ctx->stats.pads = fp.pads;
     ctx->reaper.drop(fp.scratch);
-    clk.lap(dev_plan ? "cell emission + pairs (device)" : "cell plan");
+    clk.lap(dev_full ? "schedule (device)" : dev_plan ? "cell emission + pairs (device)" : "cell plan");
     {  // priority threshold: 3x the mean non-empty cell length
       int64_t cells = 0, recs = 0;
       for (int64_t b = 0; b < nb2; ++b)

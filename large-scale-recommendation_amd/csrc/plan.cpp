@@ -1422,6 +1422,8 @@ int64_t stream_protocol_deadlocks(const PairPlan& pp, int32_t nb, std::string* r
   return bad;
 }
 
+void lpt_assign(const std::vector<int64_t>& load, int32_t G, std::vector<int32_t>& group) { lpt_groups(load, G, group); }
+
 std::vector<int32_t> choose_block_groups(const RatingBlocks& rb, const SideLayout& I, int32_t c, int32_t shard,
                                          int32_t waves, int32_t split_run) {
   const int32_t nb = rb.n_blocks;

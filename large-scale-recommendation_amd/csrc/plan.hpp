@@ -352,6 +352,10 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
                      uint32_t scratch_base = 0, int32_t ustride = 1, bool gmajor = false,
                      std::vector<FastBlockWork>* entries_out = nullptr);
 
+// Longest-processing-time assignment of rows (by load) to G groups, as build_fast_plan's phase 1
+// does for the users and items of a rating block (kernels_plan.hip uses it on device counts).
+void lpt_assign(const std::vector<int64_t>& load, int32_t G, std::vector<int32_t>& group);
+
 // Rotation groups per rating block for the systolic sweep, where every rating block of a
 // superstep is its own G_j x G_j grid and only the superstep's longest wave matters.  For each
 // superstep of this shard it picks the smallest G_j (multiples of 8) that bring every block's

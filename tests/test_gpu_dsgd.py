@@ -605,13 +605,13 @@ def test_stream_rmse_within_half_percent_of_reference(monkeypatch, K):
 
 @pytest.mark.parametrize("k,nb,kind", [(64, 4, "zipf"), (128, 8, "zipf"), (128, 2, "hot"), (256, 4, "zipf")])
 def test_device_plan_equals_host_plan(monkeypatch, k, nb, kind):
-    """The fast schedule's per-cell emission and pair records built on the device
-    (kernels_plan.hip) are bitwise the host's (plan.cpp build_fast_plan + build_pair_plan):
+    """The fast schedule built on the device (kernels_plan.hip: the per-cell emission and pair
+    records, and with MFHIP_DEVICE_PLAN=2 the cell-major order and spreading too) is bitwise the host's (plan.cpp build_fast_plan + build_pair_plan):
     same pair records, wave and systolic tables (digest), same padding and requested bytes, and
     so the same factors after a fit."""
     d = hot_item_data(11) if kind == "hot" else synth.generate(6000, 1500, 400000, seed=17)
     res = {}
-    for flag in ("0", "1"):
+    for flag in ("0", "1", "2"):  # host / device emission / whole schedule on the device
         monkeypatch.setenv("MFHIP_DEVICE_PLAN", flag)
         with mfhip.Context(params(k, 2, nb, 5, mode=L.MODE_FAST_F32)) as ctx:
             ctx.prepare(d.u, d.i, d.r)
@@ -619,7 +619,10 @@ def test_device_plan_equals_host_plan(monkeypatch, k, nb, kind):
             st = ctx.stats()
             ctx.run(2 * nb)
             res[flag] = (dig, st["pads"], st["groups"], ctx.factors(0)[1], ctx.factors(1)[1])
-    h, g = res["0"], res["1"]
-    assert h[1] > 0 and h[0] == g[0], (h[0], g[0])
-    assert h[1:3] == g[1:3]
-    assert np.array_equal(h[3], g[3]) and np.array_equal(h[4], g[4])
+    h = res["0"]
+    assert h[0][1] > 0
+    for flag in ("1", "2"):
+        g = res[flag]
+        assert h[0] == g[0], (flag, h[0], g[0])
+        assert h[1:3] == g[1:3], flag
+        assert np.array_equal(h[3], g[3]) and np.array_equal(h[4], g[4]), flag
