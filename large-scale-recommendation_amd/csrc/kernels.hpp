@@ -118,9 +118,15 @@ class DevBuf;
 // keep (optional): the rating blocks' device arrays (urow u32, irow u32, r f64, rb order, the
 // first rb.start[n*n] entries valid) are handed over instead of freed.
 struct DevRatingBlocks;
+// host_arrays = false (with keep): rb gets only its block starts; fetch_rating_blocks copies the
+// arrays later if a host-side plan needs them.
 void device_blocking(hipStream_t st, const int32_t* u, const int32_t* i, const double* r, int64_t n, int32_t nb,
                      int64_t seed, int32_t ub_lo, int32_t ub_hi, bool sort_ui, SideLayout& U, SideLayout& I,
-                     RatingBlocks& rb, DevRatingBlocks* keep = nullptr);
+                     RatingBlocks& rb, DevRatingBlocks* keep = nullptr, bool host_arrays = true);
+void fetch_rating_blocks(hipStream_t st, const DevRatingBlocks& dr, RatingBlocks& rb);
+// Per rating block (n*n): the rating count of its most rated item, from the device arrays.
+std::vector<int64_t> device_block_tops(hipStream_t st, const DevRatingBlocks& dr, const RatingBlocks& rb,
+                                       const SideLayout& I);
 
 // The fast pair schedule's per-cell work on the device (kernels_plan.hip): the greedy emission of
 // every cell of `work` (build_fast_plan's phase-1 output, blocks in ascending order) and the pair

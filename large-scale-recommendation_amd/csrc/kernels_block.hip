@@ -236,7 +236,7 @@ void block_side(hipStream_t st, Temp& tmp, const int32_t* d_ids, int64_t n, int3
 
 void device_blocking(hipStream_t st, const int32_t* u, const int32_t* i, const double* r, int64_t n, int32_t nb,
                      int64_t seed, int32_t ub_lo, int32_t ub_hi, bool sort_ui, SideLayout& U, SideLayout& I,
-                     RatingBlocks& rb, DevRatingBlocks* keep) {
+                     RatingBlocks& rb, DevRatingBlocks* keep, bool host_arrays) {
   MF_REQUIRE(n < (int64_t{1} << 31), "device blocking sorts with 32-bit indices (< 2^31 ratings)");
   const int64_t nb2 = static_cast<int64_t>(nb) * nb;
   Temp tmp;
@@ -313,10 +313,13 @@ void device_blocking(hipStream_t st, const int32_t* u, const int32_t* i, const d
   MF_HIP(hipMemcpyAsync(rb.start.data(), dstart.get(), static_cast<size_t>(nb2 + 1) * 8, hipMemcpyDeviceToHost, st));
   MF_HIP(hipStreamSynchronize(st));
   const int64_t total = rb.start[nb2];
-  resize_huge(rb.urow, total);
-  resize_huge(rb.irow, total);
-  resize_huge(rb.r, total);
-  if (total > 0) {
+  if (!keep) host_arrays = true;
+  if (host_arrays) {
+    resize_huge(rb.urow, total);
+    resize_huge(rb.irow, total);
+    resize_huge(rb.r, total);
+  }
+  if (total > 0 && host_arrays) {
     MF_HIP(hipMemcpyAsync(rb.urow.data(), gu.get(), total * 4, hipMemcpyDeviceToHost, st));
     MF_HIP(hipMemcpyAsync(rb.irow.data(), gi.get(), total * 4, hipMemcpyDeviceToHost, st));
     MF_HIP(hipMemcpyAsync(rb.r.data(), gr.get(), total * 8, hipMemcpyDeviceToHost, st));

@@ -666,7 +666,69 @@ void emit_and_pair(hipStream_t st, const PlanBlocks& pb, DevBuf& dE, DevBuf& dcs
   for (int64_t x = 0; x < nsub; ++x) pp.sm_bytes[substep_waves ? x / fp.G : x] += sub_bytes[x];
 }
 
+// per rating of the shard's blocks: the per-block item histogram (the group model's top counts)
+__global__ void k_item_hist(const uint32_t* __restrict__ irow, int64_t n, const int64_t* __restrict__ bstart,
+                            int64_t nb2, int32_t nb, const int64_t* __restrict__ ibs, const int64_t* __restrict__ ioff,
+                            int32_t* __restrict__ icnt) {
+  for (int64_t x = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; x < n;
+       x += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    int64_t lo = 0, hi = nb2;
+    while (hi - lo > 1) {
+      const int64_t mid = (lo + hi) / 2;
+      if (bstart[mid] <= x) lo = mid;
+      else hi = mid;
+    }
+    const int32_t b = static_cast<int32_t>(lo);
+    atomicAdd(icnt + ioff[b] + (irow[x] - static_cast<uint32_t>(ibs[b % nb])), 1);
+  }
+}
+
 }  // namespace
+
+std::vector<int64_t> device_block_tops(hipStream_t st, const DevRatingBlocks& dr, const RatingBlocks& rb,
+                                       const SideLayout& I) {
+  const int32_t nb = rb.n_blocks;
+  const int64_t nb2 = static_cast<int64_t>(nb) * nb;
+  std::vector<int64_t> ioff(nb2, 0), top(nb2, 0);
+  int64_t isum = 0;
+  for (int64_t b = 0; b < nb2; ++b) {
+    ioff[b] = isum;
+    if (rb.size(b) > 0) isum += I.block_start[b % nb + 1] - I.block_start[b % nb];
+  }
+  if (dr.total == 0 || isum == 0) return top;
+  DevBuf dbs, dibs, dio, dcnt;
+  upload(dbs, rb.start.data(), rb.start.size(), st);
+  upload(dibs, I.block_start.data(), I.block_start.size(), st);
+  upload(dio, ioff.data(), ioff.size(), st);
+  dcnt.alloc(static_cast<size_t>(isum) * 4);
+  MF_HIP(hipMemsetAsync(dcnt.get(), 0, dcnt.bytes(), st));
+  hipLaunchKernelGGL(k_item_hist, dim3(plan_grid(dr.total)), dim3(256), 0, st, dr.irow.as<uint32_t>(), dr.total,
+                     dbs.as<int64_t>(), nb2, nb, dibs.as<int64_t>(), dio.as<int64_t>(), dcnt.as<int32_t>());
+  MF_HIP(hipGetLastError());
+  std::vector<int32_t> cnt(isum);
+  MF_HIP(hipMemcpyAsync(cnt.data(), dcnt.get(), isum * 4, hipMemcpyDeviceToHost, st));
+  MF_HIP(hipStreamSynchronize(st));
+  for (int64_t b = 0; b < nb2; ++b) {
+    if (rb.size(b) == 0) continue;
+    const int64_t ni = I.block_start[b % nb + 1] - I.block_start[b % nb];
+    int32_t mx = 0;
+    for (int64_t il = 0; il < ni; ++il) mx = std::max(mx, cnt[ioff[b] + il]);
+    top[b] = mx;
+  }
+  return top;
+}
+
+void fetch_rating_blocks(hipStream_t st, const DevRatingBlocks& dr, RatingBlocks& rb) {
+  resize_huge(rb.urow, dr.total);
+  resize_huge(rb.irow, dr.total);
+  resize_huge(rb.r, dr.total);
+  if (dr.total > 0) {
+    MF_HIP(hipMemcpyAsync(rb.urow.data(), dr.urow.get(), dr.total * 4, hipMemcpyDeviceToHost, st));
+    MF_HIP(hipMemcpyAsync(rb.irow.data(), dr.irow.get(), dr.total * 4, hipMemcpyDeviceToHost, st));
+    MF_HIP(hipMemcpyAsync(rb.r.data(), dr.r.get(), dr.total * 8, hipMemcpyDeviceToHost, st));
+  }
+  MF_HIP(hipStreamSynchronize(st));
+}
 
 void device_pair_schedule(hipStream_t st, std::vector<FastBlockWork>& work, FastPlan& fp, int32_t nb, int32_t c,
                           int32_t shard, int32_t k, uint32_t dummy_row, int32_t window, bool substep_waves,

@@ -1119,7 +1119,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
                       choose_fast_kernel(ctx->P.num_factors) == FastKernel::kPair && !want_stream() &&
                       !(dpv0 && (std::string(dpv0) == "0" || std::string(dpv0) == "1"));
     device_blocking(s0.stream, u, i, r, n, ctx->nb, ctx->P.seed, lo, hi, ctx->f64, ctx->U, ctx->I, ctx->rb,
-                    keep ? &dev_rb : nullptr);
+                    keep ? &dev_rb : nullptr, !keep);
     clk.lap("blocking + rating blocks (device)");
   }
   build_model(ctx, u, i, n, on_device);
@@ -1200,7 +1200,16 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
       if (ctx->P.fast_waves == 0 && !(bg && std::string(bg) == "0")) {
         block_groups.assign(nb2, 0);
         for (auto& s : ctx->shards) {
-          const auto gb = choose_block_groups(ctx->rb, ctx->I, ctx->c, s.index, simds, ctx->P.fast_item_split);
+          std::vector<int32_t> gb;
+          if (ctx->rb.urow.empty() && dev_rb.urow.get()) {  // rating blocks on the device only
+            DeviceGuard g(s.device);
+            std::vector<int64_t> size(nb2, 0);
+            for (int64_t b = 0; b < nb2; ++b) size[b] = ctx->rb.size(b);
+            gb = choose_block_groups(size, device_block_tops(s.stream, dev_rb, ctx->rb, ctx->I), ctx->nb, ctx->c,
+                                     s.index, simds);
+          } else {
+            gb = choose_block_groups(ctx->rb, ctx->I, ctx->c, s.index, simds, ctx->P.fast_item_split);
+          }
           for (int64_t b = 0; b < nb2; ++b)
             if (gb[b] > 0) block_groups[b] = gb[b];
         }
@@ -1252,6 +1261,11 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
                            dummy, 2 * kPairRing, dev_pp, dev_pairs);
       dev_rb = DevRatingBlocks();
     } else {
+      if (ctx->rb.urow.empty() && dev_rb.urow.get()) {  // a host-built plan after all
+        Shard& s0 = ctx->shards[0];
+        DeviceGuard g(s0.device);
+        fetch_rating_blocks(s0.stream, dev_rb, ctx->rb);
+      }
       build_fast_plan(fp, ctx->rb, ctx->U, ctx->I, ctx->G_fast, k, ctx->P.lambda,
                       static_cast<uint64_t>(ctx->P.seed) * 0x9E3779B97F4A7C15ULL + 1, dummy, nullptr,
                       ctx->fast_stream ? 2 * ctx->stream_ring : ctx->fast_pair ? 2 * kPairRing : kHazardWindow,
@@ -1622,24 +1636,43 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
     ctx->have_model = true;
   }
   const int k = ctx->P.num_factors;
+  PhaseClock clk;
   std::vector<int32_t> fu, fi;
   std::vector<uint32_t> ur(n), ir(n);
   const int64_t u0 = ctx->U.rows(), i0 = ctx->I.rows();
   std::vector<uint8_t> seen_u, seen_i;
   int64_t cu = 0, ci = 0;
+  // rows of known ids in parallel (the index is only read); then, in rating order, the ids first
+  // seen in this batch get new rows in order of appearance, exactly as one sequential scan would
+  std::vector<int32_t> fr_u(n), fr_i(n);
+  parallel_for(n, [&](int64_t lo2, int64_t hi2, int) {
+    for (int64_t j = lo2; j < hi2; ++j) {
+      fr_u[j] = ctx->U.index.find(u[j]);
+      fr_i[j] = ctx->I.index.find(i[j]);
+    }
+  });
   for (int64_t j = 0; j < n; ++j) {
-    ur[j] = static_cast<uint32_t>(online_row(ctx, ctx->U, u[j], fu));
-    ir[j] = static_cast<uint32_t>(online_row(ctx, ctx->I, i[j], fi));
+    ur[j] = static_cast<uint32_t>(fr_u[j] >= 0 ? fr_u[j] : online_row(ctx, ctx->U, u[j], fu));
+    ir[j] = static_cast<uint32_t>(fr_i[j] >= 0 ? fr_i[j] : online_row(ctx, ctx->I, i[j], fi));
   }
   // touched-row counts (UpdateSeparatedHashMap.updates, OfflineSpark.scala:33-67)
   seen_u.assign(ctx->U.rows(), 0);
   seen_i.assign(ctx->I.rows(), 0);
-  for (int64_t j = 0; j < n; ++j) {
-    if (!seen_u[ur[j]]) { seen_u[ur[j]] = 1; ++cu; }
-    if (!seen_i[ir[j]]) { seen_i[ir[j]] = 1; ++ci; }
-  }
+  std::atomic<int64_t> acu{0}, aci{0};
+  parallel_for(n, [&](int64_t lo2, int64_t hi2, int) {
+    int64_t lu = 0, li = 0;
+    for (int64_t j = lo2; j < hi2; ++j) {  // first writer of a row's flag counts it
+      lu += __atomic_exchange_n(&seen_u[ur[j]], static_cast<uint8_t>(1), __ATOMIC_RELAXED) == 0;
+      li += __atomic_exchange_n(&seen_i[ir[j]], static_cast<uint8_t>(1), __ATOMIC_RELAXED) == 0;
+    }
+    acu += lu;
+    aci += li;
+  });
+  cu = acu;
+  ci = aci;
   if (tu) *tu = cu;
   if (ti) *ti = ci;
+  clk.lap("online: id lookup + touched rows");
   // new rows take the slab rows the fast DSGD schedule keeps zeroed (padding / idle prefetch
   // rows past the real ones): that schedule is void now, a further fit must prepare again
   if (ctx->prepared && !ctx->f64 && (!fu.empty() || !fi.empty())) ctx->prepared = false;
@@ -1693,7 +1726,9 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
   LevelPlan lp;
   const bool outs = uout || iout;
   std::vector<int32_t> src;
+  clk.lap("online: new rows + order");
   build_level_plan({sq}, lp, outs ? &src : nullptr);
+  clk.lap("online: level plan");
   DeviceGuard g(s.device);
   const size_t bytes = lp.entries.size() * sizeof(DetEntry);
   MF_HIP(hipStreamSynchronize(s.stream));
@@ -1722,7 +1757,9 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
                    s.regi.get(), k, ctx->P.online_learning_rate, Arith::kSgdNext, ctx->f64);
   }
   MF_HIP(hipGetLastError());
+  clk.lap("online: H2D + level launches queued");
   MF_HIP(hipStreamSynchronize(s.stream));
+  clk.lap("online: kernels done");
   if (uout) MF_HIP(hipMemcpy(uout, duo.get(), obytes, hipMemcpyDeviceToHost));
   if (iout) MF_HIP(hipMemcpy(iout, dio.get(), obytes, hipMemcpyDeviceToHost));
   ctx->stats.levels += lp.levels();

@@ -1428,7 +1428,6 @@ std::vector<int32_t> choose_block_groups(const RatingBlocks& rb, const SideLayou
                                          int32_t waves, int32_t split_run) {
   const int32_t nb = rb.n_blocks;
   const int64_t nb2 = static_cast<int64_t>(nb) * nb;
-  std::vector<int32_t> Gb(nb2, 0);
   std::vector<int64_t> size(nb2, 0), top(nb2, 0);  // ratings, ratings of the most rated item
   parallel_tasks(nb2, [&](int64_t b) {
     const int32_t p = static_cast<int32_t>(b / nb), q = static_cast<int32_t>(b % nb);
@@ -1440,6 +1439,13 @@ std::vector<int32_t> choose_block_groups(const RatingBlocks& rb, const SideLayou
     size[b] = rb.size(b);
     top[b] = split_run > 0 ? std::min(mx, split_run) : mx;
   });
+  return choose_block_groups(size, top, nb, c, shard, waves);
+}
+
+std::vector<int32_t> choose_block_groups(const std::vector<int64_t>& size, const std::vector<int64_t>& top, int32_t nb,
+                                         int32_t c, int32_t shard, int32_t waves) {
+  const int64_t nb2 = static_cast<int64_t>(nb) * nb;
+  std::vector<int32_t> Gb(nb2, 0);
   double cell_ns = kSysCellNs, pair_ns = kSysPairNs, run_ns = kSysRunPairNs;
   if (const char* v = std::getenv("MFHIP_SYS_MODEL"))  // tuning knob: "cell_ns,pair_ns,run_pair_ns"
     std::sscanf(v, "%lf,%lf,%lf", &cell_ns, &pair_ns, &run_ns);

@@ -368,5 +368,9 @@ constexpr double kSysRunPairNs = 186.0;   // single-item-run pair step (wave tra
 // split_run > 0: an item's run counts at most split_run ratings (hot-item replicas).
 std::vector<int32_t> choose_block_groups(const RatingBlocks& rb, const SideLayout& I, int32_t c, int32_t shard,
                                          int32_t waves, int32_t split_run = 0);
+// The same model on per-block rating counts and most-rated-item counts (size / top, n*n each,
+// shard blocks only; e.g. from device histograms, kernels_plan.hip device_block_tops).
+std::vector<int32_t> choose_block_groups(const std::vector<int64_t>& size, const std::vector<int64_t>& top, int32_t nb,
+                                         int32_t c, int32_t shard, int32_t waves);
 
 }  // namespace mfhip
