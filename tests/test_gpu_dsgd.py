@@ -603,13 +603,19 @@ def test_stream_rmse_within_half_percent_of_reference(monkeypatch, K):
     assert abs(fast - ref) / ref < 0.005, (fast, ref)
 
 
-@pytest.mark.parametrize("k,nb,kind", [(64, 4, "zipf"), (128, 8, "zipf"), (128, 2, "hot"), (256, 4, "zipf")])
+@pytest.mark.parametrize("k,nb,kind", [(64, 4, "zipf"), (128, 8, "zipf"), (128, 2, "hot"), (256, 4, "zipf"),
+                                       (64, 8, "tiny")])
 def test_device_plan_equals_host_plan(monkeypatch, k, nb, kind):
     """The fast schedule built on the device (kernels_plan.hip: the per-cell emission and pair
     records, and with MFHIP_DEVICE_PLAN=2 the cell-major order and spreading too) is bitwise the host's (plan.cpp build_fast_plan + build_pair_plan):
     same pair records, wave and systolic tables (digest), same padding and requested bytes, and
     so the same factors after a fit."""
-    d = hot_item_data(11) if kind == "hot" else synth.generate(6000, 1500, 400000, seed=17)
+    if kind == "hot":
+        d = hot_item_data(11)
+    elif kind == "tiny":  # empty rating blocks and empty cells
+        d = synth.generate(60, 40, 300, seed=23)
+    else:
+        d = synth.generate(6000, 1500, 400000, seed=17)
     res = {}
     for flag in ("0", "1", "2"):  # host / device emission / whole schedule on the device
         monkeypatch.setenv("MFHIP_DEVICE_PLAN", flag)
