@@ -20,6 +20,13 @@ enum class Arith : int {
 // (kDsgd) or SGDUpdater's learningRate (kSgdNext).
 void launch_level(hipStream_t st, const DetEntry* entries, int64_t n, void* U, void* I,
                   const void* regU, const void* regI, int k, double eta, Arith arith, bool f64);
+// Online micro-batch as one persistent launch (k_online_sweep, kernels_det.hip): wave w applies
+// entries [wbeg[w], wbeg[w+1]) (the updates of its items, in sequence order), each after its
+// user's ticket reaches useq; tickets (one int32 per user row) start at 0.  Every wave must be
+// resident: nw <= online_sweep_capacity(k, f64).
+int online_sweep_capacity(int k, bool f64);
+void launch_online_sweep(hipStream_t st, int nw, const int64_t* wbeg, const DetEntry* ent, const uint32_t* useq,
+                         void* U, void* I, int k, double eta, bool f64, int32_t* ticket, int32_t* err);
 // Per-rating records of the online operators (mf_online_update_out), f64 rows of k at
 // [src[entry] * k]: kOutNext = (user', item') (FlinkOnlineMF.scala:131-135), kOutDelta =
 // (user + deltaItem, deltaItem) with user before the update (PSOfflineOnlineMF.scala:174-176).

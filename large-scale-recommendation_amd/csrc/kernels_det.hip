@@ -87,6 +87,71 @@ __global__ __launch_bounds__(256) void k_level(const DetEntry* __restrict__ ent,
   }
 }
 
+// Online micro-batch in ONE launch (SGDUpdater.nextFactors, core/FactorUpdater.scala:37-45, in
+// sequence order): wave w applies, in order, every update of the items it owns, so an item's
+// updates follow program order; an update waits for the earlier updates of its user (other waves)
+// through a per-user ticket -- the count of that user's updates done in this batch -- and runs
+// when it equals its useq.  The unfinished update earliest in the sequence is always runnable,
+// so with every wave resident the launch cannot deadlock.  Hand-off as in kernels_detsweep.hip
+// (MI355X_MICROARCH.md, inter-workgroup visibility, valid forms row 1): rows are loaded and
+// stored with agent-scope relaxed atomics (sc1), the wave drains its stores, then lane 0 stores
+// the ticket.  The per-update arithmetic is k_level's (kSgdNext), so the factors are bitwise the
+// level-by-level replay (tests/test_gpu_online.py).  A wait over ~1 s sets err and the wave leaves.
+template <typename T, int KPL>
+__global__ __launch_bounds__(64) void k_online_sweep(const int64_t* __restrict__ wbeg, const DetEntry* __restrict__ ent,
+                                                     const uint32_t* __restrict__ useq, T* U, T* I, int k, T eta,
+                                                     int32_t* ticket, int32_t* err) {
+  const int lane = threadIdx.x;
+  const int64_t j0 = wbeg[blockIdx.x], j1 = wbeg[blockIdx.x + 1];
+  for (int64_t j = j0; j < j1; ++j) {
+    const uint32_t ur = ent[j].u, ir = ent[j].i;
+    const int32_t q = static_cast<int32_t>(useq[j]);
+    const T r = static_cast<T>(ent[j].r);
+    if (q > 0) {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (__builtin_amdgcn_readfirstlane(
+                 __hip_atomic_load(ticket + ur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != q) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {  // 100 MHz clock: ~1 s
+          if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          return;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    T* p = U + static_cast<size_t>(ur) * k;
+    T* qi = I + static_cast<size_t>(ir) * k;
+    T pv[KPL], qv[KPL], pr[KPL];
+#pragma unroll
+    for (int c = 0; c < KPL; ++c) {
+      const int f = lane + 64 * c;
+      pv[c] = f < k ? __hip_atomic_load(p + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : T(0);
+      qv[c] = f < k ? __hip_atomic_load(qi + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : T(0);
+      pr[c] = pv[c] * qv[c];
+    }
+    const T e = r - seq_dot<T, KPL>(pr, k);
+    const T le = eta * e;  // learningRate * e * i == (learningRate * e) * i
+#pragma unroll
+    for (int c = 0; c < KPL; ++c) {
+      const int f = lane + 64 * c;
+      if (f < k) {
+        __hip_atomic_store(p + f, pv[c] + le * qv[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(qi + f, qv[c] + le * pv[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this update's rows have landed
+    if (lane == 0) __hip_atomic_store(ticket + ur, q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+template <typename T, int KPL>
+int online_capacity() {
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_online_sweep<T, KPL>, 64, 0) != hipSuccess) return 0;
+  return cus * per_cu;
+}
+
 // k_level's SGDUpdater arithmetic (core/FactorUpdater.scala:37-53) plus the per-rating record
 // the online operator emits, f64 row src[j] of uout / iout (either may be null):
 //   OUT == 1: (user', item'), FlinkOnlineMF.ItemOperator's collect (:131-135)
@@ -280,6 +345,33 @@ void level_out_dispatch(hipStream_t st, const DetEntry* e, int64_t n, void* U, v
   else if (k <= 128) hipLaunchKernelGGL((k_level_out<T, 2, OUT>), grid, block, 0, st, e, n, u, i, k, et, src, uo, io);
   else if (k <= 256) hipLaunchKernelGGL((k_level_out<T, 4, OUT>), grid, block, 0, st, e, n, u, i, k, et, src, uo, io);
   else hipLaunchKernelGGL((k_level_out<T, 8, OUT>), grid, block, 0, st, e, n, u, i, k, et, src, uo, io);
+}
+
+int online_sweep_capacity(int k, bool f64) {
+  if (f64) return k <= 64 ? online_capacity<double, 1>() : k <= 128 ? online_capacity<double, 2>()
+                : k <= 256 ? online_capacity<double, 4>() : online_capacity<double, 8>();
+  return k <= 64 ? online_capacity<float, 1>() : k <= 128 ? online_capacity<float, 2>()
+         : k <= 256 ? online_capacity<float, 4>() : online_capacity<float, 8>();
+}
+
+void launch_online_sweep(hipStream_t st, int nw, const int64_t* wbeg, const DetEntry* ent, const uint32_t* useq,
+                         void* U, void* I, int k, double eta, bool f64, int32_t* ticket, int32_t* err) {
+  if (nw <= 0) return;
+  const dim3 g(static_cast<unsigned>(nw)), b(64);
+#define MF_OS(T, KPL) hipLaunchKernelGGL((k_online_sweep<T, KPL>), g, b, 0, st, wbeg, ent, useq, static_cast<T*>(U), \
+                                         static_cast<T*>(I), k, static_cast<T>(eta), ticket, err)
+  if (f64) {
+    if (k <= 64) MF_OS(double, 1);
+    else if (k <= 128) MF_OS(double, 2);
+    else if (k <= 256) MF_OS(double, 4);
+    else MF_OS(double, 8);
+  } else {
+    if (k <= 64) MF_OS(float, 1);
+    else if (k <= 128) MF_OS(float, 2);
+    else if (k <= 256) MF_OS(float, 4);
+    else MF_OS(float, 8);
+  }
+#undef MF_OS
 }
 
 void launch_level_out(hipStream_t st, const DetEntry* entries, int64_t n, void* U, void* I, int k, double eta, bool f64,

@@ -1712,6 +1712,56 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
         order.insert(order.end(), c.begin(), c.end());
       }
   }
+  const bool outs = uout || iout;
+  const char* okv = std::getenv("MFHIP_ONLINE_KERNEL");
+  if (!outs && !(okv && std::string(okv) == "level")) {
+    // one persistent launch (k_online_sweep): items spread over the waves, each wave's updates in
+    // sequence order, and per update the number of earlier updates of its user (its ticket value)
+    DeviceGuard g(s.device);
+    const int cap = online_sweep_capacity(k, ctx->f64);
+    const int64_t W = std::max<int64_t>(1, std::min<int64_t>({static_cast<int64_t>(cap / 2), 4096, n}));
+    std::vector<int64_t> wbeg(W + 1, 0);
+    for (int64_t x = 0; x < n; ++x) wbeg[ir[order[x]] % W + 1]++;
+    for (int64_t w = 0; w < W; ++w) wbeg[w + 1] += wbeg[w];
+    std::vector<int64_t> cur(wbeg.begin(), wbeg.end() - 1);
+    std::vector<uint32_t> ucnt(ctx->U.rows(), 0);
+    MF_HIP(hipStreamSynchronize(s.stream));
+    const size_t ebytes = static_cast<size_t>(n) * sizeof(DetEntry), qbytes = static_cast<size_t>(n) * 4;
+    s.det_pin.alloc(ebytes + qbytes);
+    DetEntry* he = s.det_pin.as<DetEntry>();
+    uint32_t* hq = reinterpret_cast<uint32_t*>(s.det_pin.as<char>() + ebytes);
+    for (int64_t x = 0; x < n; ++x) {
+      const int32_t j = order[x];
+      const int64_t y = cur[ir[j] % W]++;
+      he[y] = DetEntry{ur[j], ir[j], r[j]};
+      hq[y] = ucnt[ur[j]]++;
+    }
+    clk.lap("online: sweep plan");
+    s.det_dev.alloc(ebytes + qbytes);
+    MF_HIP(hipMemcpyAsync(s.det_dev.get(), s.det_pin.as<void>(), ebytes + qbytes, hipMemcpyHostToDevice, s.stream));
+    DevBuf dwb, dticket, derr;
+    dwb.alloc(wbeg.size() * 8);
+    MF_HIP(hipMemcpyAsync(dwb.get(), wbeg.data(), wbeg.size() * 8, hipMemcpyHostToDevice, s.stream));
+    dticket.alloc(static_cast<size_t>(std::max<int64_t>(ctx->U.rows(), 1)) * 4);
+    MF_HIP(hipMemsetAsync(dticket.get(), 0, dticket.bytes(), s.stream));
+    derr.alloc(4);
+    MF_HIP(hipMemsetAsync(derr.get(), 0, 4, s.stream));
+    {
+      LaunchTimer t(s, ctx->profiling);
+      launch_online_sweep(s.stream, static_cast<int>(W), dwb.as<int64_t>(), s.det_dev.as<DetEntry>(),
+                          reinterpret_cast<const uint32_t*>(s.det_dev.as<char>() + ebytes), s.uf.get(), s.itf.get(), k,
+                          ctx->P.online_learning_rate, ctx->f64, dticket.as<int32_t>(), derr.as<int32_t>());
+    }
+    MF_HIP(hipGetLastError());
+    int32_t err = 0;
+    MF_HIP(hipMemcpyAsync(&err, derr.get(), 4, hipMemcpyDeviceToHost, s.stream));
+    MF_HIP(hipStreamSynchronize(s.stream));
+    clk.lap("online: sweep (device)");
+    if (err) fail(MF_ERR_TIMEOUT, "online sweep: a ticket wait timed out");
+    ctx->stats.kernel_launches += 1;
+    ctx->stats.updates += n;
+    return;
+  }
   std::vector<double> rr(r, r + n);
   OrderedSeq sq;
   sq.u = ur.data();
@@ -1724,7 +1774,6 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
   sq.i_lo = 0;
   sq.i_hi = static_cast<uint32_t>(ctx->I.rows());
   LevelPlan lp;
-  const bool outs = uout || iout;
   std::vector<int32_t> src;
   clk.lap("online: new rows + order");
   build_level_plan({sq}, lp, outs ? &src : nullptr);

@@ -173,3 +173,28 @@ def test_per_rating_outputs_bit_exact(flavour, name):
     assert np.array_equal(fi[1], np.array([items[x] for x in fi[0].tolist()]))
     with mfhip.Context(p) as ctx, pytest.raises(mfhip.MFError, match="touched rows"):
         ctx.online_update_out(u[:10], i[:10], r[:10], L.ONLINE_SPARK_SWEEP)
+
+
+@pytest.mark.parametrize("mode,k", [(L.MODE_FAST_F32, 128), (L.MODE_DETERMINISTIC_F64, 200), (L.MODE_FAST_F32, 40)])
+def test_online_sweep_equals_level_replay(monkeypatch, mode, k):
+    """The one-launch online sweep (per-item waves, per-user tickets, k_online_sweep) gives the
+    factors of the level-by-level replay (MFHIP_ONLINE_KERNEL=level) bit for bit, including a hot
+    item, repeated (user, item) pairs and ids first seen in a later batch."""
+    rng = np.random.default_rng(7)
+    n = 120000
+    u = rng.integers(0, 5000, n).astype(np.int32)
+    i = (rng.zipf(1.2, n) % 2000).astype(np.int32)
+    i[::37] = 3  # a hot item
+    r = rng.integers(1, 6, n).astype(np.float64)
+    res = {}
+    for kern in ("level", "sweep"):
+        monkeypatch.setenv("MFHIP_ONLINE_KERNEL", kern)
+        p = L.default_params()
+        p.num_factors, p.mode, p.online_learning_rate = k, mode, 0.01
+        with mfhip.Context(p) as ctx:
+            for s in range(0, n, 40000):
+                ctx.online_update(u[s:s + 40000], i[s:s + 40000], r[s:s + 40000], L.ONLINE_NEXT_FACTORS)
+            res[kern] = (ctx.factors(0), ctx.factors(1))
+    for side in (0, 1):
+        assert np.array_equal(res["level"][side][0], res["sweep"][side][0])
+        assert np.array_equal(res["level"][side][1], res["sweep"][side][1])
