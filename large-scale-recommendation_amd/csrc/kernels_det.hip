@@ -103,42 +103,87 @@ __global__ __launch_bounds__(64) void k_online_sweep(const int64_t* __restrict__
                                                      int32_t* ticket, int32_t* err) {
   const int lane = threadIdx.x;
   const int64_t j0 = wbeg[blockIdx.x], j1 = wbeg[blockIdx.x + 1];
+  if (j0 >= j1) return;
+  auto ld = [&](const T* row, int c) {
+    const int f = lane + 64 * c;
+    return f < k ? __hip_atomic_load(row + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : T(0);
+  };
+  auto wait_ticket = [&](uint32_t ur, int32_t q) -> bool {
+    if (q == 0) return true;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(ticket + ur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != q) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {  // 100 MHz clock: ~1 s
+        if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return false;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    return true;
+  };
+  // the item row stays in registers while consecutive updates of this wave share the item (a hot
+  // item's chain); the next update's user row is loaded ahead when its ticket is already due
+  T qv[KPL], pn[KPL];
+  bool have_q = false, have_pn = false;
+  uint32_t cur_i = 0;
   for (int64_t j = j0; j < j1; ++j) {
     const uint32_t ur = ent[j].u, ir = ent[j].i;
     const int32_t q = static_cast<int32_t>(useq[j]);
     const T r = static_cast<T>(ent[j].r);
-    if (q > 0) {
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      while (__builtin_amdgcn_readfirstlane(
-                 __hip_atomic_load(ticket + ur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != q) {
-        if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {  // 100 MHz clock: ~1 s
-          if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          return;
-        }
-        __builtin_amdgcn_s_sleep(1);
+    T* p = U + static_cast<size_t>(ur) * k;
+    T pv[KPL], pr[KPL];
+    if (have_pn) {
+#pragma unroll
+      for (int c = 0; c < KPL; ++c) pv[c] = pn[c];
+    } else {
+      if (!wait_ticket(ur, q)) return;
+#pragma unroll
+      for (int c = 0; c < KPL; ++c) pv[c] = ld(p, c);
+    }
+    if (!have_q || ir != cur_i) {
+      const T* qi = I + static_cast<size_t>(ir) * k;
+#pragma unroll
+      for (int c = 0; c < KPL; ++c) qv[c] = ld(qi, c);
+      cur_i = ir;
+      have_q = true;
+    }
+    // the next update's user row, if it does not wait on anyone (or its ticket is already due)
+    have_pn = false;
+    if (j + 1 < j1) {
+      const uint32_t un = ent[j + 1].u;
+      const int32_t qn = static_cast<int32_t>(useq[j + 1]);
+      if (un != ur &&
+          (qn == 0 || __builtin_amdgcn_readfirstlane(
+                          __hip_atomic_load(ticket + un, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == qn)) {
+        const T* pnr = U + static_cast<size_t>(un) * k;
+#pragma unroll
+        for (int c = 0; c < KPL; ++c) pn[c] = ld(pnr, c);
+        have_pn = true;
       }
     }
-    T* p = U + static_cast<size_t>(ur) * k;
-    T* qi = I + static_cast<size_t>(ir) * k;
-    T pv[KPL], qv[KPL], pr[KPL];
 #pragma unroll
-    for (int c = 0; c < KPL; ++c) {
-      const int f = lane + 64 * c;
-      pv[c] = f < k ? __hip_atomic_load(p + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : T(0);
-      qv[c] = f < k ? __hip_atomic_load(qi + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : T(0);
-      pr[c] = pv[c] * qv[c];
-    }
+    for (int c = 0; c < KPL; ++c) pr[c] = pv[c] * qv[c];
     const T e = r - seq_dot<T, KPL>(pr, k);
     const T le = eta * e;  // learningRate * e * i == (learningRate * e) * i
+    T qnew[KPL];
 #pragma unroll
     for (int c = 0; c < KPL; ++c) {
       const int f = lane + 64 * c;
-      if (f < k) {
-        __hip_atomic_store(p + f, pv[c] + le * qv[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(qi + f, qv[c] + le * pv[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+      qnew[c] = qv[c] + le * pv[c];
+      if (f < k) __hip_atomic_store(p + f, pv[c] + le * qv[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this update's rows have landed
+#pragma unroll
+    for (int c = 0; c < KPL; ++c) qv[c] = qnew[c];
+    // the item row is written back when the wave's next update is on another item (or at the end)
+    if (j + 1 == j1 || ent[j + 1].i != ir) {
+      T* qi = I + static_cast<size_t>(ir) * k;
+#pragma unroll
+      for (int c = 0; c < KPL; ++c) {
+        const int f = lane + 64 * c;
+        if (f < k) __hip_atomic_store(qi + f, qv[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      have_q = false;
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this update's user row has landed
     if (lane == 0) __hip_atomic_store(ticket + ur, q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }

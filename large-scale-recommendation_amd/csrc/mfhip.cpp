@@ -1720,22 +1720,29 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
     DeviceGuard g(s.device);
     const int cap = online_sweep_capacity(k, ctx->f64);
     const int64_t W = std::max<int64_t>(1, std::min<int64_t>({static_cast<int64_t>(cap / 2), 4096, n}));
+    const uint32_t W32 = static_cast<uint32_t>(W);
+    std::vector<uint32_t> wv(n);  // wave of each update in sequence order
     std::vector<int64_t> wbeg(W + 1, 0);
-    for (int64_t x = 0; x < n; ++x) wbeg[ir[order[x]] % W + 1]++;
+    for (int64_t x = 0; x < n; ++x) {
+      wv[x] = ir[order[x]] % W32;
+      wbeg[wv[x] + 1]++;
+    }
     for (int64_t w = 0; w < W; ++w) wbeg[w + 1] += wbeg[w];
     std::vector<int64_t> cur(wbeg.begin(), wbeg.end() - 1);
     std::vector<uint32_t> ucnt(ctx->U.rows(), 0);
-    MF_HIP(hipStreamSynchronize(s.stream));
     const size_t ebytes = static_cast<size_t>(n) * sizeof(DetEntry), qbytes = static_cast<size_t>(n) * 4;
-    s.det_pin.alloc(ebytes + qbytes);
-    DetEntry* he = s.det_pin.as<DetEntry>();
-    uint32_t* hq = reinterpret_cast<uint32_t*>(s.det_pin.as<char>() + ebytes);
+    std::vector<char> stage(ebytes + qbytes);  // built in cached memory, then one copy to the pinned buffer
+    DetEntry* he = reinterpret_cast<DetEntry*>(stage.data());
+    uint32_t* hq = reinterpret_cast<uint32_t*>(stage.data() + ebytes);
     for (int64_t x = 0; x < n; ++x) {
       const int32_t j = order[x];
-      const int64_t y = cur[ir[j] % W]++;
+      const int64_t y = cur[wv[x]]++;
       he[y] = DetEntry{ur[j], ir[j], r[j]};
       hq[y] = ucnt[ur[j]]++;
     }
+    MF_HIP(hipStreamSynchronize(s.stream));
+    s.det_pin.alloc(ebytes + qbytes);
+    std::memcpy(s.det_pin.as<void>(), stage.data(), ebytes + qbytes);
     clk.lap("online: sweep plan");
     s.det_dev.alloc(ebytes + qbytes);
     MF_HIP(hipMemcpyAsync(s.det_dev.get(), s.det_pin.as<void>(), ebytes + qbytes, hipMemcpyHostToDevice, s.stream));
