@@ -203,7 +203,7 @@ def online_leg(ctx, synth, nu, ni, a, batch=1_000_000):
     """BASELINE config 5: streaming micro-batches on top of the offline DSGD model just fitted.
     Each batch: SGDUpdater.nextFactors in arrival order with per-user FIFO (FlinkOnlineMF.scala:
     52-137; core/FactorUpdater.scala:37-45), unseen ids initialised on first touch; timed end to
-    end (host id lookup, sweep plan, H2D, the persistent kernel, sync)."""
+    end (host id lookup, dependency-level plan, H2D, kernels, sync)."""
     import numpy as np
     from mfhip import _lib as L
     stream = synth.generate(max(1, int(nu * a.scale)), max(1, int(ni * a.scale)), batch * a.online_batches,
@@ -222,8 +222,8 @@ def online_leg(ctx, synth, nu, ni, a, batch=1_000_000):
             "batch": batch, "batches": a.online_batches, "launches_median": float(np.median(levels)),
             "flavour": "FlinkOnlineMF / SGDUpdater.nextFactors (lr 0.01)", "target": 10e6,
             "dtype": "f32" if a.mode == "fast" else "f64",
-            "kernel": "k_online_sweep (per-item waves, per-user tickets, one launch per batch)",
-            "timing": "end to end per micro-batch: host id lookup, sweep plan, H2D, kernel, sync"}
+            "kernel": "k_level (one launch per dependency level)",
+            "timing": "end to end per micro-batch: host id lookup, dependency-level plan, H2D, kernels, sync"}
 
 
 def main():

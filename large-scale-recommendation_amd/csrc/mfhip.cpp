@@ -1713,8 +1713,10 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
       }
   }
   const bool outs = uout || iout;
+  // MFHIP_ONLINE_KERNEL=sweep: one persistent launch instead of the level-by-level replay
+  // (opt-in: measured slower end to end on NFLX 1M-rating batches)
   const char* okv = std::getenv("MFHIP_ONLINE_KERNEL");
-  if (!outs && !(okv && std::string(okv) == "level")) {
+  if (!outs && okv && std::string(okv) == "sweep") {
     // one persistent launch (k_online_sweep): items spread over the waves, each wave's updates in
     // sequence order, and per update the number of earlier updates of its user (its ticket value)
     DeviceGuard g(s.device);

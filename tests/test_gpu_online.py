@@ -177,9 +177,9 @@ def test_per_rating_outputs_bit_exact(flavour, name):
 
 @pytest.mark.parametrize("mode,k", [(L.MODE_FAST_F32, 128), (L.MODE_DETERMINISTIC_F64, 200), (L.MODE_FAST_F32, 40)])
 def test_online_sweep_equals_level_replay(monkeypatch, mode, k):
-    """The one-launch online sweep (per-item waves, per-user tickets, k_online_sweep) gives the
-    factors of the level-by-level replay (MFHIP_ONLINE_KERNEL=level) bit for bit, including a hot
-    item, repeated (user, item) pairs and ids first seen in a later batch."""
+    """The opt-in one-launch online sweep (MFHIP_ONLINE_KERNEL=sweep: per-item waves, per-user
+    tickets, k_online_sweep) gives the factors of the default level-by-level replay bit for bit,
+    including a hot item, repeated (user, item) pairs and ids first seen in a later batch."""
     rng = np.random.default_rng(7)
     n = 120000
     u = rng.integers(0, 5000, n).astype(np.int32)
