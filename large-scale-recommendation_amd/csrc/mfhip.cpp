@@ -1030,49 +1030,6 @@ void reset_item_loc(mf_ctx* ctx) {
       }
 }
 
-// MFHIP_SYS_PLACE (experiment): inside each XCD's range of a superstep's systolic waves
-// (k_sweep_pair_sys maps blockIdx b to XCD b % 8, position b / 8), the heaviest waves take the
-// first 32 positions and the lightest the next 32, so that with the CUs filled round-robin a heavy
-// wave shares its CU with a light one.  Only positions change: the progress-word neighbours are
-// remapped, the cells and their order are the same (results identical).
-void place_sys_waves(PairPlan& pp) {
-  const int64_t nsm = static_cast<int64_t>(pp.sys_off.size()) - 1;
-  for (int64_t sm = 0; sm < nsm; ++sm) {
-    const int64_t w0 = pp.sys_off[sm], nw = pp.sys_off[sm + 1] - w0;
-    if (nw <= 0) continue;
-    std::vector<double> wt(nw, 0.0);
-    for (int64_t w = 0; w < nw; ++w) {
-      const SysWave& sw = pp.sys_waves[w0 + w];
-      for (int32_t t = 0; t < sw.G; ++t) {
-        const WaveDesc& d = pp.sys[sw.cell0 + t];
-        wt[w] += d.steps * (d.cells == kWaveSingleRun ? 0.7 : 1.0);
-      }
-    }
-    std::vector<int64_t> newpos(nw);  // old index -> new index
-    const int64_t per = nw / 8, extra = nw % 8;
-    for (int64_t x = 0; x < 8; ++x) {
-      const int64_t b0 = x * per + std::min(x, extra), cnt = per + (x < extra ? 1 : 0);
-      std::vector<int64_t> ids(cnt);
-      std::iota(ids.begin(), ids.end(), b0);
-      std::stable_sort(ids.begin(), ids.end(), [&](int64_t a, int64_t b) { return wt[a] > wt[b]; });
-      std::vector<int64_t> slot(cnt);  // rank order -> position
-      int64_t y = 0;
-      const int64_t heavy = std::min<int64_t>(32, cnt), light = std::min<int64_t>(32, cnt - heavy);
-      for (int64_t q = 0; q < heavy; ++q) slot[y++] = q;                       // heaviest: positions 0..31
-      for (int64_t q = 0; q < cnt - heavy - light; ++q) slot[y++] = 64 + q;    // middle: 64..
-      for (int64_t q = 0; q < light; ++q) slot[y++] = 32 + (light - 1 - q);     // lightest: 32..63
-      for (int64_t q = 0; q < cnt; ++q) newpos[ids[q]] = b0 + slot[q];
-    }
-    std::vector<SysWave> nsw(nw);
-    for (int64_t w = 0; w < nw; ++w) {
-      SysWave sw = pp.sys_waves[w0 + w];
-      sw.nbr = static_cast<int32_t>(newpos[sw.nbr]);
-      nsw[newpos[w]] = sw;
-    }
-    std::copy(nsw.begin(), nsw.end(), pp.sys_waves.begin() + w0);
-  }
-}
-
 // MFHIP_TIMING=1: host phases of prepare on stderr.
 struct PhaseClock {
   bool on = std::getenv("MFHIP_TIMING") != nullptr;
@@ -1435,7 +1392,6 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
           s.st_sys.alloc(std::max<size_t>(pp.sys.size(), 1) * sizeof(WaveDesc));
           if (!pp.sys.empty())
             MF_HIP(hipMemcpy(s.st_sys.get(), pp.sys.data(), pp.sys.size() * sizeof(WaveDesc), hipMemcpyHostToDevice));
-          if (!ctx->ring_overlap && std::getenv("MFHIP_SYS_PLACE")) place_sys_waves(pp);
           s.st_sysw.alloc(std::max<size_t>(pp.sys_waves.size(), 1) * sizeof(SysWave));
           if (!pp.sys_waves.empty())
             MF_HIP(hipMemcpy(s.st_sysw.get(), pp.sys_waves.data(), pp.sys_waves.size() * sizeof(SysWave),
