@@ -316,7 +316,8 @@ def main():
         ksec = st_p["kernel_ms"] / 1e3
         achieved = st_p["moved_bytes"] / ksec / 1e9  # GB/s, this rank's sweep kernel
         kname = L.lib().mf_fast_kernel_name(k).decode() if a.mode == "fast" else "k_level"
-        traffic, traffic_src = pmc_traffic(a, k, st["groups"], kname)
+        # the committed PMC summaries are one-GPU runs: a rank of an N-GPU ring runs other launches
+        traffic, traffic_src = pmc_traffic(a, k, st["groups"], kname) if D.world == 1 else (None, None)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kname,
                 "bytes_per_launch": round(st_p["moved_bytes"] / max(launches, 1)),
