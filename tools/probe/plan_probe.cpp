@@ -144,6 +144,27 @@ int main(int argc, char** argv) {
   build_pair_plan(pp, fp, nb, nb, 0, k, false);
   std::printf("pair plan %.3f s\n", lap());
   std::printf("pads %lld noop halves %lld pairs %zu\n", (long long)fp.pads, (long long)pp.noop_halves, pp.recs.size());
+  {  // out-of-range operations per pair step, generic vs single-run waves
+    int64_t gen_pairs = 0, gen_oob[8] = {0}, run_pairs = 0, run_oob = 0;
+    for (const WaveDesc& w : pp.waves)
+      for (int64_t x = w.base; x < w.base + w.steps; ++x) {
+        const PairRec& r = pp.recs[x];
+        if (w.cells == kWaveSingleRun) {
+          ++run_pairs;
+          run_oob += (r.ua == kOffOOB) + (r.ub == kOffOOB) + (r.sa == kOffOOB) + (r.sb == kOffOOB);
+        } else {
+          ++gen_pairs;
+          const uint32_t o[8] = {r.ua, r.ub, r.ia, r.ib, r.sa, r.sb, r.sia, r.si};
+          for (int y = 0; y < 8; ++y) gen_oob[y] += o[y] == kOffOOB;
+        }
+      }
+    std::printf("generic pairs %lld: out-of-range ua %.2f ub %.2f ia %.2f ib %.2f sa %.2f sb %.2f sia %.2f si %.2f\n",
+                (long long)gen_pairs, gen_oob[0] / double(gen_pairs), gen_oob[1] / double(gen_pairs),
+                gen_oob[2] / double(gen_pairs), gen_oob[3] / double(gen_pairs), gen_oob[4] / double(gen_pairs),
+                gen_oob[5] / double(gen_pairs), gen_oob[6] / double(gen_pairs), gen_oob[7] / double(gen_pairs));
+    std::printf("single-run pairs %lld: out-of-range per pair %.2f of 4\n", (long long)run_pairs,
+                run_oob / double(std::max<int64_t>(run_pairs, 1)));
+  }
   {  // fingerprint of the plans (FNV-1a over the records, cell offsets and pair records)
     uint64_t h = 1469598103934665603ull;
     auto mix = [&](const void* p, size_t n) {
