@@ -164,6 +164,20 @@ int main(int argc, char** argv) {
                 gen_oob[5] / double(gen_pairs), gen_oob[6] / double(gen_pairs), gen_oob[7] / double(gen_pairs));
     std::printf("single-run pairs %lld: out-of-range per pair %.2f of 4\n", (long long)run_pairs,
                 run_oob / double(std::max<int64_t>(run_pairs, 1)));
+    int64_t fwd_pairs = 0, fwd_cells = 0, run_cells = 0, pad_b = 0;
+    for (const WaveDesc& w : pp.waves) {
+      if (w.cells != kWaveSingleRun) continue;
+      ++run_cells;
+      bool any = false;
+      for (int64_t x = w.base; x < w.base + w.steps; ++x) {
+        const PairRec& r = pp.recs[x];
+        if (r.flags & (kPairFwdA | kPairFwdB)) { ++fwd_pairs; any = true; }
+        pad_b += r.ub == kOffOOB;
+      }
+      fwd_cells += any;
+    }
+    std::printf("single-run cells %lld: with forwarding %lld; pairs with forwarding %lld, with a no-op B %lld\n",
+                (long long)run_cells, (long long)fwd_cells, (long long)fwd_pairs, (long long)pad_b);
   }
   {  // fingerprint of the plans (FNV-1a over the records, cell offsets and pair records)
     uint64_t h = 1469598103934665603ull;
