@@ -97,6 +97,12 @@ struct DevRatingBlocks {
   int64_t total = 0;
 };
 
+// Device scratch of online_sweep_plan (kernels_online.hip), kept across micro-batches.
+struct OnlineSweepScratch {
+  DevBuf ukey, wkey, wkey2, iota, ux, wx, head, start, ticket, tmp;
+  DevBuf in, wbeg, uticket, err;  // the batch as uploaded; the sweep's wave starts, tickets, error flag
+};
+
 // Pinned host staging buffer.
 class PinnedBuf {
  public:

@@ -11,55 +11,60 @@ namespace mfhip {
 
 class IdIndex {
  public:
-  void clear() { keys_.clear(); vals_.clear(); size_ = 0; mask_ = 0; }
+  void clear() { slots_.clear(); size_ = 0; mask_ = 0; }
   int64_t size() const { return size_; }
 
   void reserve(int64_t n) {
     uint64_t cap = 16;
     while (cap < static_cast<uint64_t>(n) * 2 + 16) cap <<= 1;
-    if (cap <= keys_.size()) return;
+    if (cap <= slots_.size()) return;
     rehash(cap);
   }
 
   // Returns the row for id, or -1.
   int32_t find(int32_t id) const {
-    if (keys_.empty()) return -1;
+    if (slots_.empty()) return -1;
     uint64_t h = hash(id) & mask_;
     while (true) {
-      const int32_t v = vals_[h];
-      if (v < 0) return -1;
-      if (keys_[h] == id) return v;
+      const Slot sl = slots_[h];
+      if (sl.row < 0) return -1;
+      if (sl.id == id) return sl.row;
       h = (h + 1) & mask_;
     }
   }
 
   // Inserts id -> row if absent; returns the stored row.
   int32_t insert(int32_t id, int32_t row) {
-    if (static_cast<uint64_t>(size_ + 1) * 2 > keys_.size()) rehash(keys_.empty() ? 16 : keys_.size() * 2);
+    if (static_cast<uint64_t>(size_ + 1) * 2 > slots_.size()) rehash(slots_.empty() ? 16 : slots_.size() * 2);
     uint64_t h = hash(id) & mask_;
     while (true) {
-      if (vals_[h] < 0) { keys_[h] = id; vals_[h] = row; ++size_; return row; }
-      if (keys_[h] == id) return vals_[h];
+      Slot& sl = slots_[h];
+      if (sl.row < 0) { sl = Slot{id, row}; ++size_; return row; }
+      if (sl.id == id) return sl.row;
       h = (h + 1) & mask_;
     }
   }
 
  private:
+  // id and row side by side: a lookup touches one cache line, not two
+  struct Slot {
+    int32_t id;
+    int32_t row;  // -1: empty
+  };
   static uint64_t hash(int32_t id) {
     uint64_t x = static_cast<uint32_t>(id);
     x ^= x >> 16; x *= 0x7feb352dULL; x ^= x >> 15; x *= 0x846ca68bULL; x ^= x >> 16;
     return x;
   }
   void rehash(uint64_t cap) {
-    std::vector<int32_t> ok(std::move(keys_)), ov(std::move(vals_));
-    keys_.assign(cap, 0);
-    vals_.assign(cap, -1);
+    std::vector<Slot> old(std::move(slots_));
+    slots_.assign(cap, Slot{0, -1});
     mask_ = cap - 1;
     size_ = 0;
-    for (size_t j = 0; j < ov.size(); ++j)
-      if (ov[j] >= 0) insert(ok[j], ov[j]);
+    for (const Slot& sl : old)
+      if (sl.row >= 0) insert(sl.id, sl.row);
   }
-  std::vector<int32_t> keys_, vals_;
+  std::vector<Slot> slots_;
   uint64_t mask_ = 0;
   int64_t size_ = 0;
 };

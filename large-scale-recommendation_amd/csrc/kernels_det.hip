@@ -146,23 +146,22 @@ __global__ __launch_bounds__(64) void k_online_sweep(const int64_t* __restrict__
       cur_i = ir;
       have_q = true;
     }
-    // the next update's user row, if it does not wait on anyone (or its ticket is already due)
-    have_pn = false;
-    if (j + 1 < j1) {
-      const uint32_t un = ent[j + 1].u;
-      const int32_t qn = static_cast<int32_t>(useq[j + 1]);
-      if (un != ur &&
-          (qn == 0 || __builtin_amdgcn_readfirstlane(
-                          __hip_atomic_load(ticket + un, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == qn)) {
-        const T* pnr = U + static_cast<size_t>(un) * k;
-#pragma unroll
-        for (int c = 0; c < KPL; ++c) pn[c] = ld(pnr, c);
-        have_pn = true;
-      }
-    }
+    // the next update's user row is loaded ahead if it waits on no one or its ticket is already
+    // due; the ticket is read here and looked at after the dot, so its round trip overlaps it
+    const bool nxt = j + 1 < j1;
+    const uint32_t un = nxt ? ent[j + 1].u : ur;
+    const int32_t qn = nxt ? static_cast<int32_t>(useq[j + 1]) : 0;
+    const bool ask = nxt && un != ur && qn != 0;
+    const int32_t tk = ask ? __hip_atomic_load(ticket + un, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
 #pragma unroll
     for (int c = 0; c < KPL; ++c) pr[c] = pv[c] * qv[c];
     const T e = r - seq_dot<T, KPL>(pr, k);
+    have_pn = nxt && un != ur && (qn == 0 || __builtin_amdgcn_readfirstlane(tk) == qn);
+    if (have_pn) {
+      const T* pnr = U + static_cast<size_t>(un) * k;
+#pragma unroll
+      for (int c = 0; c < KPL; ++c) pn[c] = ld(pnr, c);
+    }
     const T le = eta * e;  // learningRate * e * i == (learningRate * e) * i
     T qnew[KPL];
 #pragma unroll

@@ -1,0 +1,136 @@
+// kernels_online.hip -- the inputs of k_online_sweep (kernels_det.hip) built on the device from
+// one micro-batch in sequence order (SGDUpdater.nextFactors applied in arrival order,
+// core/FactorUpdater.scala:37-53, OnlineSpark.scala:191-194 / FlinkOnlineMF.scala's per-rating
+// updates).  The host version of the same plan (a sequential counting sort) cost more than the
+// sweep it fed; this one is two stable radix sorts and three gathers:
+//   tickets : stable sort of (user row, x) -> an update's ticket value is its rank inside its
+//             user's run = the number of earlier updates of that user (the kernel waits until
+//             the user's ticket word reaches it)
+//   waves   : stable sort of (item row mod W, x) -> wave w's updates in sequence order; every
+//             update of an item lands in one wave, so the item's order is the sequence order
+//   wbeg[w] : first position of wave w (lower bound in the sorted wave keys), wbeg[W] = n
+// HBM-bound integer work (4-byte keys, 4-byte payloads).  Bitwise the host plan: the factors of
+// the sweep equal the level replay's (tests/test_gpu_online.py).
+
+#include <hip/hip_runtime.h>
+
+#include <hipcub/device/device_radix_sort.hpp>
+#include <hipcub/device/device_scan.hpp>
+
+#include <algorithm>
+
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace mfhip {
+namespace {
+
+constexpr int kThreads = 256;
+unsigned grid_for(int64_t n) {
+  return static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((n + kThreads - 1) / kThreads, 1 << 16)));
+}
+
+__global__ void k_keys(const uint32_t* __restrict__ eu, const uint32_t* __restrict__ ei, int64_t n, uint32_t W,
+                       uint32_t* __restrict__ wkey, int32_t* __restrict__ iota) {
+  for (int64_t x = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; x < n;
+       x += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    wkey[x] = ei[x] % W;
+    iota[x] = static_cast<int32_t>(x);
+  }
+}
+
+// head[p] = p where a user's run starts in the user-sorted keys, else 0 (a max-scan then gives
+// every position its run start)
+__global__ void k_run_heads(const uint32_t* __restrict__ ukey, int64_t n, int32_t* __restrict__ head) {
+  for (int64_t p = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; p < n;
+       p += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    head[p] = (p == 0 || ukey[p] != ukey[p - 1]) ? static_cast<int32_t>(p) : 0;
+}
+
+__global__ void k_tickets(const int32_t* __restrict__ ux, const int32_t* __restrict__ start, int64_t n,
+                          uint32_t* __restrict__ ticket) {
+  for (int64_t p = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; p < n;
+       p += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    ticket[ux[p]] = static_cast<uint32_t>(p - start[p]);
+}
+
+__global__ void k_gather(const int32_t* __restrict__ wx, const uint32_t* __restrict__ eu,
+                         const uint32_t* __restrict__ ei, const double* __restrict__ er,
+                         const uint32_t* __restrict__ ticket, int64_t n, DetEntry* __restrict__ ent,
+                         uint32_t* __restrict__ useq) {
+  for (int64_t y = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; y < n;
+       y += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int32_t x = wx[y];
+    ent[y] = DetEntry{eu[x], ei[x], er[x]};
+    useq[y] = ticket[x];
+  }
+}
+
+__global__ void k_wave_begin(const uint32_t* __restrict__ wsorted, int64_t n, uint32_t W, int64_t* __restrict__ wbeg) {
+  for (int64_t w = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; w <= W;
+       w += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    int64_t lo = 0, hi = n;  // first position whose key is >= w
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) / 2;
+      if (wsorted[mid] < static_cast<uint32_t>(w)) lo = mid + 1;
+      else hi = mid;
+    }
+    wbeg[w] = lo;
+  }
+}
+
+int bits_for(uint64_t v) {  // radix bits that hold every key < v
+  int b = 1;
+  while (b < 32 && (uint64_t{1} << b) < v) ++b;
+  return b;
+}
+
+}  // namespace
+
+void online_sweep_plan(hipStream_t st, OnlineSweepScratch& sc, const uint32_t* eu, const uint32_t* ei,
+                       const double* er, int64_t n, uint32_t W, uint32_t user_rows, DetEntry* ent, uint32_t* useq,
+                       int64_t* wbeg) {
+  MF_REQUIRE(n > 0 && n < (int64_t{1} << 31) && W >= 1, "online sweep plan: bad batch shape");
+  const int N = static_cast<int>(n);
+  sc.ukey.alloc(n * 4);
+  sc.wkey.alloc(n * 4);
+  sc.wkey2.alloc(n * 4);
+  sc.iota.alloc(n * 4);
+  sc.ux.alloc(n * 4);
+  sc.wx.alloc(n * 4);
+  sc.head.alloc(n * 4);
+  sc.start.alloc(n * 4);
+  sc.ticket.alloc(n * 4);
+  hipLaunchKernelGGL(k_keys, dim3(grid_for(n)), dim3(kThreads), 0, st, eu, ei, n, W, sc.wkey.as<uint32_t>(),
+                     sc.iota.as<int32_t>());
+  size_t tb = 0;
+  const int ub = bits_for(user_rows), wb = bits_for(W);
+  // tickets
+  MF_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, eu, sc.ukey.as<uint32_t>(), sc.iota.as<int32_t>(),
+                                            sc.ux.as<int32_t>(), N, 0, ub, st));
+  sc.tmp.alloc(std::max<size_t>(tb, 256));
+  MF_HIP(hipcub::DeviceRadixSort::SortPairs(sc.tmp.get(), tb, eu, sc.ukey.as<uint32_t>(), sc.iota.as<int32_t>(),
+                                            sc.ux.as<int32_t>(), N, 0, ub, st));
+  hipLaunchKernelGGL(k_run_heads, dim3(grid_for(n)), dim3(kThreads), 0, st, sc.ukey.as<uint32_t>(), n,
+                     sc.head.as<int32_t>());
+  MF_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb, sc.head.as<int32_t>(), sc.start.as<int32_t>(), hipcub::Max(),
+                                           N, st));
+  sc.tmp.alloc(std::max<size_t>(tb, 256));
+  MF_HIP(hipcub::DeviceScan::InclusiveScan(sc.tmp.get(), tb, sc.head.as<int32_t>(), sc.start.as<int32_t>(),
+                                           hipcub::Max(), N, st));
+  hipLaunchKernelGGL(k_tickets, dim3(grid_for(n)), dim3(kThreads), 0, st, sc.ux.as<int32_t>(), sc.start.as<int32_t>(),
+                     n, sc.ticket.as<uint32_t>());
+  // waves
+  MF_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, sc.wkey.as<uint32_t>(), sc.wkey2.as<uint32_t>(),
+                                            sc.iota.as<int32_t>(), sc.wx.as<int32_t>(), N, 0, wb, st));
+  sc.tmp.alloc(std::max<size_t>(tb, 256));
+  MF_HIP(hipcub::DeviceRadixSort::SortPairs(sc.tmp.get(), tb, sc.wkey.as<uint32_t>(), sc.wkey2.as<uint32_t>(),
+                                            sc.iota.as<int32_t>(), sc.wx.as<int32_t>(), N, 0, wb, st));
+  hipLaunchKernelGGL(k_gather, dim3(grid_for(n)), dim3(kThreads), 0, st, sc.wx.as<int32_t>(), eu, ei, er,
+                     sc.ticket.as<uint32_t>(), n, ent, useq);
+  hipLaunchKernelGGL(k_wave_begin, dim3(grid_for(W + 1)), dim3(kThreads), 0, st, sc.wkey2.as<uint32_t>(), n, W,
+                     wbeg);
+  MF_HIP(hipGetLastError());
+}
+
+}  // namespace mfhip

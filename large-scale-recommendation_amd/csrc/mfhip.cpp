@@ -83,6 +83,7 @@ struct Shard {
   // deterministic mode staging
   DevBuf det_dev;
   PinnedBuf det_pin;
+  OnlineSweepScratch online_sc;  // online micro-batches (k_online_sweep)
   // fast mode
   DevBuf fast_recs, fast_cells, fast_blks;
   DevBuf fast_prog, fast_err;  // persistent sweep: progress words + timeout flag
@@ -119,6 +120,7 @@ struct Shard {
 struct mf_ctx {
   mfhip::Reaper reaper;  // host plan buffers being released in the background (first member: joined last)
   mf_params P{};
+  std::vector<uint32_t> on_ur, on_ir;  // online batches: factor rows per rating (kept: no page faults per batch)
   bool f64 = true;
   size_t es = 8;  // bytes per factor element
   int G = 1;      // global shard count
@@ -1638,32 +1640,52 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
   const int k = ctx->P.num_factors;
   PhaseClock clk;
   std::vector<int32_t> fu, fi;
-  std::vector<uint32_t> ur(n), ir(n);
+  if (static_cast<int64_t>(ctx->on_ur.size()) < n) {
+    ctx->on_ur.resize(n);
+    ctx->on_ir.resize(n);
+  }
+  std::vector<uint32_t>& ur = ctx->on_ur;
+  std::vector<uint32_t>& ir = ctx->on_ir;
   const int64_t u0 = ctx->U.rows(), i0 = ctx->I.rows();
   std::vector<uint8_t> seen_u, seen_i;
   int64_t cu = 0, ci = 0;
-  // rows of known ids in parallel (the index is only read); then, in rating order, the ids first
-  // seen in this batch get new rows in order of appearance, exactly as one sequential scan would
-  std::vector<int32_t> fr_u(n), fr_i(n);
+  // rows of known ids in parallel (the index is only read; kMiss marks the others); then, in
+  // rating order, the ids first seen in this batch get new rows in order of appearance, exactly
+  // as one sequential scan would
+  constexpr uint32_t kMiss = 0xFFFFFFFFu;
+  std::atomic<int64_t> misses{0};
   parallel_for(n, [&](int64_t lo2, int64_t hi2, int) {
+    int64_t m = 0;
     for (int64_t j = lo2; j < hi2; ++j) {
-      fr_u[j] = ctx->U.index.find(u[j]);
-      fr_i[j] = ctx->I.index.find(i[j]);
+      ur[j] = static_cast<uint32_t>(ctx->U.index.find(u[j]));  // -1 -> kMiss
+      ir[j] = static_cast<uint32_t>(ctx->I.index.find(i[j]));
+      m += (ur[j] == kMiss) + (ir[j] == kMiss);
     }
+    misses += m;
   });
-  for (int64_t j = 0; j < n; ++j) {
-    ur[j] = static_cast<uint32_t>(fr_u[j] >= 0 ? fr_u[j] : online_row(ctx, ctx->U, u[j], fu));
-    ir[j] = static_cast<uint32_t>(fr_i[j] >= 0 ? fr_i[j] : online_row(ctx, ctx->I, i[j], fi));
-  }
+  if (misses > 0)
+    for (int64_t j = 0; j < n; ++j) {
+      if (ur[j] == kMiss) ur[j] = static_cast<uint32_t>(online_row(ctx, ctx->U, u[j], fu));
+      if (ir[j] == kMiss) ir[j] = static_cast<uint32_t>(online_row(ctx, ctx->I, i[j], fi));
+    }
+  clk.lap("online: id lookup");
   // touched-row counts (UpdateSeparatedHashMap.updates, OfflineSpark.scala:33-67)
   seen_u.assign(ctx->U.rows(), 0);
   seen_i.assign(ctx->I.rows(), 0);
-  std::atomic<int64_t> acu{0}, aci{0};
+  // flags set with plain relaxed stores, and only when still clear (a locked exchange per rating
+  // kept the flag lines bouncing between cores: 8 ms per 1M ratings), then counted
   parallel_for(n, [&](int64_t lo2, int64_t hi2, int) {
+    for (int64_t j = lo2; j < hi2; ++j) {
+      if (!__atomic_load_n(&seen_u[ur[j]], __ATOMIC_RELAXED)) __atomic_store_n(&seen_u[ur[j]], 1, __ATOMIC_RELAXED);
+      if (!__atomic_load_n(&seen_i[ir[j]], __ATOMIC_RELAXED)) __atomic_store_n(&seen_i[ir[j]], 1, __ATOMIC_RELAXED);
+    }
+  });
+  std::atomic<int64_t> acu{0}, aci{0};
+  parallel_for(static_cast<int64_t>(std::max(seen_u.size(), seen_i.size())), [&](int64_t lo2, int64_t hi2, int) {
     int64_t lu = 0, li = 0;
-    for (int64_t j = lo2; j < hi2; ++j) {  // first writer of a row's flag counts it
-      lu += __atomic_exchange_n(&seen_u[ur[j]], static_cast<uint8_t>(1), __ATOMIC_RELAXED) == 0;
-      li += __atomic_exchange_n(&seen_i[ir[j]], static_cast<uint8_t>(1), __ATOMIC_RELAXED) == 0;
+    for (int64_t x = lo2; x < hi2; ++x) {
+      if (x < static_cast<int64_t>(seen_u.size())) lu += seen_u[x];
+      if (x < static_cast<int64_t>(seen_i.size())) li += seen_i[x];
     }
     acu += lu;
     aci += li;
@@ -1672,7 +1694,7 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
   ci = aci;
   if (tu) *tu = cu;
   if (ti) *ti = ci;
-  clk.lap("online: id lookup + touched rows");
+  clk.lap("online: touched rows");
   // new rows take the slab rows the fast DSGD schedule keeps zeroed (padding / idle prefetch
   // rows past the real ones): that schedule is void now, a further fit must prepare again
   if (ctx->prepared && !ctx->f64 && (!fu.empty() || !fi.empty())) ctx->prepared = false;
@@ -1713,57 +1735,61 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
       }
   }
   const bool outs = uout || iout;
-  // MFHIP_ONLINE_KERNEL=sweep: one persistent launch instead of the level-by-level replay
-  // (opt-in: measured slower end to end on NFLX 1M-rating batches)
+  // one persistent launch (the default; MFHIP_ONLINE_KERNEL=level forces the level-by-level
+  // replay, which is also the path with per-rating outputs): NFLX 1M-rating batches 37-38M vs
+  // 28-30M ratings/s end to end
   const char* okv = std::getenv("MFHIP_ONLINE_KERNEL");
-  if (!outs && okv && std::string(okv) == "sweep") {
+  int cap = 0;
+  if (!outs && !(okv && std::string(okv) == "level")) {
+    DeviceGuard g(s.device);
+    cap = online_sweep_capacity(k, ctx->f64);  // 0 (occupancy query failed): the level replay
+  }
+  if (cap > 0) {
     // one persistent launch (k_online_sweep): items spread over the waves, each wave's updates in
     // sequence order, and per update the number of earlier updates of its user (its ticket value)
     DeviceGuard g(s.device);
-    const int cap = online_sweep_capacity(k, ctx->f64);
     const int64_t W = std::max<int64_t>(1, std::min<int64_t>({static_cast<int64_t>(cap / 2), 4096, n}));
     const uint32_t W32 = static_cast<uint32_t>(W);
-    std::vector<uint32_t> wv(n);  // wave of each update in sequence order
-    std::vector<int64_t> wbeg(W + 1, 0);
-    for (int64_t x = 0; x < n; ++x) {
-      wv[x] = ir[order[x]] % W32;
-      wbeg[wv[x] + 1]++;
-    }
-    for (int64_t w = 0; w < W; ++w) wbeg[w + 1] += wbeg[w];
-    std::vector<int64_t> cur(wbeg.begin(), wbeg.end() - 1);
-    std::vector<uint32_t> ucnt(ctx->U.rows(), 0);
+    // the batch in sequence order goes up as is (16 bytes an update); the per-wave lists and the
+    // tickets are built on the device (online_sweep_plan, kernels_online.hip)
+    OnlineSweepScratch& sc = s.online_sc;
     const size_t ebytes = static_cast<size_t>(n) * sizeof(DetEntry), qbytes = static_cast<size_t>(n) * 4;
-    std::vector<char> stage(ebytes + qbytes);  // built in cached memory, then one copy to the pinned buffer
-    DetEntry* he = reinterpret_cast<DetEntry*>(stage.data());
-    uint32_t* hq = reinterpret_cast<uint32_t*>(stage.data() + ebytes);
-    for (int64_t x = 0; x < n; ++x) {
-      const int32_t j = order[x];
-      const int64_t y = cur[wv[x]]++;
-      he[y] = DetEntry{ur[j], ir[j], r[j]};
-      hq[y] = ucnt[ur[j]]++;
-    }
-    MF_HIP(hipStreamSynchronize(s.stream));
-    s.det_pin.alloc(ebytes + qbytes);
-    std::memcpy(s.det_pin.as<void>(), stage.data(), ebytes + qbytes);
-    clk.lap("online: sweep plan");
+    const size_t ibytes = static_cast<size_t>(n) * 16;
+    MF_HIP(hipStreamSynchronize(s.stream));  // det_pin may still feed an earlier copy
+    s.det_pin.alloc(ibytes);
+    uint32_t* pu = s.det_pin.as<uint32_t>();
+    uint32_t* pi = pu + n;
+    double* pr = reinterpret_cast<double*>(pi + n);
+    parallel_for(n, [&](int64_t lo2, int64_t hi2, int) {
+      for (int64_t x = lo2; x < hi2; ++x) {
+        const int32_t j = order[x];
+        pu[x] = ur[j];
+        pi[x] = ir[j];
+        pr[x] = r[j];
+      }
+    });
+    clk.lap("online: sweep staging");
+    sc.in.alloc(ibytes);
+    MF_HIP(hipMemcpyAsync(sc.in.get(), pu, ibytes, hipMemcpyHostToDevice, s.stream));
     s.det_dev.alloc(ebytes + qbytes);
-    MF_HIP(hipMemcpyAsync(s.det_dev.get(), s.det_pin.as<void>(), ebytes + qbytes, hipMemcpyHostToDevice, s.stream));
-    DevBuf dwb, dticket, derr;
-    dwb.alloc(wbeg.size() * 8);
-    MF_HIP(hipMemcpyAsync(dwb.get(), wbeg.data(), wbeg.size() * 8, hipMemcpyHostToDevice, s.stream));
-    dticket.alloc(static_cast<size_t>(std::max<int64_t>(ctx->U.rows(), 1)) * 4);
-    MF_HIP(hipMemsetAsync(dticket.get(), 0, dticket.bytes(), s.stream));
-    derr.alloc(4);
-    MF_HIP(hipMemsetAsync(derr.get(), 0, 4, s.stream));
+    sc.wbeg.alloc(static_cast<size_t>(W + 1) * 8);
+    const uint32_t* du = sc.in.as<uint32_t>();
+    online_sweep_plan(s.stream, sc, du, du + n, reinterpret_cast<const double*>(du + 2 * n), n, W32,
+                      static_cast<uint32_t>(ctx->U.rows()), s.det_dev.as<DetEntry>(),
+                      reinterpret_cast<uint32_t*>(s.det_dev.as<char>() + ebytes), sc.wbeg.as<int64_t>());
+    sc.uticket.alloc(static_cast<size_t>(std::max<int64_t>(ctx->U.rows(), 1)) * 4);
+    MF_HIP(hipMemsetAsync(sc.uticket.get(), 0, static_cast<size_t>(std::max<int64_t>(ctx->U.rows(), 1)) * 4, s.stream));
+    sc.err.alloc(4);
+    MF_HIP(hipMemsetAsync(sc.err.get(), 0, 4, s.stream));
     {
       LaunchTimer t(s, ctx->profiling);
-      launch_online_sweep(s.stream, static_cast<int>(W), dwb.as<int64_t>(), s.det_dev.as<DetEntry>(),
+      launch_online_sweep(s.stream, static_cast<int>(W), sc.wbeg.as<int64_t>(), s.det_dev.as<DetEntry>(),
                           reinterpret_cast<const uint32_t*>(s.det_dev.as<char>() + ebytes), s.uf.get(), s.itf.get(), k,
-                          ctx->P.online_learning_rate, ctx->f64, dticket.as<int32_t>(), derr.as<int32_t>());
+                          ctx->P.online_learning_rate, ctx->f64, sc.uticket.as<int32_t>(), sc.err.as<int32_t>());
     }
     MF_HIP(hipGetLastError());
     int32_t err = 0;
-    MF_HIP(hipMemcpyAsync(&err, derr.get(), 4, hipMemcpyDeviceToHost, s.stream));
+    MF_HIP(hipMemcpyAsync(&err, sc.err.get(), 4, hipMemcpyDeviceToHost, s.stream));
     MF_HIP(hipStreamSynchronize(s.stream));
     clk.lap("online: sweep (device)");
     if (err) fail(MF_ERR_TIMEOUT, "online sweep: a ticket wait timed out");

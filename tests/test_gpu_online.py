@@ -177,9 +177,10 @@ def test_per_rating_outputs_bit_exact(flavour, name):
 
 @pytest.mark.parametrize("mode,k", [(L.MODE_FAST_F32, 128), (L.MODE_DETERMINISTIC_F64, 200), (L.MODE_FAST_F32, 40)])
 def test_online_sweep_equals_level_replay(monkeypatch, mode, k):
-    """The opt-in one-launch online sweep (MFHIP_ONLINE_KERNEL=sweep: per-item waves, per-user
-    tickets, k_online_sweep) gives the factors of the default level-by-level replay bit for bit,
-    including a hot item, repeated (user, item) pairs and ids first seen in a later batch."""
+    """The one-launch online sweep (the default: per-item waves, per-user tickets, k_online_sweep,
+    its wave lists and tickets built on the device by kernels_online.hip) gives the factors of the
+    level-by-level replay (MFHIP_ONLINE_KERNEL=level) bit for bit, including a hot item, repeated
+    (user, item) pairs and ids first seen in a later batch."""
     rng = np.random.default_rng(7)
     n = 120000
     u = rng.integers(0, 5000, n).astype(np.int32)
@@ -194,6 +195,39 @@ def test_online_sweep_equals_level_replay(monkeypatch, mode, k):
         with mfhip.Context(p) as ctx:
             for s in range(0, n, 40000):
                 ctx.online_update(u[s:s + 40000], i[s:s + 40000], r[s:s + 40000], L.ONLINE_NEXT_FACTORS)
+            res[kern] = (ctx.factors(0), ctx.factors(1))
+    for side in (0, 1):
+        assert np.array_equal(res["level"][side][0], res["sweep"][side][0])
+        assert np.array_equal(res["level"][side][1], res["sweep"][side][1])
+
+
+@pytest.mark.parametrize("shape", ["one", "few", "one_user", "one_item", "spark"])
+def test_online_sweep_edge_batches(monkeypatch, shape):
+    """Edge batches of the device-built sweep plan (kernels_online.hip) against the level replay,
+    bit for bit: a single rating, fewer ratings than waves, one user across every wave (a ticket
+    chain through all of them), one item (one wave holds the whole batch), and the Spark-sweep
+    order (a permuted sequence)."""
+    rng = np.random.default_rng(11)
+    n = {"one": 1, "few": 37}.get(shape, 30000)
+    u = rng.integers(0, 3000, n).astype(np.int32)
+    i = rng.integers(0, 900, n).astype(np.int32)
+    if shape == "one_user":
+        u[:] = 42
+    if shape == "one_item":
+        i[:] = 7
+    r = rng.integers(1, 6, n).astype(np.float64)
+    flav = L.ONLINE_SPARK_SWEEP if shape == "spark" else L.ONLINE_NEXT_FACTORS
+    res = {}
+    for kern in ("level", "sweep"):
+        monkeypatch.setenv("MFHIP_ONLINE_KERNEL", kern)
+        p = L.default_params()
+        p.num_factors, p.mode, p.online_learning_rate = 32, L.MODE_FAST_F32, 0.01
+        with mfhip.Context(p) as ctx:
+            for s in range(0, n, 10000):
+                if flav == L.ONLINE_SPARK_SWEEP:
+                    ctx.online_update(u[s:s + 10000], i[s:s + 10000], r[s:s + 10000], flav, num_partitions=4)
+                else:
+                    ctx.online_update(u[s:s + 10000], i[s:s + 10000], r[s:s + 10000], flav)
             res[kern] = (ctx.factors(0), ctx.factors(1))
     for side in (0, 1):
         assert np.array_equal(res["level"][side][0], res["sweep"][side][0])
