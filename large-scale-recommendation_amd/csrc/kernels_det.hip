@@ -37,8 +37,15 @@ __device__ __forceinline__ T seq_dot(const T (&prod)[KPL], int k) {
   T acc = T(0);
 #pragma unroll
   for (int c = 0; c < KPL; ++c) {
-    const int lim = min(64, k - 64 * c);
-    for (int l = 0; l < lim; ++l) acc = acc + readlane(prod[c], l);
+    if (64 * (c + 1) <= k) {
+      // a full chunk: constant lane indices, no loop (the adds are one dependent chain; the
+      // readlanes run ahead of it)
+#pragma unroll
+      for (int l = 0; l < 64; ++l) acc = acc + readlane(prod[c], l);
+    } else {
+      const int lim = min(64, k - 64 * c);
+      for (int l = 0; l < lim; ++l) acc = acc + readlane(prod[c], l);
+    }
   }
   return acc;
 }
@@ -120,22 +127,34 @@ __global__ __launch_bounds__(64) void k_online_sweep(const int64_t* __restrict__
     }
     return true;
   };
-  // the item row stays in registers while consecutive updates of this wave share the item (a hot
-  // item's chain); the next update's user row is loaded ahead when its ticket is already due
-  T qv[KPL], pn[KPL];
-  bool have_q = false, have_pn = false;
+  // loads ahead: every lane issues one load per c (clamped address), so the vmcnt count of a row
+  // loaded ahead is exactly KPL; lanes past k are zeroed where the row is used (not here, which
+  // would wait for the load at once)
+  auto ld_row = [&](const T* row, T (&v)[KPL]) {
+#pragma unroll
+    for (int c = 0; c < KPL; ++c)
+      v[c] = __hip_atomic_load(row + min(lane + 64 * c, k - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  // The item row stays in registers while consecutive updates of this wave share the item (a hot
+  // item's chain).  User rows are loaded ahead into two slots: update j's row sits in slot
+  // (j - j0) & 1, loaded during update j - 2 when its ticket was already due (or during j - 1, or
+  // else by j itself after waiting).  The loads ahead are issued after the update's stores, so the
+  // drain before the ticket store waits for the stores only (vmcnt = the loads issued after them).
+  T qv[KPL], sa[KPL], sb[KPL];
+  bool ha = false, hb = false;
+  bool have_q = false;
   uint32_t cur_i = 0;
-  for (int64_t j = j0; j < j1; ++j) {
+  auto step = [&](int64_t j, T (&slot)[KPL], bool& have, T (&oslot)[KPL], bool& ohave) -> bool {
     const uint32_t ur = ent[j].u, ir = ent[j].i;
     const int32_t q = static_cast<int32_t>(useq[j]);
     const T r = static_cast<T>(ent[j].r);
     T* p = U + static_cast<size_t>(ur) * k;
     T pv[KPL], pr[KPL];
-    if (have_pn) {
+    if (have) {
 #pragma unroll
-      for (int c = 0; c < KPL; ++c) pv[c] = pn[c];
+      for (int c = 0; c < KPL; ++c) pv[c] = lane + 64 * c < k ? slot[c] : T(0);
     } else {
-      if (!wait_ticket(ur, q)) return;
+      if (!wait_ticket(ur, q)) return false;
 #pragma unroll
       for (int c = 0; c < KPL; ++c) pv[c] = ld(p, c);
     }
@@ -146,22 +165,19 @@ __global__ __launch_bounds__(64) void k_online_sweep(const int64_t* __restrict__
       cur_i = ir;
       have_q = true;
     }
-    // the next update's user row is loaded ahead if it waits on no one or its ticket is already
-    // due; the ticket is read here and looked at after the dot, so its round trip overlaps it
-    const bool nxt = j + 1 < j1;
-    const uint32_t un = nxt ? ent[j + 1].u : ur;
-    const int32_t qn = nxt ? static_cast<int32_t>(useq[j + 1]) : 0;
-    const bool ask = nxt && un != ur && qn != 0;
-    const int32_t tk = ask ? __hip_atomic_load(ticket + un, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+    // tickets of update j + 1 (unless its row is loaded already) and j + 2, read here and looked
+    // at after the dot (their round trip overlaps it).  A row is loaded ahead only when its
+    // ticket is due, i.e. every earlier update of that user is done (so never this update's user
+    // nor update j + 1's, whose updates are still to come)
+    const bool n1 = j + 1 < j1 && !ohave, n2 = j + 2 < j1;
+    const uint32_t u1 = n1 ? ent[j + 1].u : 0u, u2 = n2 ? ent[j + 2].u : 0u;
+    const int32_t q1 = n1 ? static_cast<int32_t>(useq[j + 1]) : 0, q2 = n2 ? static_cast<int32_t>(useq[j + 2]) : 0;
+    // (both reads unconditional, so the compiler's wait before the dot can leave them in flight)
+    const int32_t t1 = __hip_atomic_load(ticket + (n1 ? u1 : ur), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int32_t t2 = __hip_atomic_load(ticket + (n2 ? u2 : ur), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
     for (int c = 0; c < KPL; ++c) pr[c] = pv[c] * qv[c];
     const T e = r - seq_dot<T, KPL>(pr, k);
-    have_pn = nxt && un != ur && (qn == 0 || __builtin_amdgcn_readfirstlane(tk) == qn);
-    if (have_pn) {
-      const T* pnr = U + static_cast<size_t>(un) * k;
-#pragma unroll
-      for (int c = 0; c < KPL; ++c) pn[c] = ld(pnr, c);
-    }
     const T le = eta * e;  // learningRate * e * i == (learningRate * e) * i
     T qnew[KPL];
 #pragma unroll
@@ -182,8 +198,30 @@ __global__ __launch_bounds__(64) void k_online_sweep(const int64_t* __restrict__
       }
       have_q = false;
     }
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this update's user row has landed
+    const bool g1 = n1 && u1 != ur && (q1 == 0 || __builtin_amdgcn_readfirstlane(t1) == q1);
+    const bool g2 = n2 && u2 != ur && (q2 == 0 || __builtin_amdgcn_readfirstlane(t2) == q2);
+    // the loads ahead must issue after this update's stores (the vmcnt below counts on it)
+    __asm__ volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (g1) {
+      ld_row(U + static_cast<size_t>(u1) * k, oslot);
+      ohave = true;
+    }
+    have = g2;
+    if (g2) ld_row(U + static_cast<size_t>(u2) * k, slot);
+    // vmcnt(n): every operation older than the n loads just issued (this update's stores) has
+    // landed; vector memory operations complete in issue order
+    constexpr int V1 = KPL, V2 = 2 * KPL;
+    constexpr int kW1 = 0x0F70 | (V1 & 15) | ((V1 >> 4) << 14), kW2 = 0x0F70 | (V2 & 15) | ((V2 >> 4) << 14);
+    if (g1 && g2) __builtin_amdgcn_s_waitcnt(kW2);
+    else if (g1 || g2) __builtin_amdgcn_s_waitcnt(kW1);
+    else __builtin_amdgcn_s_waitcnt(0x0F70);
     if (lane == 0) __hip_atomic_store(ticket + ur, q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+  };
+  for (int64_t j = j0; j < j1; j += 2) {
+    if (!step(j, sa, ha, sb, hb)) return;
+    if (j + 1 < j1 && !step(j + 1, sb, hb, sa, ha)) return;
   }
 }
 
