@@ -50,6 +50,26 @@ __device__ __forceinline__ T seq_dot(const T (&prod)[KPL], int k) {
   return acc;
 }
 
+// seq_dot's order with the products through a wave-private LDS row, read back by every lane as
+// broadcast reads: the dependent add chain takes its operands from VGPRs (no v_readlane and
+// hazard nop per add).  Bitwise seq_dot.
+template <typename T, int KPL>
+__device__ __forceinline__ T seq_dot_lds(const T (&prod)[KPL], int k, T* lds, int lane) {
+#pragma unroll
+  for (int c = 0; c < KPL; ++c) lds[64 * c + lane] = prod[c];
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the wave's own LDS writes are done
+  __builtin_amdgcn_wave_barrier();
+  T acc = T(0);
+  if (k == 64 * KPL) {
+#pragma unroll
+    for (int x = 0; x < 64 * KPL; ++x) acc = acc + lds[x];
+  } else {
+    for (int x = 0; x < k; ++x) acc = acc + lds[x];
+  }
+  __builtin_amdgcn_wave_barrier();  // the next call's writes stay behind these reads
+  return acc;
+}
+
 template <typename T, int KPL, int ARITH>
 __global__ __launch_bounds__(256) void k_level(const DetEntry* __restrict__ ent, int64_t n,
                                                T* __restrict__ U, T* __restrict__ I,
@@ -111,6 +131,7 @@ __global__ __launch_bounds__(64) void k_online_sweep(const int64_t* __restrict__
   const int lane = threadIdx.x;
   const int64_t j0 = wbeg[blockIdx.x], j1 = wbeg[blockIdx.x + 1];
   if (j0 >= j1) return;
+  __shared__ __attribute__((aligned(16))) T lds[64 * KPL];
   auto ld = [&](const T* row, int c) {
     const int f = lane + 64 * c;
     return f < k ? __hip_atomic_load(row + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : T(0);
@@ -177,7 +198,7 @@ __global__ __launch_bounds__(64) void k_online_sweep(const int64_t* __restrict__
     const int32_t t2 = __hip_atomic_load(ticket + (n2 ? u2 : ur), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
     for (int c = 0; c < KPL; ++c) pr[c] = pv[c] * qv[c];
-    const T e = r - seq_dot<T, KPL>(pr, k);
+    const T e = r - seq_dot_lds<T, KPL>(pr, k, lds, lane);
     const T le = eta * e;  // learningRate * e * i == (learningRate * e) * i
     T qnew[KPL];
 #pragma unroll
