@@ -100,7 +100,7 @@ struct DevRatingBlocks {
 // Device scratch of online_sweep_plan (kernels_online.hip), kept across micro-batches.
 struct OnlineSweepScratch {
   DevBuf ukey, wkey, wkey2, iota, ux, wx, head, start, ticket, tmp;
-  DevBuf in, wbeg, uticket, err;  // the batch as uploaded; the sweep's wave starts, tickets, error flag
+  DevBuf in, wbeg, uticket, err, touched;  // the batch as uploaded; wave starts, tickets, error flag, counts
 };
 
 // Pinned host staging buffer.

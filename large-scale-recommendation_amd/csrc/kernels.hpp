@@ -30,11 +30,12 @@ void launch_online_sweep(hipStream_t st, int nw, const int64_t* wbeg, const DetE
 // k_online_sweep's inputs from one batch in sequence order (eu / ei / er: user row, item row,
 // rating of update x; device arrays), on the device (kernels_online.hip): ent / useq (n each,
 // grouped by wave = item row mod W, sequence order inside a wave, useq = the update's rank among
-// its user's updates) and wbeg (W + 1).  user_rows bounds eu.
+// its user's updates) and wbeg (W + 1); touched[0..1] = distinct user / item rows of the batch.
+// user_rows / item_rows bound eu / ei.
 struct OnlineSweepScratch;
 void online_sweep_plan(hipStream_t st, OnlineSweepScratch& sc, const uint32_t* eu, const uint32_t* ei,
-                       const double* er, int64_t n, uint32_t W, uint32_t user_rows, DetEntry* ent, uint32_t* useq,
-                       int64_t* wbeg);
+                       const double* er, int64_t n, uint32_t W, uint32_t user_rows, uint32_t item_rows,
+                       DetEntry* ent, uint32_t* useq, int64_t* wbeg, int32_t* touched);
 // Per-rating records of the online operators (mf_online_update_out), f64 rows of k at
 // [src[entry] * k]: kOutNext = (user', item') (FlinkOnlineMF.scala:131-135), kOutDelta =
 // (user + deltaItem, deltaItem) with user before the update (PSOfflineOnlineMF.scala:174-176).

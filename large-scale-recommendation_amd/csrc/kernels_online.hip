@@ -9,12 +9,16 @@
 //   waves   : stable sort of (item row mod W, x) -> wave w's updates in sequence order; every
 //             update of an item lands in one wave, so the item's order is the sequence order
 //   wbeg[w] : first position of wave w (lower bound in the sorted wave keys), wbeg[W] = n
+//   touched : distinct user rows (run heads of the user sort) and item rows (run heads of a
+//             key-only item sort) of the batch (UpdateSeparatedHashMap.updates,
+//             OfflineSpark.scala:33-67)
 // HBM-bound integer work (4-byte keys, 4-byte payloads).  Bitwise the host plan: the factors of
 // the sweep equal the level replay's (tests/test_gpu_online.py).
 
 #include <hip/hip_runtime.h>
 
 #include <hipcub/device/device_radix_sort.hpp>
+#include <hipcub/device/device_reduce.hpp>
 #include <hipcub/device/device_scan.hpp>
 
 #include <algorithm>
@@ -79,6 +83,12 @@ __global__ void k_wave_begin(const uint32_t* __restrict__ wsorted, int64_t n, ui
   }
 }
 
+__global__ void k_head_flags(const uint32_t* __restrict__ sorted, int64_t n, int32_t* __restrict__ flag) {
+  for (int64_t p = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; p < n;
+       p += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    flag[p] = (p == 0 || sorted[p] != sorted[p - 1]) ? 1 : 0;
+}
+
 int bits_for(uint64_t v) {  // radix bits that hold every key < v
   int b = 1;
   while (b < 32 && (uint64_t{1} << b) < v) ++b;
@@ -88,8 +98,8 @@ int bits_for(uint64_t v) {  // radix bits that hold every key < v
 }  // namespace
 
 void online_sweep_plan(hipStream_t st, OnlineSweepScratch& sc, const uint32_t* eu, const uint32_t* ei,
-                       const double* er, int64_t n, uint32_t W, uint32_t user_rows, DetEntry* ent, uint32_t* useq,
-                       int64_t* wbeg) {
+                       const double* er, int64_t n, uint32_t W, uint32_t user_rows, uint32_t item_rows,
+                       DetEntry* ent, uint32_t* useq, int64_t* wbeg, int32_t* touched) {
   MF_REQUIRE(n > 0 && n < (int64_t{1} << 31) && W >= 1, "online sweep plan: bad batch shape");
   const int N = static_cast<int>(n);
   sc.ukey.alloc(n * 4);
@@ -130,6 +140,20 @@ void online_sweep_plan(hipStream_t st, OnlineSweepScratch& sc, const uint32_t* e
                      sc.ticket.as<uint32_t>(), n, ent, useq);
   hipLaunchKernelGGL(k_wave_begin, dim3(grid_for(W + 1)), dim3(kThreads), 0, st, sc.wkey2.as<uint32_t>(), n, W,
                      wbeg);
+  // touched rows: run heads of the user-sorted keys, and of the item rows sorted (keys only)
+  hipLaunchKernelGGL(k_head_flags, dim3(grid_for(n)), dim3(kThreads), 0, st, sc.ukey.as<uint32_t>(), n,
+                     sc.head.as<int32_t>());
+  MF_HIP(hipcub::DeviceReduce::Sum(nullptr, tb, sc.head.as<int32_t>(), touched, N, st));
+  sc.tmp.alloc(std::max<size_t>(tb, 256));
+  MF_HIP(hipcub::DeviceReduce::Sum(sc.tmp.get(), tb, sc.head.as<int32_t>(), touched, N, st));
+  MF_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, ei, sc.wkey.as<uint32_t>(), N, 0, bits_for(item_rows), st));
+  sc.tmp.alloc(std::max<size_t>(tb, 256));
+  MF_HIP(hipcub::DeviceRadixSort::SortKeys(sc.tmp.get(), tb, ei, sc.wkey.as<uint32_t>(), N, 0, bits_for(item_rows), st));
+  hipLaunchKernelGGL(k_head_flags, dim3(grid_for(n)), dim3(kThreads), 0, st, sc.wkey.as<uint32_t>(), n,
+                     sc.start.as<int32_t>());
+  MF_HIP(hipcub::DeviceReduce::Sum(nullptr, tb, sc.start.as<int32_t>(), touched + 1, N, st));
+  sc.tmp.alloc(std::max<size_t>(tb, 256));
+  MF_HIP(hipcub::DeviceReduce::Sum(sc.tmp.get(), tb, sc.start.as<int32_t>(), touched + 1, N, st));
   MF_HIP(hipGetLastError());
 }
 

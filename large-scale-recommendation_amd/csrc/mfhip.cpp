@@ -1669,7 +1669,19 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
       if (ir[j] == kMiss) ir[j] = static_cast<uint32_t>(online_row(ctx, ctx->I, i[j], fi));
     }
   clk.lap("online: id lookup");
-  // touched-row counts (UpdateSeparatedHashMap.updates, OfflineSpark.scala:33-67)
+  // one persistent launch (the default; MFHIP_ONLINE_KERNEL=level forces the level-by-level
+  // replay, which is also the path with per-rating outputs): NFLX 1M-rating batches 83-87M vs
+  // 51M ratings/s end to end
+  const bool outs = uout || iout;
+  const char* okv = std::getenv("MFHIP_ONLINE_KERNEL");
+  int cap = 0;
+  if (n > 0 && !outs && !(okv && std::string(okv) == "level")) {
+    DeviceGuard g(s.device);
+    cap = online_sweep_capacity(k, ctx->f64);  // 0 (occupancy query failed): the level replay
+  }
+  // touched-row counts (UpdateSeparatedHashMap.updates, OfflineSpark.scala:33-67): counted on the
+  // device by the sweep's plan, else here
+  if (cap == 0) {
   seen_u.assign(ctx->U.rows(), 0);
   seen_i.assign(ctx->I.rows(), 0);
   // flags set with plain relaxed stores, and only when still clear (a locked exchange per rating
@@ -1695,6 +1707,7 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
   if (tu) *tu = cu;
   if (ti) *ti = ci;
   clk.lap("online: touched rows");
+  }
   // new rows take the slab rows the fast DSGD schedule keeps zeroed (padding / idle prefetch
   // rows past the real ones): that schedule is void now, a further fit must prepare again
   if (ctx->prepared && !ctx->f64 && (!fu.empty() || !fi.empty())) ctx->prepared = false;
@@ -1734,16 +1747,6 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
         order.insert(order.end(), c.begin(), c.end());
       }
   }
-  const bool outs = uout || iout;
-  // one persistent launch (the default; MFHIP_ONLINE_KERNEL=level forces the level-by-level
-  // replay, which is also the path with per-rating outputs): NFLX 1M-rating batches 37-38M vs
-  // 28-30M ratings/s end to end
-  const char* okv = std::getenv("MFHIP_ONLINE_KERNEL");
-  int cap = 0;
-  if (!outs && !(okv && std::string(okv) == "level")) {
-    DeviceGuard g(s.device);
-    cap = online_sweep_capacity(k, ctx->f64);  // 0 (occupancy query failed): the level replay
-  }
   if (cap > 0) {
     // one persistent launch (k_online_sweep): items spread over the waves, each wave's updates in
     // sequence order, and per update the number of earlier updates of its user (its ticket value)
@@ -1774,9 +1777,11 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
     s.det_dev.alloc(ebytes + qbytes);
     sc.wbeg.alloc(static_cast<size_t>(W + 1) * 8);
     const uint32_t* du = sc.in.as<uint32_t>();
+    sc.touched.alloc(8);
     online_sweep_plan(s.stream, sc, du, du + n, reinterpret_cast<const double*>(du + 2 * n), n, W32,
-                      static_cast<uint32_t>(ctx->U.rows()), s.det_dev.as<DetEntry>(),
-                      reinterpret_cast<uint32_t*>(s.det_dev.as<char>() + ebytes), sc.wbeg.as<int64_t>());
+                      static_cast<uint32_t>(ctx->U.rows()), static_cast<uint32_t>(ctx->I.rows()),
+                      s.det_dev.as<DetEntry>(), reinterpret_cast<uint32_t*>(s.det_dev.as<char>() + ebytes),
+                      sc.wbeg.as<int64_t>(), sc.touched.as<int32_t>());
     sc.uticket.alloc(static_cast<size_t>(std::max<int64_t>(ctx->U.rows(), 1)) * 4);
     MF_HIP(hipMemsetAsync(sc.uticket.get(), 0, static_cast<size_t>(std::max<int64_t>(ctx->U.rows(), 1)) * 4, s.stream));
     sc.err.alloc(4);
@@ -1788,11 +1793,14 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
                           ctx->P.online_learning_rate, ctx->f64, sc.uticket.as<int32_t>(), sc.err.as<int32_t>());
     }
     MF_HIP(hipGetLastError());
-    int32_t err = 0;
+    int32_t err = 0, touched[2] = {0, 0};
     MF_HIP(hipMemcpyAsync(&err, sc.err.get(), 4, hipMemcpyDeviceToHost, s.stream));
+    MF_HIP(hipMemcpyAsync(touched, sc.touched.get(), 8, hipMemcpyDeviceToHost, s.stream));
     MF_HIP(hipStreamSynchronize(s.stream));
     clk.lap("online: sweep (device)");
     if (err) fail(MF_ERR_TIMEOUT, "online sweep: a ticket wait timed out");
+    if (tu) *tu = touched[0];
+    if (ti) *ti = touched[1];
     ctx->stats.kernel_launches += 1;
     ctx->stats.updates += n;
     return;

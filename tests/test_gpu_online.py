@@ -224,10 +224,13 @@ def test_online_sweep_edge_batches(monkeypatch, shape):
         p.num_factors, p.mode, p.online_learning_rate = 32, L.MODE_FAST_F32, 0.01
         with mfhip.Context(p) as ctx:
             for s in range(0, n, 10000):
+                bu, bi = u[s:s + 10000], i[s:s + 10000]
                 if flav == L.ONLINE_SPARK_SWEEP:
-                    ctx.online_update(u[s:s + 10000], i[s:s + 10000], r[s:s + 10000], flav, num_partitions=4)
+                    tu, ti = ctx.online_update(bu, bi, r[s:s + 10000], flav, num_partitions=4)
                 else:
-                    ctx.online_update(u[s:s + 10000], i[s:s + 10000], r[s:s + 10000], flav)
+                    tu, ti = ctx.online_update(bu, bi, r[s:s + 10000], flav)
+                # touched rows (device-counted on the sweep path)
+                assert (tu, ti) == (len(np.unique(bu)), len(np.unique(bi)))
             res[kern] = (ctx.factors(0), ctx.factors(1))
     for side in (0, 1):
         assert np.array_equal(res["level"][side][0], res["sweep"][side][0])
