@@ -124,7 +124,7 @@ __global__ __launch_bounds__(256) void k_level(const DetEntry* __restrict__ ent,
 // stored with agent-scope relaxed atomics (sc1), the wave drains its stores, then lane 0 stores
 // the ticket.  The per-update arithmetic is k_level's (kSgdNext), so the factors are bitwise the
 // level-by-level replay (tests/test_gpu_online.py).  A wait over ~1 s sets err and the wave leaves.
-template <typename T, int KPL>
+template <typename T, int KPL, bool FULL>
 __global__ __launch_bounds__(64) void k_online_sweep(const int64_t* __restrict__ wbeg, const DetEntry* __restrict__ ent,
                                                      const uint32_t* __restrict__ useq, T* U, T* I, int k, T eta,
                                                      int32_t* ticket, int32_t* err) {
@@ -134,7 +134,7 @@ __global__ __launch_bounds__(64) void k_online_sweep(const int64_t* __restrict__
   __shared__ __attribute__((aligned(16))) T lds[64 * KPL];
   auto ld = [&](const T* row, int c) {
     const int f = lane + 64 * c;
-    return f < k ? __hip_atomic_load(row + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : T(0);
+    return FULL || f < k ? __hip_atomic_load(row + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : T(0);
   };
   auto wait_ticket = [&](uint32_t ur, int32_t q) -> bool {
     if (q == 0) return true;
@@ -161,6 +161,15 @@ __global__ __launch_bounds__(64) void k_online_sweep(const int64_t* __restrict__
   // (j - j0) & 1, loaded during update j - 2 when its ticket was already due (or during j - 1, or
   // else by j itself after waiting).  The loads ahead are issued after the update's stores, so the
   // drain before the ticket store waits for the stores only (vmcnt = the loads issued after them).
+  // With every lane in use (k == 64 * KPL, so every store instruction really issues) the ticket
+  // store is also deferred by one update: update j's ticket goes out during update j + 1, after
+  // a vmcnt that counts only j + 1's own stores and loads, so j's store drain overlaps j + 1's
+  // dot.  A wave never waits for a ticket while holding one back (it publishes first), so the
+  // earliest unfinished update stays runnable and the launch cannot deadlock.
+  constexpr bool defer = FULL;  // FULL: k == 64 * KPL (the host picks the instance)
+  uint32_t pend_u = 0;
+  int32_t pend_q = 0;
+  bool has_pend = false;
   T qv[KPL], sa[KPL], sb[KPL];
   bool ha = false, hb = false;
   bool have_q = false;
@@ -173,8 +182,13 @@ __global__ __launch_bounds__(64) void k_online_sweep(const int64_t* __restrict__
     T pv[KPL], pr[KPL];
     if (have) {
 #pragma unroll
-      for (int c = 0; c < KPL; ++c) pv[c] = lane + 64 * c < k ? slot[c] : T(0);
+      for (int c = 0; c < KPL; ++c) pv[c] = FULL || lane + 64 * c < k ? slot[c] : T(0);
     } else {
+      if (has_pend) {  // publish the held-back ticket before any wait
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        if (lane == 0) __hip_atomic_store(ticket + pend_u, pend_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        has_pend = false;
+      }
       if (!wait_ticket(ur, q)) return false;
 #pragma unroll
       for (int c = 0; c < KPL; ++c) pv[c] = ld(p, c);
@@ -199,28 +213,30 @@ __global__ __launch_bounds__(64) void k_online_sweep(const int64_t* __restrict__
 #pragma unroll
     for (int c = 0; c < KPL; ++c) pr[c] = pv[c] * qv[c];
     const T e = r - seq_dot_lds<T, KPL>(pr, k, lds, lane);
+    // the tickets are looked at before the stores (so no wait for them lands behind the stores)
+    const bool g1 = n1 && u1 != ur && (q1 == 0 || __builtin_amdgcn_readfirstlane(t1) == q1);
+    const bool g2 = n2 && u2 != ur && (q2 == 0 || __builtin_amdgcn_readfirstlane(t2) == q2);
     const T le = eta * e;  // learningRate * e * i == (learningRate * e) * i
     T qnew[KPL];
 #pragma unroll
     for (int c = 0; c < KPL; ++c) {
       const int f = lane + 64 * c;
       qnew[c] = qv[c] + le * pv[c];
-      if (f < k) __hip_atomic_store(p + f, pv[c] + le * qv[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (FULL || f < k) __hip_atomic_store(p + f, pv[c] + le * qv[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 #pragma unroll
     for (int c = 0; c < KPL; ++c) qv[c] = qnew[c];
     // the item row is written back when the wave's next update is on another item (or at the end)
-    if (j + 1 == j1 || ent[j + 1].i != ir) {
+    const bool istore = j + 1 == j1 || ent[j + 1].i != ir;
+    if (istore) {
       T* qi = I + static_cast<size_t>(ir) * k;
 #pragma unroll
       for (int c = 0; c < KPL; ++c) {
         const int f = lane + 64 * c;
-        if (f < k) __hip_atomic_store(qi + f, qv[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (FULL || f < k) __hip_atomic_store(qi + f, qv[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       have_q = false;
     }
-    const bool g1 = n1 && u1 != ur && (q1 == 0 || __builtin_amdgcn_readfirstlane(t1) == q1);
-    const bool g2 = n2 && u2 != ur && (q2 == 0 || __builtin_amdgcn_readfirstlane(t2) == q2);
     // the loads ahead must issue after this update's stores (the vmcnt below counts on it)
     __asm__ volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
@@ -230,19 +246,41 @@ __global__ __launch_bounds__(64) void k_online_sweep(const int64_t* __restrict__
     }
     have = g2;
     if (g2) ld_row(U + static_cast<size_t>(u2) * k, slot);
-    // vmcnt(n): every operation older than the n loads just issued (this update's stores) has
-    // landed; vector memory operations complete in issue order
-    constexpr int V1 = KPL, V2 = 2 * KPL;
-    constexpr int kW1 = 0x0F70 | (V1 & 15) | ((V1 >> 4) << 14), kW2 = 0x0F70 | (V2 & 15) | ((V2 >> 4) << 14);
-    if (g1 && g2) __builtin_amdgcn_s_waitcnt(kW2);
-    else if (g1 || g2) __builtin_amdgcn_s_waitcnt(kW1);
-    else __builtin_amdgcn_s_waitcnt(0x0F70);
-    if (lane == 0) __hip_atomic_store(ticket + ur, q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // vmcnt(n): every operation older than the n just issued has landed (vector memory
+    // operations complete in issue order)
+    constexpr int kW1 = 0x0F70 | ((1 * KPL) & 15) | (((1 * KPL) >> 4) << 14);
+    constexpr int kW2 = 0x0F70 | ((2 * KPL) & 15) | (((2 * KPL) >> 4) << 14);
+    constexpr int kW3 = 0x0F70 | ((3 * KPL) & 15) | (((3 * KPL) >> 4) << 14);
+    constexpr int kW4 = 0x0F70 | ((4 * KPL) & 15) | (((4 * KPL) >> 4) << 14);
+    if (defer) {
+      // n = this update's stores (its user row, its item row when written back) and the loads
+      // ahead: the previous update's stores have landed, so its ticket goes out now
+      const int m = (istore ? 2 : 1) + (g1 ? 1 : 0) + (g2 ? 1 : 0);
+      if (m == 1) __builtin_amdgcn_s_waitcnt(kW1);
+      else if (m == 2) __builtin_amdgcn_s_waitcnt(kW2);
+      else if (m == 3) __builtin_amdgcn_s_waitcnt(kW3);
+      else __builtin_amdgcn_s_waitcnt(kW4);
+      if (has_pend && lane == 0)
+        __hip_atomic_store(ticket + pend_u, pend_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      pend_u = ur;
+      pend_q = q + 1;
+      has_pend = true;
+    } else {
+      // n = the loads just issued: this update's stores have landed
+      if (g1 && g2) __builtin_amdgcn_s_waitcnt(kW2);
+      else if (g1 || g2) __builtin_amdgcn_s_waitcnt(kW1);
+      else __builtin_amdgcn_s_waitcnt(0x0F70);
+      if (lane == 0) __hip_atomic_store(ticket + ur, q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     return true;
   };
   for (int64_t j = j0; j < j1; j += 2) {
     if (!step(j, sa, ha, sb, hb)) return;
     if (j + 1 < j1 && !step(j + 1, sb, hb, sa, ha)) return;
+  }
+  if (has_pend) {
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    if (lane == 0) __hip_atomic_store(ticket + pend_u, pend_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -251,7 +289,12 @@ int online_capacity() {
   int dev = 0, cus = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_online_sweep<T, KPL>, 64, 0) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_online_sweep<T, KPL, false>, 64, 0) != hipSuccess)
+    return 0;
+  int per_cu_full = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_full, k_online_sweep<T, KPL, true>, 64, 0) != hipSuccess)
+    return 0;
+  per_cu = std::min(per_cu, per_cu_full);
   return cus * per_cu;
 }
 
@@ -461,8 +504,15 @@ void launch_online_sweep(hipStream_t st, int nw, const int64_t* wbeg, const DetE
                          void* U, void* I, int k, double eta, bool f64, int32_t* ticket, int32_t* err) {
   if (nw <= 0) return;
   const dim3 g(static_cast<unsigned>(nw)), b(64);
-#define MF_OS(T, KPL) hipLaunchKernelGGL((k_online_sweep<T, KPL>), g, b, 0, st, wbeg, ent, useq, static_cast<T*>(U), \
-                                         static_cast<T*>(I), k, static_cast<T>(eta), ticket, err)
+#define MF_OS(T, KPL)                                                                                       \
+  do {                                                                                                      \
+    if (k == 64 * (KPL))                                                                                    \
+      hipLaunchKernelGGL((k_online_sweep<T, KPL, true>), g, b, 0, st, wbeg, ent, useq, static_cast<T*>(U),  \
+                         static_cast<T*>(I), k, static_cast<T>(eta), ticket, err);                          \
+    else                                                                                                    \
+      hipLaunchKernelGGL((k_online_sweep<T, KPL, false>), g, b, 0, st, wbeg, ent, useq, static_cast<T*>(U), \
+                         static_cast<T*>(I), k, static_cast<T>(eta), ticket, err);                          \
+  } while (0)
   if (f64) {
     if (k <= 64) MF_OS(double, 1);
     else if (k <= 128) MF_OS(double, 2);

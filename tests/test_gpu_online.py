@@ -201,8 +201,9 @@ def test_online_sweep_equals_level_replay(monkeypatch, mode, k):
         assert np.array_equal(res["level"][side][1], res["sweep"][side][1])
 
 
+@pytest.mark.parametrize("k", [32, 64])  # 64: every lane in use, the deferred-ticket instance
 @pytest.mark.parametrize("shape", ["one", "few", "one_user", "one_item", "spark"])
-def test_online_sweep_edge_batches(monkeypatch, shape):
+def test_online_sweep_edge_batches(monkeypatch, shape, k):
     """Edge batches of the device-built sweep plan (kernels_online.hip) against the level replay,
     bit for bit: a single rating, fewer ratings than waves, one user across every wave (a ticket
     chain through all of them), one item (one wave holds the whole batch), and the Spark-sweep
@@ -221,7 +222,7 @@ def test_online_sweep_edge_batches(monkeypatch, shape):
     for kern in ("level", "sweep"):
         monkeypatch.setenv("MFHIP_ONLINE_KERNEL", kern)
         p = L.default_params()
-        p.num_factors, p.mode, p.online_learning_rate = 32, L.MODE_FAST_F32, 0.01
+        p.num_factors, p.mode, p.online_learning_rate = k, L.MODE_FAST_F32, 0.01
         with mfhip.Context(p) as ctx:
             for s in range(0, n, 10000):
                 bu, bi = u[s:s + 10000], i[s:s + 10000]
