@@ -33,6 +33,21 @@ class IdIndex {
     }
   }
 
+  // find() of n ids into rows (-1 as 0xFFFFFFFF), the slot of the id kPrefetch places ahead
+  // prefetched: the table is far larger than L2, so independent lookups overlap their misses.
+  void find_many(const int32_t* ids, int64_t n, uint32_t* rows) const {
+    constexpr int64_t kPrefetch = 16;
+    if (slots_.empty()) {
+      for (int64_t j = 0; j < n; ++j) rows[j] = 0xFFFFFFFFu;
+      return;
+    }
+    for (int64_t j = 0; j < n && j < kPrefetch; ++j) __builtin_prefetch(&slots_[hash(ids[j]) & mask_]);
+    for (int64_t j = 0; j < n; ++j) {
+      if (j + kPrefetch < n) __builtin_prefetch(&slots_[hash(ids[j + kPrefetch]) & mask_]);
+      rows[j] = static_cast<uint32_t>(find(ids[j]));
+    }
+  }
+
   // Inserts id -> row if absent; returns the stored row.
   int32_t insert(int32_t id, int32_t row) {
     if (static_cast<uint64_t>(size_ + 1) * 2 > slots_.size()) rehash(slots_.empty() ? 16 : slots_.size() * 2);

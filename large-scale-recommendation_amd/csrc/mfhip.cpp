@@ -1640,12 +1640,35 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
   const int k = ctx->P.num_factors;
   PhaseClock clk;
   std::vector<int32_t> fu, fi;
-  if (static_cast<int64_t>(ctx->on_ur.size()) < n) {
-    ctx->on_ur.resize(n);
-    ctx->on_ir.resize(n);
+  // one persistent launch (the default; MFHIP_ONLINE_KERNEL=level forces the level-by-level
+  // replay, which is also the path with per-rating outputs): NFLX 1M-rating batches 1.1e8 vs
+  // 0.5e8 ratings/s end to end
+  const bool outs = uout || iout;
+  const char* okv = std::getenv("MFHIP_ONLINE_KERNEL");
+  int cap = 0;
+  if (n > 0 && !outs && !(okv && std::string(okv) == "level")) {
+    DeviceGuard g(s.device);
+    cap = online_sweep_capacity(k, ctx->f64);  // 0 (occupancy query failed): the level replay
   }
-  std::vector<uint32_t>& ur = ctx->on_ur;
-  std::vector<uint32_t>& ir = ctx->on_ir;
+  // the sweep in arrival order takes the rows straight into its pinned upload buffer (user rows,
+  // item rows, ratings: 16 B per rating), with no staging pass; otherwise they go to on_ur / on_ir
+  const bool direct = cap > 0 && flavour != MF_ONLINE_SPARK_SWEEP;
+  uint32_t* ur = nullptr;
+  uint32_t* ir = nullptr;
+  if (direct) {
+    DeviceGuard g(s.device);
+    MF_HIP(hipStreamSynchronize(s.stream));  // det_pin may still feed an earlier copy
+    s.det_pin.alloc(static_cast<size_t>(n) * 16);
+    ur = s.det_pin.as<uint32_t>();
+    ir = ur + n;
+  } else {
+    if (static_cast<int64_t>(ctx->on_ur.size()) < n) {
+      ctx->on_ur.resize(n);
+      ctx->on_ir.resize(n);
+    }
+    ur = ctx->on_ur.data();
+    ir = ctx->on_ir.data();
+  }
   const int64_t u0 = ctx->U.rows(), i0 = ctx->I.rows();
   std::vector<uint8_t> seen_u, seen_i;
   int64_t cu = 0, ci = 0;
@@ -1655,12 +1678,11 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
   constexpr uint32_t kMiss = 0xFFFFFFFFu;
   std::atomic<int64_t> misses{0};
   parallel_for(n, [&](int64_t lo2, int64_t hi2, int) {
+    ctx->U.index.find_many(u + lo2, hi2 - lo2, ur + lo2);
+    ctx->I.index.find_many(i + lo2, hi2 - lo2, ir + lo2);
+    if (direct) std::memcpy(reinterpret_cast<double*>(ir + n) + lo2, r + lo2, static_cast<size_t>(hi2 - lo2) * 8);
     int64_t m = 0;
-    for (int64_t j = lo2; j < hi2; ++j) {
-      ur[j] = static_cast<uint32_t>(ctx->U.index.find(u[j]));  // -1 -> kMiss
-      ir[j] = static_cast<uint32_t>(ctx->I.index.find(i[j]));
-      m += (ur[j] == kMiss) + (ir[j] == kMiss);
-    }
+    for (int64_t j = lo2; j < hi2; ++j) m += (ur[j] == kMiss) + (ir[j] == kMiss);
     misses += m;
   });
   if (misses > 0)
@@ -1669,16 +1691,6 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
       if (ir[j] == kMiss) ir[j] = static_cast<uint32_t>(online_row(ctx, ctx->I, i[j], fi));
     }
   clk.lap("online: id lookup");
-  // one persistent launch (the default; MFHIP_ONLINE_KERNEL=level forces the level-by-level
-  // replay, which is also the path with per-rating outputs): NFLX 1M-rating batches 83-87M vs
-  // 51M ratings/s end to end
-  const bool outs = uout || iout;
-  const char* okv = std::getenv("MFHIP_ONLINE_KERNEL");
-  int cap = 0;
-  if (n > 0 && !outs && !(okv && std::string(okv) == "level")) {
-    DeviceGuard g(s.device);
-    cap = online_sweep_capacity(k, ctx->f64);  // 0 (occupancy query failed): the level replay
-  }
   // touched-row counts (UpdateSeparatedHashMap.updates, OfflineSpark.scala:33-67): counted on the
   // device by the sweep's plan, else here
   if (cap == 0) {
@@ -1758,20 +1770,23 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
     OnlineSweepScratch& sc = s.online_sc;
     const size_t ebytes = static_cast<size_t>(n) * sizeof(DetEntry), qbytes = static_cast<size_t>(n) * 4;
     const size_t ibytes = static_cast<size_t>(n) * 16;
-    MF_HIP(hipStreamSynchronize(s.stream));  // det_pin may still feed an earlier copy
-    s.det_pin.alloc(ibytes);
+    if (!direct) {  // the Spark-sweep order: staged here
+      MF_HIP(hipStreamSynchronize(s.stream));  // det_pin may still feed an earlier copy
+      s.det_pin.alloc(ibytes);
+      uint32_t* pu = s.det_pin.as<uint32_t>();
+      uint32_t* pi = pu + n;
+      double* pr = reinterpret_cast<double*>(pi + n);
+      parallel_for(n, [&](int64_t lo2, int64_t hi2, int) {
+        for (int64_t x = lo2; x < hi2; ++x) {
+          const int32_t j = order[x];
+          pu[x] = ur[j];
+          pi[x] = ir[j];
+          pr[x] = r[j];
+        }
+      });
+      clk.lap("online: sweep staging");
+    }
     uint32_t* pu = s.det_pin.as<uint32_t>();
-    uint32_t* pi = pu + n;
-    double* pr = reinterpret_cast<double*>(pi + n);
-    parallel_for(n, [&](int64_t lo2, int64_t hi2, int) {
-      for (int64_t x = lo2; x < hi2; ++x) {
-        const int32_t j = order[x];
-        pu[x] = ur[j];
-        pi[x] = ir[j];
-        pr[x] = r[j];
-      }
-    });
-    clk.lap("online: sweep staging");
     sc.in.alloc(ibytes);
     MF_HIP(hipMemcpyAsync(sc.in.get(), pu, ibytes, hipMemcpyHostToDevice, s.stream));
     s.det_dev.alloc(ebytes + qbytes);
@@ -1807,8 +1822,8 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
   }
   std::vector<double> rr(r, r + n);
   OrderedSeq sq;
-  sq.u = ur.data();
-  sq.i = ir.data();
+  sq.u = ur;
+  sq.i = ir;
   sq.r = rr.data();
   sq.order = order.data();
   sq.len = n;
