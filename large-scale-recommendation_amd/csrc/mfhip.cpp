@@ -62,6 +62,7 @@ struct DetBuf {
   hipEvent_t swept = nullptr;   // the sweep that read `dev` finished (dev may be rewritten)
   bool pending = false;         // `copied` was recorded and not yet waited for
   int64_t n = 0, nw = 0, keeps = 0, defers = 0;
+  DetStepScratch scratch;  // build_det_step's gathers for this slot (kept: no page faults per superstep)
 };
 
 struct Shard {
@@ -916,7 +917,7 @@ void det_build(mf_ctx* ctx, int64_t superstep, int slot) {
     DetStepOut out{reinterpret_cast<DetWave*>(base + o.waves), reinterpret_cast<uint32_t*>(base + o.u),
                    reinterpret_cast<uint32_t*>(base + o.i), reinterpret_cast<uint32_t*>(base + o.qf),
                    reinterpret_cast<double*>(base + o.r)};
-    build_det_step(ctx->rb, ctx->U, ctx->I, s.det_layout, blocks, seeds, ctx->P.has_seed != 0, out);
+    build_det_step(ctx->rb, ctx->U, ctx->I, s.det_layout, blocks, seeds, ctx->P.has_seed != 0, out, &db.scratch);
     for (int64_t x = 0; x < db.n; ++x) {
       db.keeps += (out.qf[x] & kDetKeepQ) != 0;
       db.defers += (out.qf[x] & kDetDeferQ) != 0;

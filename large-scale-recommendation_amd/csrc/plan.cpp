@@ -334,9 +334,14 @@ void build_det_layout(DetSweepLayout& L, const RatingBlocks& rb, const SideLayou
 
 void build_det_step(const RatingBlocks& rb, const SideLayout& U, const SideLayout& I, const DetSweepLayout& L,
                     const std::vector<int64_t>& blocks, const std::vector<int64_t>& seeds, bool seeded,
-                    const DetStepOut& out) {
+                    const DetStepOut& out, DetStepScratch* scratch) {
   const int32_t nb = rb.n_blocks;
   const int64_t nbk = static_cast<int64_t>(blocks.size());
+  DetStepScratch local;
+  DetStepScratch& sc = scratch ? *scratch : local;
+  for (auto* v : {&sc.order, &sc.wv}) if (static_cast<int64_t>(v->size()) < nbk) v->resize(nbk);
+  for (auto* v : {&sc.gu, &sc.gi}) if (static_cast<int64_t>(v->size()) < nbk) v->resize(nbk);
+  if (static_cast<int64_t>(sc.gr.size()) < nbk) sc.gr.resize(nbk);
   std::vector<int64_t> e0(nbk + 1, 0), w0(nbk + 1, 0);  // entry / wave offsets of each block
   for (int64_t x = 0; x < nbk; ++x) {
     e0[x + 1] = e0[x] + rb.size(blocks[x]);
@@ -347,34 +352,127 @@ void build_det_step(const RatingBlocks& rb, const SideLayout& U, const SideLayou
     std::random_device rd;
     for (auto& v : rseeds) v = (static_cast<uint64_t>(rd()) << 32) ^ rd();
   }
+  // 1. the shuffle of each block (serial within a block: one JavaRandom stream)
+  auto& order = sc.order;
   parallel_tasks(nbk, [&](int64_t x) {
-    const int64_t b = blocks[x], len = rb.size(b), st = rb.start[b];
+    const int64_t len = rb.size(blocks[x]);
     if (len == 0) return;
-    const int32_t p = static_cast<int32_t>(b / nb), q = static_cast<int32_t>(b % nb);
-    const int64_t u0 = U.block_start[p], nu = U.block_start[p + 1] - u0, i0 = I.block_start[q];
-    std::vector<int32_t> order(len);
+    order[x].resize(len);
     JavaRandom rng(seeded ? seeds[x] : static_cast<int64_t>(rseeds[x]));
-    scala_shuffle(rng, order.data(), len);  // DSGDforMF.scala:392-393
-    const auto& iw = L.item_wave[b];
-    const int32_t W = L.block_waves[b];
-    std::vector<int64_t> woff(W + 1, 0);
-    for (int64_t j = 0; j < len; ++j) woff[iw[rb.irow[st + order[j]] - i0] + 1]++;
-    for (int32_t w = 0; w < W; ++w) woff[w + 1] += woff[w];
-    for (int32_t w = 0; w < W; ++w)
-      out.waves[w0[x] + w] = DetWave{e0[x] + woff[w], static_cast<int32_t>(woff[w + 1] - woff[w]), 0};
-    std::vector<int32_t> useq(nu, 0);
-    std::vector<int64_t> cur(woff.begin(), woff.end() - 1);
-    for (int64_t j = 0; j < len; ++j) {
-      const int64_t e = st + order[j];
+    scala_shuffle(rng, order[x].data(), len);  // DSGDforMF.scala:392-393
+  });
+  // the rest runs over chunks of shuffle positions, so a large block does not hold up the step
+  constexpr int64_t kChunk = int64_t{1} << 18;
+  struct Chunk {
+    int64_t x, j0, j1;
+  };
+  std::vector<Chunk> ch;
+  std::vector<int64_t> ch0(nbk + 1, 0);
+  for (int64_t x = 0; x < nbk; ++x) {
+    ch0[x] = static_cast<int64_t>(ch.size());
+    const int64_t len = rb.size(blocks[x]);
+    for (int64_t j = 0; j < len; j += kChunk) ch.push_back(Chunk{x, j, std::min(len, j + kChunk)});
+  }
+  ch0[nbk] = static_cast<int64_t>(ch.size());
+  auto& gu = sc.gu;
+  auto& gi = sc.gi;
+  auto& gr = sc.gr;
+  auto& wv = sc.wv;
+  for (int64_t x = 0; x < nbk; ++x) {
+    const int64_t len = rb.size(blocks[x]);
+    gu[x].resize(len);
+    gi[x].resize(len);
+    gr[x].resize(len);
+    wv[x].resize(len);
+  }
+  auto block_geom = [&](int64_t x, int64_t& st, int64_t& u0, int64_t& nu, int64_t& i0) {
+    const int64_t b = blocks[x];
+    const int32_t p = static_cast<int32_t>(b / nb), q = static_cast<int32_t>(b % nb);
+    st = rb.start[b];
+    u0 = U.block_start[p];
+    nu = U.block_start[p + 1] - u0;
+    i0 = I.block_start[q];
+  };
+  // 2. per chunk: the ratings in shuffle order, gathered once (the only random reads), their
+  // waves, and per-chunk counts of waves and users
+  std::vector<std::vector<int64_t>> wcur(ch.size());
+  std::vector<std::vector<int32_t>> ucur(ch.size());
+  parallel_tasks(static_cast<int64_t>(ch.size()), [&](int64_t t) {
+    const Chunk c = ch[t];
+    int64_t st, u0, nu, i0;
+    block_geom(c.x, st, u0, nu, i0);
+    const auto& iw = L.item_wave[blocks[c.x]];
+    const int32_t* ord = order[c.x].data();
+    wcur[t].assign(L.block_waves[blocks[c.x]], 0);
+    ucur[t].assign(nu, 0);
+    constexpr int64_t kAhead = 16;  // the rating arrays are far larger than the caches
+    for (int64_t j = c.j0; j < c.j1; ++j) {
+      if (j + kAhead < c.j1) {
+        const int64_t ea = st + ord[j + kAhead];
+        __builtin_prefetch(&rb.urow[ea]);
+        __builtin_prefetch(&rb.irow[ea]);
+        __builtin_prefetch(&rb.r[ea]);
+      }
+      const int64_t e = st + ord[j];
       const uint32_t ur = rb.urow[e], ir = rb.irow[e];
-      const int64_t at = e0[x] + cur[iw[ir - i0]]++;
-      out.u[at] = ur;
-      out.i[at] = ir;
-      out.qf[at] = static_cast<uint32_t>(useq[ur - u0]++);
-      out.r[at] = rb.r[e];
+      gu[c.x][j] = ur;
+      gi[c.x][j] = ir;
+      gr[c.x][j] = rb.r[e];
+      const int32_t w = iw[ir - i0];
+      wv[c.x][j] = w;
+      wcur[t][w]++;
+      ucur[t][ur - u0]++;
     }
-    for (int32_t w = 0; w < W; ++w) {  // items repeated back to back stay in registers
-      const int64_t a = e0[x] + woff[w], z = e0[x] + woff[w + 1];
+  });
+  // 3. per block: wave offsets, and each chunk's start per wave and per user (its counts turned
+  // into exclusive prefixes over the block's chunks)
+  parallel_tasks(nbk, [&](int64_t x) {
+    const int32_t W = L.block_waves[blocks[x]];
+    if (rb.size(blocks[x]) == 0) return;
+    int64_t st, u0, nu, i0;
+    block_geom(x, st, u0, nu, i0);
+    int64_t at = e0[x];
+    for (int32_t w = 0; w < W; ++w) {
+      const int64_t wbeg = at;
+      for (int64_t t = ch0[x]; t < ch0[x + 1]; ++t) {
+        const int64_t cnt = wcur[t][w];
+        wcur[t][w] = at;
+        at += cnt;
+      }
+      out.waves[w0[x] + w] = DetWave{wbeg, static_cast<int32_t>(at - wbeg), 0};
+    }
+    for (int64_t uu = 0; uu < nu; ++uu) {
+      int32_t run = 0;
+      for (int64_t t = ch0[x]; t < ch0[x + 1]; ++t) {
+        const int32_t cnt = ucur[t][uu];
+        ucur[t][uu] = run;
+        run += cnt;
+      }
+    }
+  });
+  // 4. per chunk: the scatter into wave-major order; useq = the user's count of earlier ratings
+  // in shuffle order
+  parallel_tasks(static_cast<int64_t>(ch.size()), [&](int64_t t) {
+    const Chunk c = ch[t];
+    int64_t st, u0, nu, i0;
+    block_geom(c.x, st, u0, nu, i0);
+    std::vector<int64_t>& cur = wcur[t];
+    std::vector<int32_t>& useq = ucur[t];
+    for (int64_t j = c.j0; j < c.j1; ++j) {
+      const uint32_t ur = gu[c.x][j];
+      const int64_t at = cur[wv[c.x][j]]++;
+      out.u[at] = ur;
+      out.i[at] = gi[c.x][j];
+      out.qf[at] = static_cast<uint32_t>(useq[ur - u0]++);
+      out.r[at] = gr[c.x][j];
+    }
+  });
+  // 5. items repeated back to back stay in registers
+  parallel_tasks(nbk, [&](int64_t x) {
+    const int32_t W = L.block_waves[blocks[x]];
+    for (int32_t w = 0; w < W; ++w) {
+      const DetWave dw = out.waves[w0[x] + w];
+      const int64_t a = dw.begin, z = dw.begin + dw.count;
       for (int64_t y = a; y < z; ++y) {
         if (y > a && out.i[y - 1] == out.i[y]) out.qf[y] |= kDetKeepQ;
         if (y + 1 < z && out.i[y + 1] == out.i[y]) out.qf[y] |= kDetDeferQ;

@@ -142,6 +142,14 @@ struct DetSweepLayout {
 void build_det_layout(DetSweepLayout& L, const RatingBlocks& rb, const SideLayout& U, const SideLayout& I, int32_t c,
                       int32_t shard, int32_t waves_per_superstep);
 
+// Host scratch of build_det_step, kept by the caller across supersteps (per staging slot), so
+// the ~24 B per rating it gathers into are not page-faulted in again every superstep.
+struct DetStepScratch {
+  std::vector<RecVec<int32_t>> order, wv;
+  std::vector<RecVec<uint32_t>> gu, gi;
+  std::vector<RecVec<double>> gr;
+};
+
 // One superstep's entries (SoA, wave-major, each wave in shuffle-position order) for the rating
 // blocks `blocks` with their shuffle seeds (order = scala_shuffle(new Random(seed)), :392-393;
 // seeded = false: a random seed).  Sizes: waves = sum of block_waves, entries = sum of block sizes.
@@ -154,7 +162,8 @@ struct DetStepOut {
 };
 void build_det_step(const RatingBlocks& rb, const SideLayout& U, const SideLayout& I, const DetSweepLayout& L,
                     const std::vector<int64_t>& blocks, const std::vector<int64_t>& seeds, bool seeded,
-                    const DetStepOut& out);
+                    const DetStepOut& out,
+                    DetStepScratch* scratch = nullptr);
 
 // ---------------------------------------------------------------------------------------
 // Fast mode.
