@@ -1764,7 +1764,9 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
     // one persistent launch (k_online_sweep): items spread over the waves, each wave's updates in
     // sequence order, and per update the number of earlier updates of its user (its ticket value)
     DeviceGuard g(s.device);
-    const int64_t W = std::max<int64_t>(1, std::min<int64_t>({static_cast<int64_t>(cap / 2), 4096, n}));
+    int64_t wmax = 4096;
+    if (const char* v = std::getenv("MFHIP_ONLINE_WAVES")) wmax = std::max(1, std::atoi(v));  // experiments
+    const int64_t W = std::max<int64_t>(1, std::min<int64_t>({static_cast<int64_t>(cap / 2), wmax, n}));
     const uint32_t W32 = static_cast<uint32_t>(W);
     // the batch in sequence order goes up as is (16 bytes an update); the per-wave lists and the
     // tickets are built on the device (online_sweep_plan, kernels_online.hip)
