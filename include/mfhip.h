@@ -25,6 +25,9 @@
 
 #include <stdint.h>
 
+/* Testing hooks (schedule and ring invariants, plan digests) are declared in mfhip_testing.h:
+   exported by the same library for the test suite, not part of the product surface. */
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -91,11 +94,7 @@ typedef struct mf_params {
   /* fast-mode blocking: MF_BLOCKING_REFERENCE (default) or MF_BLOCKING_BALANCED;
      the deterministic mode always uses the reference's blocking */
   int32_t fast_blocking;
-  /* fast-mode hot-item replicas: an item with more than this many ratings in one rating block
-     is swept as ceil(m / fast_item_split) parallel chains averaged when the superstep ends
-     (plan.hpp SplitItem).  0 (default) = off: every item is one sequential chain. */
-  int32_t fast_item_split;
-  int32_t reserved[5];
+  int32_t reserved[6];
 } mf_params;
 
 /* Aggregated device statistics (timed with HIP events on the library's stream). */
@@ -228,56 +227,6 @@ int mf_jvm_block_of(int32_t id, int64_t seed, int32_t n_blocks, int32_t* out);  
 int mf_jvm_random_factors(int64_t rng_seed, int32_t k, double* out);   /* k x nextDouble */
 int mf_learning_rate(int method, double lr, int32_t iteration, double lambda, double arg,
                      double* out);
-
-/* Testing hooks (host only, no GPU): expose the device schedules so their invariants can be
-   checked on a CPU machine.
-   mf_debug_levels: dependency level of each update of a sequence visited in `order`
-   (order may be NULL = identity); rows are caller indices.
-   mf_debug_fast_schedule: for every input rating, the rating block (ub*n+ib), rotation
-   sub-step, item group and position inside its cell of the fast-mode plan with `groups`
-   groups per rating block (groups < 0: the systolic sweep's per-block choice for a budget of
-   -groups waves per superstep, as mf_dsgd_prepare makes it with MFHIP_SYS_WAVES=-groups),
-   MF_BLOCKING_* `blocking` and hazard window `window` (0: 8). */
-int mf_debug_levels(const uint32_t* urow, const uint32_t* irow, const int32_t* order, int64_t n,
-                    int32_t* level_out);
-int mf_debug_fast_schedule(const int32_t* users, const int32_t* items, int64_t n, int32_t n_blocks,
-                           int64_t seed, int32_t groups, int32_t blocking, int32_t window, int32_t* block_out,
-                           int32_t* substep_out, int32_t* group_out, int64_t* pos_out);
-/* mf_debug_fast_split: mf_debug_fast_schedule with hot-item replicas (mf_params.fast_item_split
-   = item_split); replica_out[j] = 0 when rating j updates its item's own row, r >= 1 when it
-   updates replica r (merged when the superstep ends). */
-int mf_debug_fast_split(const int32_t* users, const int32_t* items, int64_t n, int32_t n_blocks,
-                        int64_t seed, int32_t groups, int32_t blocking, int32_t window, int32_t item_split,
-                        int32_t* block_out, int32_t* substep_out, int32_t* group_out, int64_t* pos_out,
-                        int32_t* replica_out);
-/* mf_debug_fast_stream: the stream sweep's plan (k_sweep_stream; reference blocking) with G = groups
-   item groups and ustride * G user groups per rating block: rating j is in sub-step substep_out[j]
-   (0 .. ustride*G-1) of item group group_out[j], at pos_out[j] inside its cell.  Applying the
-   ratings sequentially in (sub-step, block, group, pos) order is what the sweep computes. */
-int mf_debug_fast_stream(const int32_t* users, const int32_t* items, int64_t n, int32_t n_blocks, int64_t seed,
-                         int32_t groups, int32_t ustride, int32_t window, int32_t* block_out, int32_t* substep_out,
-                         int32_t* group_out, int64_t* pos_out);
-/* mf_debug_stream_protocol: builds the stream sweep's plan exactly as mf_dsgd_prepare does on one
-   device (k, groups, ustride) and replays the kernel's hand-off protocol on the host:
-   *stuck_out = the supersteps whose waves could not all finish (0 = deadlock-free). */
-int mf_debug_stream_protocol(const int32_t* users, const int32_t* items, int64_t n, int32_t n_blocks, int64_t seed,
-                             int32_t groups, int32_t ustride, int32_t k, int64_t* stuck_out);
-/* mf_debug_ring_schedule: the item-block ring step ring_shift runs after superstep `superstep`
-   (1-based) on rank `rank` of `world` with n blocks (n = c * world): the item block it sends
-   (*out_blk) to rank *dst and the one it receives (*in_blk) from rank *src -- nextRatingBlock
-   (DSGDforMF.scala:611-619) over ranks. */
-int mf_debug_ring_schedule(int32_t rank, int32_t world, int32_t n_blocks, int64_t superstep, int32_t* out_blk,
-                           int32_t* in_blk, int32_t* dst, int32_t* src);
-/* mf_debug_plan_digest: after mf_dsgd_prepare of a fast-mode fit on one shard, an FNV-1a digest
-   of the device schedule -- the pair records, the wave table and (systolic) the per-wave cell
-   tables -- and the pair-record count: out[0] = digest, out[1] = records.  Compares the device-
-   built plan (kernels_plan.hip) with the host-built one (MFHIP_DEVICE_PLAN=0). */
-int mf_debug_plan_digest(mf_ctx* ctx, uint64_t out[2]);
-/* The plan window (records between two uses of a row inside a cell unless adjacent) the fast
-   sweep uses at rank k: the prefetch distance of the kernel selected for k. */
-int mf_fast_plan_window(int32_t k, int32_t* window_out);
-/* Name of the fast-mode sweep kernel used at rank k (for profiles and bench reports). */
-const char* mf_fast_kernel_name(int32_t k);
 
 #ifdef __cplusplus
 }

@@ -6,9 +6,13 @@
  *       -o libmfhipjni.so
  * Every non-zero status becomes a java.lang.RuntimeException carrying mf_last_error(), which is
  * what the reference throws for the same conditions (MatrixFactorization.scala:189-190, 270-271).
- * Arrays are pinned with GetPrimitiveArrayCritical only around the copy-in / copy-out calls (the
- * library never retains host pointers).  tests/test_abi.py compiles this file against include/mfhip.h
- * (with a minimal jni.h stand-in, this image has no JDK) so every call matches the C ABI.
+ * Array lengths are checked against what the C call reads or writes BEFORE any element is
+ * touched (IllegalArgumentException, as the reference's argument checks).  Arrays cross with
+ * Get<Type>ArrayElements / Release<Type>ArrayElements, never as JNI critical regions: a fit or a
+ * micro-batch runs for seconds, and a critical region held that long would stall the garbage
+ * collector of every Flink/Spark task thread.  (The library never retains host pointers.)
+ * tests/test_abi.py compiles this file against include/mfhip.h (with a minimal jni.h stand-in,
+ * this image has no JDK) so every call matches the C ABI.
  */
 #include <jni.h>
 #include <stdint.h>
@@ -16,20 +20,65 @@
 
 #include "mfhip.h"
 
+static void throw_named(JNIEnv* env, const char* cls, const char* msg) {
+  jclass ex = (*env)->FindClass(env, cls);
+  if (ex) (*env)->ThrowNew(env, ex, msg);
+}
+
 static int check(JNIEnv* env, int st) {
-  if (st != MF_OK) {
-    jclass ex = (*env)->FindClass(env, "java/lang/RuntimeException");
-    (*env)->ThrowNew(env, ex, mf_last_error());
-  }
+  if (st != MF_OK) throw_named(env, "java/lang/RuntimeException", mf_last_error());
   return st;
 }
-#define PIN(a) ((a) ? (*env)->GetPrimitiveArrayCritical(env, (a), NULL) : NULL)
-#define UNPIN(a, p, mode) \
-  do {                    \
-    if (a) (*env)->ReleasePrimitiveArrayCritical(env, (a), (p), (mode)); \
-  } while (0)
+
+/* 0 when ok; otherwise an IllegalArgumentException is pending. */
+static int require(JNIEnv* env, int ok, const char* msg) {
+  if (!ok) throw_named(env, "java/lang/IllegalArgumentException", msg);
+  return ok ? 0 : -1;
+}
+
+static jsize len(JNIEnv* env, jarray a) { return a ? (*env)->GetArrayLength(env, a) : 0; }
+
+/* Element access by copy (or by the VM's choice, never a critical region). */
+enum { kInt, kDouble, kByte };
+typedef struct {
+  jarray a;
+  void* p;
+  int kind;
+} Elems;
+
+static int acquire(JNIEnv* env, Elems* e, jarray a, int kind) {
+  e->a = a;
+  e->kind = kind;
+  e->p = NULL;
+  if (!a) return 0;
+  switch (kind) {
+    case kInt: e->p = (*env)->GetIntArrayElements(env, (jintArray)a, NULL); break;
+    case kDouble: e->p = (*env)->GetDoubleArrayElements(env, (jdoubleArray)a, NULL); break;
+    default: e->p = (*env)->GetByteArrayElements(env, (jbyteArray)a, NULL); break;
+  }
+  return e->p ? 0 : -1; /* NULL: OutOfMemoryError is pending */
+}
+
+/* mode 0: copy back (outputs), JNI_ABORT: discard (inputs). */
+static void release(JNIEnv* env, Elems* e, jint mode) {
+  if (!e->a || !e->p) return;
+  switch (e->kind) {
+    case kInt: (*env)->ReleaseIntArrayElements(env, (jintArray)e->a, (jint*)e->p, mode); break;
+    case kDouble: (*env)->ReleaseDoubleArrayElements(env, (jdoubleArray)e->a, (jdouble*)e->p, mode); break;
+    default: (*env)->ReleaseByteArrayElements(env, (jbyteArray)e->a, (jbyte*)e->p, mode); break;
+  }
+  e->p = NULL;
+}
+
 #define JFN(name) Java_hu_sztaki_ilab_recom_core_gpu_MfHip_##name
 #define CTX(h) ((mf_ctx*)(intptr_t)(h))
+
+/* The context's rank k (row length of every factor buffer), or -1 with an exception pending. */
+static jlong rank_of(JNIEnv* env, jlong h) {
+  mf_params p;
+  if (check(env, mf_get_params(CTX(h), &p)) != MF_OK) return -1;
+  return p.num_factors;
+}
 
 static void fill_params(mf_params* p, jint k, jint it, jdouble lambda, jdouble lr, jint lrm, jdouble lra, jint nb,
                         jlong seed, jboolean hs, jint mode) {
@@ -54,10 +103,11 @@ JNIEXPORT jlong JNICALL JFN(create)(JNIEnv* env, jclass c, jint k, jint it, jdou
   p.online_learning_rate = olr;
   p.online_init = oinit;
   mf_ctx* ctx = NULL;
-  jsize nd = devs ? (*env)->GetArrayLength(env, devs) : 0;
-  jint* d = devs ? (*env)->GetIntArrayElements(env, devs, NULL) : NULL;
-  int st = mf_create(&p, (const int*)d, nd ? nd : 1, &ctx);
-  if (d) (*env)->ReleaseIntArrayElements(env, devs, d, JNI_ABORT);
+  const jsize nd = len(env, devs);
+  Elems d = {0};
+  if (acquire(env, &d, devs, kInt)) return 0;
+  int st = mf_create(&p, (const int*)d.p, nd ? nd : 1, &ctx);
+  release(env, &d, JNI_ABORT);
   return check(env, st) == MF_OK ? (jlong)(intptr_t)ctx : 0;
 }
 
@@ -65,13 +115,14 @@ JNIEXPORT jbyteArray JNICALL JFN(commUniqueId)(JNIEnv* env, jclass c) {
   uint8_t uid[MF_UID_BYTES];
   if (check(env, mf_comm_unique_id(uid)) != MF_OK) return NULL;
   jbyteArray out = (*env)->NewByteArray(env, MF_UID_BYTES);
-  (*env)->SetByteArrayRegion(env, out, 0, MF_UID_BYTES, (const jbyte*)uid);
+  if (out) (*env)->SetByteArrayRegion(env, out, 0, MF_UID_BYTES, (const jbyte*)uid);
   return out;
 }
 
 JNIEXPORT jlong JNICALL JFN(createRank)(JNIEnv* env, jclass c, jint k, jint it, jdouble lambda, jdouble lr, jint lrm,
                                         jdouble lra, jint nb, jlong seed, jboolean hs, jint mode, jint dev,
                                         jint nranks, jint rank, jbyteArray uid) {
+  if (require(env, uid && len(env, uid) == MF_UID_BYTES, "uid must be the 128-byte array of commUniqueId")) return 0;
   mf_params p;
   fill_params(&p, k, it, lambda, lr, lrm, lra, nb, seed, hs, mode);
   uint8_t id[MF_UID_BYTES] = {0};
@@ -85,13 +136,26 @@ JNIEXPORT void JNICALL JFN(destroy)(JNIEnv* env, jclass c, jlong h) { check(env,
 
 typedef int (*ratings_fn)(mf_ctx*, const int32_t*, const int32_t*, const double*, int64_t);
 
+/* (u, i, r) columns of one DataSet[(Int, Int, Double)]: parallel arrays of one length. */
+static int rating_columns(JNIEnv* env, jintArray u, jintArray i, jdoubleArray r, jsize* n) {
+  if (require(env, u && i && r, "rating columns must not be null")) return -1;
+  *n = len(env, r);
+  return require(env, len(env, u) == *n && len(env, i) == *n, "user, item and rating columns differ in length");
+}
+
 static void with_ratings(JNIEnv* env, jlong h, jintArray u, jintArray i, jdoubleArray r, ratings_fn fn) {
-  jsize n = (*env)->GetArrayLength(env, r);
-  void *pu = PIN(u), *pi = PIN(i), *pr = PIN(r);
-  int st = fn(CTX(h), (const int32_t*)pu, (const int32_t*)pi, (const double*)pr, n);
-  UNPIN(r, pr, JNI_ABORT);
-  UNPIN(i, pi, JNI_ABORT);
-  UNPIN(u, pu, JNI_ABORT);
+  jsize n = 0;
+  if (rating_columns(env, u, i, r, &n)) return;
+  Elems eu = {0}, ei = {0}, er = {0};
+  if (acquire(env, &eu, u, kInt) || acquire(env, &ei, i, kInt) || acquire(env, &er, r, kDouble)) {
+    release(env, &eu, JNI_ABORT);
+    release(env, &ei, JNI_ABORT);
+    return;
+  }
+  int st = fn(CTX(h), (const int32_t*)eu.p, (const int32_t*)ei.p, (const double*)er.p, n);
+  release(env, &er, JNI_ABORT);
+  release(env, &ei, JNI_ABORT);
+  release(env, &eu, JNI_ABORT);
   check(env, st);
 }
 
@@ -118,123 +182,211 @@ JNIEXPORT jlong JNICALL JFN(numFactors)(JNIEnv* env, jclass c, jlong h, jint sid
 }
 
 JNIEXPORT jlong JNICALL JFN(getFactors)(JNIEnv* env, jclass c, jlong h, jint side, jintArray ids, jdoubleArray vecs) {
+  const jlong k = rank_of(env, h);
+  if (k < 0) return 0;
+  const jsize cap = len(env, ids);
+  if (require(env, ids && vecs && (jlong)len(env, vecs) >= (jlong)cap * k, "vecs must hold ids.length * k doubles"))
+    return 0;
   int64_t w = 0;
-  jsize cap = (*env)->GetArrayLength(env, ids);
-  void *pi = PIN(ids), *pv = PIN(vecs);
-  int st = mf_get_factors(CTX(h), side, (int32_t*)pi, (double*)pv, cap, &w);
-  UNPIN(vecs, pv, 0);
-  UNPIN(ids, pi, 0);
+  Elems ei = {0}, ev = {0};
+  if (acquire(env, &ei, ids, kInt) || acquire(env, &ev, vecs, kDouble)) {
+    release(env, &ei, JNI_ABORT);
+    return 0;
+  }
+  int st = mf_get_factors(CTX(h), side, (int32_t*)ei.p, (double*)ev.p, cap, &w);
+  release(env, &ev, st == MF_OK ? 0 : JNI_ABORT);
+  release(env, &ei, st == MF_OK ? 0 : JNI_ABORT);
   check(env, st);
   return w;
 }
 
 JNIEXPORT void JNICALL JFN(setFactors)(JNIEnv* env, jclass c, jlong h, jint side, jintArray ids, jdoubleArray vecs) {
-  jsize n = (*env)->GetArrayLength(env, ids);
-  void *pi = PIN(ids), *pv = PIN(vecs);
-  int st = mf_set_factors(CTX(h), side, (const int32_t*)pi, (const double*)pv, n);
-  UNPIN(vecs, pv, JNI_ABORT);
-  UNPIN(ids, pi, JNI_ABORT);
+  const jlong k = rank_of(env, h);
+  if (k < 0) return;
+  const jsize n = len(env, ids);
+  if (require(env, ids && vecs && (jlong)len(env, vecs) >= (jlong)n * k, "vecs must hold ids.length * k doubles"))
+    return;
+  Elems ei = {0}, ev = {0};
+  if (acquire(env, &ei, ids, kInt) || acquire(env, &ev, vecs, kDouble)) {
+    release(env, &ei, JNI_ABORT);
+    return;
+  }
+  int st = mf_set_factors(CTX(h), side, (const int32_t*)ei.p, (const double*)ev.p, n);
+  release(env, &ev, JNI_ABORT);
+  release(env, &ei, JNI_ABORT);
   check(env, st);
 }
 
 JNIEXPORT void JNICALL JFN(predict)(JNIEnv* env, jclass c, jlong h, jintArray u, jintArray i, jdoubleArray out,
                                     jbyteArray found) {
-  jsize n = (*env)->GetArrayLength(env, u);
-  void *pu = PIN(u), *pi = PIN(i), *po = PIN(out), *pf = PIN(found);
-  int st = mf_predict(CTX(h), (const int32_t*)pu, (const int32_t*)pi, n, (double*)po, (uint8_t*)pf);
-  UNPIN(found, pf, 0);
-  UNPIN(out, po, 0);
-  UNPIN(i, pi, JNI_ABORT);
-  UNPIN(u, pu, JNI_ABORT);
+  if (require(env, u && i && out && found, "arguments must not be null")) return;
+  const jsize n = len(env, u);
+  if (require(env, len(env, i) == n && len(env, out) >= n && len(env, found) >= n,
+              "items must match users in length; out and found must hold users.length entries"))
+    return;
+  Elems eu = {0}, ei = {0}, eo = {0}, ef = {0};
+  if (acquire(env, &eu, u, kInt) || acquire(env, &ei, i, kInt) || acquire(env, &eo, out, kDouble) ||
+      acquire(env, &ef, found, kByte)) {
+    release(env, &eo, JNI_ABORT);
+    release(env, &ei, JNI_ABORT);
+    release(env, &eu, JNI_ABORT);
+    return;
+  }
+  int st = mf_predict(CTX(h), (const int32_t*)eu.p, (const int32_t*)ei.p, n, (double*)eo.p, (uint8_t*)ef.p);
+  release(env, &ef, st == MF_OK ? 0 : JNI_ABORT);
+  release(env, &eo, st == MF_OK ? 0 : JNI_ABORT);
+  release(env, &ei, JNI_ABORT);
+  release(env, &eu, JNI_ABORT);
   check(env, st);
 }
 
-JNIEXPORT jdouble JNICALL JFN(rmse)(JNIEnv* env, jclass c, jlong h, jintArray u, jintArray i, jdoubleArray r) {
-  double rmse = 0;
+typedef int (*eval_fn)(JNIEnv*, jlong, const int32_t*, const int32_t*, const double*, jsize, jdouble, double*);
+
+static int call_rmse(JNIEnv* env, jlong h, const int32_t* u, const int32_t* i, const double* r, jsize n, jdouble unused,
+                     double* out) {
   int64_t matched = 0;
-  jsize n = (*env)->GetArrayLength(env, r);
-  void *pu = PIN(u), *pi = PIN(i), *pr = PIN(r);
-  int st = mf_rmse(CTX(h), (const int32_t*)pu, (const int32_t*)pi, (const double*)pr, n, &rmse, &matched);
-  UNPIN(r, pr, JNI_ABORT);
-  UNPIN(i, pi, JNI_ABORT);
-  UNPIN(u, pu, JNI_ABORT);
+  (void)env;
+  (void)unused;
+  return mf_rmse(CTX(h), u, i, r, n, out, &matched);
+}
+
+static int call_risk(JNIEnv* env, jlong h, const int32_t* u, const int32_t* i, const double* r, jsize n, jdouble lambda,
+                     double* out) {
+  (void)env;
+  return mf_empirical_risk(CTX(h), u, i, r, n, lambda, out);
+}
+
+static jdouble with_labeled(JNIEnv* env, jlong h, jintArray u, jintArray i, jdoubleArray r, jdouble lambda,
+                            eval_fn fn) {
+  jsize n = 0;
+  if (rating_columns(env, u, i, r, &n)) return 0;
+  Elems eu = {0}, ei = {0}, er = {0};
+  if (acquire(env, &eu, u, kInt) || acquire(env, &ei, i, kInt) || acquire(env, &er, r, kDouble)) {
+    release(env, &ei, JNI_ABORT);
+    release(env, &eu, JNI_ABORT);
+    return 0;
+  }
+  double v = 0;
+  int st = fn(env, h, (const int32_t*)eu.p, (const int32_t*)ei.p, (const double*)er.p, n, lambda, &v);
+  release(env, &er, JNI_ABORT);
+  release(env, &ei, JNI_ABORT);
+  release(env, &eu, JNI_ABORT);
   check(env, st);
-  return rmse;
+  return v;
+}
+
+JNIEXPORT jdouble JNICALL JFN(rmse)(JNIEnv* env, jclass c, jlong h, jintArray u, jintArray i, jdoubleArray r) {
+  return with_labeled(env, h, u, i, r, 0.0, call_rmse);
 }
 
 JNIEXPORT jdouble JNICALL JFN(empiricalRisk)(JNIEnv* env, jclass c, jlong h, jintArray u, jintArray i,
                                              jdoubleArray r, jdouble lambda) {
-  double risk = 0;
-  jsize n = (*env)->GetArrayLength(env, r);
-  void *pu = PIN(u), *pi = PIN(i), *pr = PIN(r);
-  int st = mf_empirical_risk(CTX(h), (const int32_t*)pu, (const int32_t*)pi, (const double*)pr, n, lambda, &risk);
-  UNPIN(r, pr, JNI_ABORT);
-  UNPIN(i, pi, JNI_ABORT);
-  UNPIN(u, pu, JNI_ABORT);
-  check(env, st);
-  return risk;
+  return with_labeled(env, h, u, i, r, lambda, call_risk);
 }
 
 JNIEXPORT void JNICALL JFN(blockUpdate)(JNIEnv* env, jclass c, jlong h, jdoubleArray r, jintArray uidx,
                                         jintArray iidx, jdoubleArray users, jintArray uom, jdoubleArray items,
                                         jintArray iom, jint k, jint iteration, jint rbid, jlong seed, jdouble lr,
                                         jint lrm, jdouble lra, jdouble lambda) {
-  jsize len = (*env)->GetArrayLength(env, r);
-  jsize nu = (*env)->GetArrayLength(env, uom), ni = (*env)->GetArrayLength(env, iom);
-  void *pr = PIN(r), *pu = PIN(uidx), *pi = PIN(iidx), *pU = PIN(users), *pUo = PIN(uom), *pI = PIN(items),
-       *pIo = PIN(iom);
-  int st = mf_block_update(CTX(h), (const double*)pr, (const int32_t*)pu, (const int32_t*)pi, len, (double*)pU,
-                           (const int32_t*)pUo, nu, (double*)pI, (const int32_t*)pIo, ni, k, iteration, rbid, seed, lr,
-                           lrm, lra, lambda);
-  UNPIN(iom, pIo, JNI_ABORT);
-  UNPIN(items, pI, 0);
-  UNPIN(uom, pUo, JNI_ABORT);
-  UNPIN(users, pU, 0);
-  UNPIN(iidx, pi, JNI_ABORT);
-  UNPIN(uidx, pu, JNI_ABORT);
-  UNPIN(r, pr, JNI_ABORT);
+  if (require(env, r && uidx && iidx && users && uom && items && iom, "arguments must not be null")) return;
+  const jsize n = len(env, r), nu = len(env, uom), ni = len(env, iom);
+  if (require(env, k >= 1 && len(env, uidx) == n && len(env, iidx) == n &&
+                       (jlong)len(env, users) >= (jlong)nu * k && (jlong)len(env, items) >= (jlong)ni * k,
+              "uidx / iidx must match r in length; users / items must hold omegas.length * k doubles"))
+    return;
+  Elems er = {0}, eu = {0}, ei = {0}, eU = {0}, eUo = {0}, eI = {0}, eIo = {0};
+  Elems* all[7] = {&er, &eu, &ei, &eU, &eUo, &eI, &eIo};
+  if (acquire(env, &er, r, kDouble) || acquire(env, &eu, uidx, kInt) || acquire(env, &ei, iidx, kInt) ||
+      acquire(env, &eU, users, kDouble) || acquire(env, &eUo, uom, kInt) || acquire(env, &eI, items, kDouble) ||
+      acquire(env, &eIo, iom, kInt)) {
+    for (int x = 0; x < 7; ++x) release(env, all[x], JNI_ABORT);
+    return;
+  }
+  int st = mf_block_update(CTX(h), (const double*)er.p, (const int32_t*)eu.p, (const int32_t*)ei.p, n, (double*)eU.p,
+                           (const int32_t*)eUo.p, nu, (double*)eI.p, (const int32_t*)eIo.p, ni, k, iteration, rbid,
+                           seed, lr, lrm, lra, lambda);
+  release(env, &eIo, JNI_ABORT);
+  release(env, &eI, st == MF_OK ? 0 : JNI_ABORT);
+  release(env, &eUo, JNI_ABORT);
+  release(env, &eU, st == MF_OK ? 0 : JNI_ABORT);
+  release(env, &ei, JNI_ABORT);
+  release(env, &eu, JNI_ABORT);
+  release(env, &er, JNI_ABORT);
   check(env, st);
 }
 
 JNIEXPORT void JNICALL JFN(onlineUpdate)(JNIEnv* env, jclass c, jlong h, jintArray u, jintArray i, jdoubleArray r,
                                          jint flavour, jint parts) {
-  jsize n = (*env)->GetArrayLength(env, r);
-  void *pu = PIN(u), *pi = PIN(i), *pr = PIN(r);
-  int st = mf_online_update(CTX(h), (const int32_t*)pu, (const int32_t*)pi, (const double*)pr, n, flavour, parts,
+  jsize n = 0;
+  if (rating_columns(env, u, i, r, &n)) return;
+  Elems eu = {0}, ei = {0}, er = {0};
+  if (acquire(env, &eu, u, kInt) || acquire(env, &ei, i, kInt) || acquire(env, &er, r, kDouble)) {
+    release(env, &ei, JNI_ABORT);
+    release(env, &eu, JNI_ABORT);
+    return;
+  }
+  int st = mf_online_update(CTX(h), (const int32_t*)eu.p, (const int32_t*)ei.p, (const double*)er.p, n, flavour, parts,
                             NULL, NULL);
-  UNPIN(r, pr, JNI_ABORT);
-  UNPIN(i, pi, JNI_ABORT);
-  UNPIN(u, pu, JNI_ABORT);
+  release(env, &er, JNI_ABORT);
+  release(env, &ei, JNI_ABORT);
+  release(env, &eu, JNI_ABORT);
   check(env, st);
 }
 
 JNIEXPORT void JNICALL JFN(onlineUpdateOut)(JNIEnv* env, jclass c, jlong h, jintArray u, jintArray i, jdoubleArray r,
                                             jint flavour, jdoubleArray uout, jdoubleArray iout) {
-  jsize n = (*env)->GetArrayLength(env, r);
-  void *pu = PIN(u), *pi = PIN(i), *pr = PIN(r), *puo = PIN(uout), *pio = PIN(iout);
-  int st = mf_online_update_out(CTX(h), (const int32_t*)pu, (const int32_t*)pi, (const double*)pr, n, flavour, 0,
-                                NULL, NULL, (double*)puo, (double*)pio);
-  UNPIN(iout, pio, 0);
-  UNPIN(uout, puo, 0);
-  UNPIN(r, pr, JNI_ABORT);
-  UNPIN(i, pi, JNI_ABORT);
-  UNPIN(u, pu, JNI_ABORT);
+  jsize n = 0;
+  if (rating_columns(env, u, i, r, &n)) return;
+  const jlong k = rank_of(env, h);
+  if (k < 0) return;
+  if (require(env, (!uout || (jlong)len(env, uout) >= (jlong)n * k) && (!iout || (jlong)len(env, iout) >= (jlong)n * k),
+              "per-rating output buffers must hold ratings.length * k doubles"))
+    return;
+  Elems eu = {0}, ei = {0}, er = {0}, euo = {0}, eio = {0};
+  if (acquire(env, &eu, u, kInt) || acquire(env, &ei, i, kInt) || acquire(env, &er, r, kDouble) ||
+      acquire(env, &euo, uout, kDouble) || acquire(env, &eio, iout, kDouble)) {
+    release(env, &euo, JNI_ABORT);
+    release(env, &er, JNI_ABORT);
+    release(env, &ei, JNI_ABORT);
+    release(env, &eu, JNI_ABORT);
+    return;
+  }
+  int st = mf_online_update_out(CTX(h), (const int32_t*)eu.p, (const int32_t*)ei.p, (const double*)er.p, n, flavour, 0,
+                                NULL, NULL, (double*)euo.p, (double*)eio.p);
+  release(env, &eio, st == MF_OK ? 0 : JNI_ABORT);
+  release(env, &euo, st == MF_OK ? 0 : JNI_ABORT);
+  release(env, &er, JNI_ABORT);
+  release(env, &ei, JNI_ABORT);
+  release(env, &eu, JNI_ABORT);
   check(env, st);
 }
 
 JNIEXPORT void JNICALL JFN(lookup)(JNIEnv* env, jclass c, jlong h, jint side, jintArray ids, jdoubleArray out,
                                    jbyteArray found) {
-  jsize n = (*env)->GetArrayLength(env, ids);
-  void *pi = PIN(ids), *po = PIN(out), *pf = PIN(found);
-  int st = mf_lookup(CTX(h), side, (const int32_t*)pi, n, (double*)po, (uint8_t*)pf);
-  UNPIN(found, pf, 0);
-  UNPIN(out, po, 0);
-  UNPIN(ids, pi, JNI_ABORT);
+  const jlong k = rank_of(env, h);
+  if (k < 0) return;
+  if (require(env, ids && out && found, "arguments must not be null")) return;
+  const jsize n = len(env, ids);
+  if (require(env, (jlong)len(env, out) >= (jlong)n * k && len(env, found) >= n,
+              "out must hold ids.length * k doubles and found ids.length entries"))
+    return;
+  Elems ei = {0}, eo = {0}, ef = {0};
+  if (acquire(env, &ei, ids, kInt) || acquire(env, &eo, out, kDouble) || acquire(env, &ef, found, kByte)) {
+    release(env, &eo, JNI_ABORT);
+    release(env, &ei, JNI_ABORT);
+    return;
+  }
+  int st = mf_lookup(CTX(h), side, (const int32_t*)ei.p, n, (double*)eo.p, (uint8_t*)ef.p);
+  release(env, &ef, st == MF_OK ? 0 : JNI_ABORT);
+  release(env, &eo, st == MF_OK ? 0 : JNI_ABORT);
+  release(env, &ei, JNI_ABORT);
   check(env, st);
 }
 
 JNIEXPORT jlong JNICALL JFN(countRatings)(JNIEnv* env, jclass c, jstring path, jchar d, jint skip) {
+  if (require(env, path != NULL, "path must not be null")) return 0;
   const char* p = (*env)->GetStringUTFChars(env, path, NULL);
+  if (!p) return 0;
   int64_t n = 0;
   int st = mf_read_ratings(p, (char)d, skip, NULL, NULL, NULL, 0, &n);
   (*env)->ReleaseStringUTFChars(env, path, p);
@@ -244,27 +396,38 @@ JNIEXPORT jlong JNICALL JFN(countRatings)(JNIEnv* env, jclass c, jstring path, j
 
 JNIEXPORT void JNICALL JFN(readRatings)(JNIEnv* env, jclass c, jstring path, jchar d, jint skip, jintArray u,
                                         jintArray i, jdoubleArray r) {
+  if (require(env, path != NULL, "path must not be null")) return;
+  jsize cap = 0;
+  if (rating_columns(env, u, i, r, &cap)) return;
+  Elems eu = {0}, ei = {0}, er = {0};
+  if (acquire(env, &eu, u, kInt) || acquire(env, &ei, i, kInt) || acquire(env, &er, r, kDouble)) {
+    release(env, &ei, JNI_ABORT);
+    release(env, &eu, JNI_ABORT);
+    return;
+  }
   const char* p = (*env)->GetStringUTFChars(env, path, NULL);
-  jsize cap = (*env)->GetArrayLength(env, r);
   int64_t n = 0;
-  void *pu = PIN(u), *pi = PIN(i), *pr = PIN(r);
-  int st = mf_read_ratings(p, (char)d, skip, (int32_t*)pu, (int32_t*)pi, (double*)pr, cap, &n);
-  UNPIN(r, pr, 0);
-  UNPIN(i, pi, 0);
-  UNPIN(u, pu, 0);
-  (*env)->ReleaseStringUTFChars(env, path, p);
-  check(env, st);
+  int st = p ? mf_read_ratings(p, (char)d, skip, (int32_t*)eu.p, (int32_t*)ei.p, (double*)er.p, cap, &n) : MF_ERR_INVALID;
+  if (p) (*env)->ReleaseStringUTFChars(env, path, p);
+  release(env, &er, st == MF_OK ? 0 : JNI_ABORT);
+  release(env, &ei, st == MF_OK ? 0 : JNI_ABORT);
+  release(env, &eu, st == MF_OK ? 0 : JNI_ABORT);
+  if (p) check(env, st);
 }
 
 JNIEXPORT void JNICALL JFN(saveModel)(JNIEnv* env, jclass c, jlong h, jstring path) {
+  if (require(env, path != NULL, "path must not be null")) return;
   const char* p = (*env)->GetStringUTFChars(env, path, NULL);
+  if (!p) return;
   int st = mf_save_model(CTX(h), p);
   (*env)->ReleaseStringUTFChars(env, path, p);
   check(env, st);
 }
 
 JNIEXPORT jlong JNICALL JFN(loadModel)(JNIEnv* env, jclass c, jlong h, jstring path) {
+  if (require(env, path != NULL, "path must not be null")) return 0;
   const char* p = (*env)->GetStringUTFChars(env, path, NULL);
+  if (!p) return 0;
   int64_t step = 0;
   int st = mf_load_model(CTX(h), p, &step);
   (*env)->ReleaseStringUTFChars(env, path, p);

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "mfhip.h"
+#include "mfhip_testing.h"
 
 namespace mfhip {
 

@@ -90,19 +90,6 @@ void launch_sweep_pair_sys(hipStream_t st, const SysWave* sw, const WaveDesc* sy
                            const PairRec* recs, float* U, float* I, uint64_t u_bytes, uint64_t i_bytes, int k, float eta,
                            int32_t* prog, uint32_t base, int32_t* err, uint64_t* trace, hipEvent_t ev0, hipEvent_t ev1);
 
-// Stream sweep (plan.hpp StreamWave), one launch per superstep: sw = this launch's waves (nw <=
-// sweep_stream_capacity(k), all resident at once), lbase = index of sw[0] among the superstep's
-// waves.  prog: one word per wave slot (kProgStride apart, prog_bytes in all), monotonic across
-// launches: this launch writes base .. base + npairs, so base must advance by more than the
-// longest stream per launch.  err[0] is set when a wave gave up waiting (~1 s).
-// ring: the plan's prefetch depth (PairPlan::ring; stream_ring_supported).  prog: kStreamProgStride
-// words per wave slot; err: 4 + 4 * waves words (flag + per-slot timeout diagnostics).
-int sweep_stream_capacity(int k);
-bool stream_ring_supported(int ring, int period);  // period: pairs between hand-off word updates
-void launch_sweep_stream(int ring, int period, hipStream_t st, const StreamWave* sw, int nw, int lbase, const PairRec* recs,
-                         float* U, float* I, uint64_t u_bytes, uint64_t i_bytes, int k, float eta, int32_t* prog,
-                         uint64_t prog_bytes, uint32_t base, int32_t* err, hipEvent_t ev0, hipEvent_t ev1);
-
 // Deterministic persistent sweep (kernels_detsweep.hip): one launch per superstep, nw waves of
 // 64 lanes, all of which must be resident at once (nw <= det_sweep_capacity(k)).  Entries are
 // build_det_step's SoA arrays; ticket: one int32 per user row, zero before the launch; err[0]

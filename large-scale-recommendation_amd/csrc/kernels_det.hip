@@ -140,6 +140,8 @@ __global__ __launch_bounds__(64) void k_online_sweep(const int64_t* __restrict__
     if (q == 0) return true;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(ticket + ur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != q) {
+      if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
+        return false;  // another wave gave up
       if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {  // 100 MHz clock: ~1 s
         if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return false;

@@ -243,6 +243,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
         const uint32_t v = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
             __hip_atomic_load(nb_prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
         if (static_cast<int32_t>(v - want) >= 0) break;
+        // another wave gave up: its downstream waves would each spin their own second, so leave now
+        if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
+          return;
         if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {  // 100 MHz clock: ~1 s
           if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           return;

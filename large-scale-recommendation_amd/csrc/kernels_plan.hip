@@ -955,8 +955,6 @@ void device_fast_schedule(hipStream_t st, const DevRatingBlocks& dr, const Ratin
   for (DevBuf* d : {&dk1s, &dv1, &dO1, &dhead, &drun, &dk2, &dk2s, &dv2, &dP2, &dseg, &dsegs, &dpos, &dposs, &dv3, &dQ1,
                     &dk3, &dk3s, &dF, &dblk, &dul, &dil, &dcc})
     d->release();
-  fp.K = 1;
-  fp.gmajor = false;
   fp.Gb.assign(Gblk.begin(), Gblk.end());
   fp.G = *std::max_element(fp.Gb.begin(), fp.Gb.end());
   fp.split_off.assign(nb2 + 1, 0);

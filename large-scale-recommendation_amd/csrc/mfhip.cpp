@@ -88,12 +88,11 @@ struct Shard {
   // fast mode
   DevBuf fast_recs, fast_cells, fast_blks;
   DevBuf fast_prog, fast_err;  // persistent sweep: progress words + timeout flag
-  DevBuf st_recs, st_waves;    // stream schedule (kernels_stream.hip)
+  DevBuf st_recs, st_waves;    // pair schedule: records and per-cell wave table
   int64_t st_nrecs = 0;        // pair records in st_recs
   std::vector<int64_t> st_sub_off;
   std::vector<WaveDesc> st_waves_host;  // kept only when tracing
   DevBuf st_sys, st_sysw;               // systolic pair tables (PairPlan::sys, sys_waves)
-  DevBuf st_stream;                     // stream sweep waves (PairPlan::stream)
   std::vector<int64_t> st_sys_off;      // PairPlan::sys_off
   std::vector<WaveDesc> st_sys_host;    // kept only when tracing
   std::vector<SysWave> st_sysw_host;    // kept only when tracing
@@ -142,11 +141,12 @@ struct mf_ctx {
   bool fast_persistent = false;  // MFHIP_FAST_KERNEL=persistent selects the systolic single launch
   bool fast_pair = false;         // two updates per step (kernels_pair.hip), k in {64, 128, 256}
   bool fast_sys = false;          // pair cells as one systolic launch per superstep (k_sweep_pair_sys)
-  bool fast_stream = false;       // k_sweep_stream: one launch per superstep, cells as one pair stream per wave
-  int32_t stream_ring = 3;        // its prefetch depth (plan window 2 * ring)
-  int32_t stream_period = 4;      // pairs between two updates of the hand-off words (MFHIP_STREAM_PUB)
   bool det_sweep = false;         // deterministic mode: one persistent k_det_sweep launch per superstep
   bool ring_overlap = false;      // fast systolic sweep, >1 shard, c >= 2: the ring step overlaps the sweep
+  // fast-mode hot-item replicas (plan.hpp SplitItem), an experiment outside the product surface:
+  // MFHIP_ITEM_SPLIT=m sweeps an item with more than m ratings in one rating block as ceil(r / m)
+  // chains averaged when the superstep ends (read at prepare; 0 / unset = off)
+  int32_t item_split = 0;
   std::vector<int64_t> fast_rb_size;  // per rating block (fast mode)
   mf_stats stats{};
   bool profiling = false;
@@ -171,13 +171,6 @@ enum class FastKernel { kPair, kCell, kPersistent };
 bool want_pair_sys() {
   const char* v = std::getenv("MFHIP_PAIR_SYS");
   return v ? std::string(v) != "0" : true;
-}
-
-// Stream sweep (k_sweep_stream): MFHIP_STREAM=0 keeps k_sweep_pair_sys.  MFHIP_STREAM_G / _K pin
-// the item groups per rating block and the user groups per item group.
-bool want_stream() {
-  const char* v = std::getenv("MFHIP_STREAM");
-  return v ? std::string(v) != "0" : false;
 }
 
 FastKernel choose_fast_kernel(int k) {
@@ -207,7 +200,6 @@ void validate_params(const mf_params* p) {
   MF_REQUIRE(p->lr_method >= MF_LR_DEFAULT && p->lr_method <= MF_LR_XU, "unknown lr_method");
   MF_REQUIRE(p->fast_blocking == MF_BLOCKING_BALANCED || p->fast_blocking == MF_BLOCKING_REFERENCE,
              "unknown fast_blocking");
-  MF_REQUIRE(p->fast_item_split >= 0, "fast_item_split must be >= 0");
 }
 
 void init_shard(Shard& s, int device, int index) {
@@ -423,37 +415,12 @@ void dump_wave_trace(mf_ctx* ctx) {
   if (f) std::fclose(f);
 }
 
-// MFHIP_STREAM_STATS: the stream sweep's per-slot wait statistics since the last report (err words
-// 4 + 8 * slot + 4 .. 7: slow-path waits, ticks waited, wave ticks, pairs), summed on stderr.
-void stream_stats_report(mf_ctx* ctx, Shard& s) {
-  if (!ctx->fast_stream || !std::getenv("MFHIP_STREAM_STATS") || s.fast_err.bytes() <= 16) return;
-  std::vector<uint32_t> dg(s.fast_err.bytes() / 4);
-  MF_HIP(hipMemcpy(dg.data(), s.fast_err.get(), s.fast_err.bytes(), hipMemcpyDeviceToHost));
-  double waits = 0, wticks = 0, dt = 0, pairs = 0, dtmax = 0;
-  int64_t slots = 0;
-  for (size_t w = 0; 4 + 8 * w + 7 < dg.size(); ++w) {
-    const uint32_t* d = dg.data() + 4 + 8 * w + 4;
-    if (!d[2]) continue;
-    ++slots;
-    waits += d[0]; wticks += d[1]; dt += d[2]; pairs += d[3];
-    dtmax = std::max<double>(dtmax, d[2]);
-  }
-  if (slots)
-    std::fprintf(stderr, "[mfhip] stream waits: %lld slots, %.1f slow waits per slot, %.1f%% of wave time waiting, "
-                 "%.1f ns per pair (wave time / pairs), longest slot total %.3f ms\n", (long long)slots, waits / slots,
-                 100.0 * wticks / std::max(dt, 1.0), 10.0 * dt / std::max(pairs, 1.0), dtmax * 1e-5);
-  for (size_t w = 0; 4 + 8 * w + 7 < dg.size(); ++w)
-    for (int x = 4; x < 8; ++x) dg[4 + 8 * w + x] = 0;
-  MF_HIP(hipMemcpy(s.fast_err.get(), dg.data(), s.fast_err.bytes(), hipMemcpyHostToDevice));
-}
-
 void sync_all(mf_ctx* ctx) {
   for (auto& s : ctx->shards) {
     DeviceGuard g(s.device);
     MF_HIP(hipStreamSynchronize(s.stream));
     MF_HIP(hipStreamSynchronize(s.aux));
     MF_HIP(hipStreamSynchronize(s.comm));
-    stream_stats_report(ctx, s);
     for (DevBuf* eb : {&s.fast_err, &s.det_err}) {
       if (!eb->get()) continue;
       int32_t err4[4] = {0, 0, 0, 0};
@@ -464,11 +431,10 @@ void sync_all(mf_ctx* ctx) {
         if (std::getenv("MFHIP_DEBUG_PLAN") && eb->bytes() > 16) {
           std::vector<uint32_t> dg(eb->bytes() / 4);
           MF_HIP(hipMemcpy(dg.data(), eb->get(), eb->bytes(), hipMemcpyDeviceToHost));
-          const size_t st = eb == &s.fast_err && ctx->fast_stream ? 8 : 4;
-          for (size_t w = 0; 4 + st * w + 3 < dg.size(); ++w)
-            if (dg[4 + st * w + 3])
+          for (size_t w = 0; 4 + 4 * w + 3 < dg.size(); ++w)
+            if (dg[4 + 4 * w + 3])
               std::fprintf(stderr, "[mfhip] sweep timeout: wave slot %zu seen %u want %u published %u\n", w,
-                           dg[4 + st * w], dg[4 + st * w + 1], dg[4 + st * w + 2]);
+                           dg[4 + 4 * w], dg[4 + 4 * w + 1], dg[4 + 4 * w + 2]);
           MF_HIP(hipMemset(eb->get(), 0, eb->bytes()));
         }
         // waves that gave up skipped the rest of their work: the model is partly updated, so
@@ -661,14 +627,6 @@ void fast_superstep(mf_ctx* ctx, Shard& s, int64_t superstep, double eta) {
     auto sweep = [&](hipStream_t st, int64_t a, int64_t z) {  // waves [a, z) of the superstep
       if (z <= a) return;
       LaunchTimer tm(s, ctx->profiling, true);
-      if (ctx->fast_stream) {
-        launch_sweep_stream(ctx->stream_ring, ctx->stream_period, st, s.st_stream.as<StreamWave>() + w0 + a, static_cast<int>(z - a), static_cast<int>(a),
-                            s.st_recs.as<PairRec>(), s.uf.as<float>(), s.itf.as<float>(), s.uf.bytes(), s.itf.bytes(),
-                            ctx->P.num_factors, static_cast<float>(eta), s.fast_prog.as<int32_t>(), s.fast_prog.bytes(),
-                            s.sys_base, s.fast_err.as<int32_t>(), tm.start(), tm.stop());
-        ctx->stats.kernel_launches += 1;
-        return;
-      }
       launch_sweep_pair_sys(st, s.st_sysw.as<SysWave>() + w0 + a, s.st_sys.as<WaveDesc>(), static_cast<int>(z - a),
                             static_cast<int>(a), s.st_recs.as<PairRec>(), s.uf.as<float>(), s.itf.as<float>(),
                             s.uf.bytes(), s.itf.bytes(), ctx->P.num_factors, static_cast<float>(eta),
@@ -1103,6 +1061,8 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
   ctx->failed.clear();
   sync_all(ctx);
   PhaseClock clk;
+  ctx->item_split = 0;
+  if (const char* v = std::getenv("MFHIP_ITEM_SPLIT")) ctx->item_split = std::max(0, std::atoi(v));
   ctx->reaper.join();
   DevRatingBlocks dev_rb;  // the device copy of the rating blocks (full device schedule only)
   ctx->nb = std::max(1, ctx->P.num_blocks);
@@ -1118,8 +1078,8 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
     Shard& s0 = ctx->shards[0];
     DeviceGuard g(s0.device);
     const char* dpv0 = std::getenv("MFHIP_DEVICE_PLAN");
-    const bool keep = !ctx->f64 && ctx->shards.size() == 1 && ctx->P.fast_item_split == 0 &&
-                      choose_fast_kernel(ctx->P.num_factors) == FastKernel::kPair && !want_stream() &&
+    const bool keep = !ctx->f64 && ctx->shards.size() == 1 && ctx->item_split == 0 &&
+                      choose_fast_kernel(ctx->P.num_factors) == FastKernel::kPair &&
                       !(dpv0 && (std::string(dpv0) == "0" || std::string(dpv0) == "1"));
     device_blocking(s0.stream, u, i, r, n, ctx->nb, ctx->P.seed, lo, hi, ctx->f64, ctx->U, ctx->I, ctx->rb,
                     keep ? &dev_rb : nullptr, !keep);
@@ -1151,45 +1111,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
     ctx->fast_pair = fk == FastKernel::kPair;
     ctx->fast_sys = false;
     std::vector<int32_t> block_groups;  // systolic sweep, automatic G: one G_j per rating block
-    ctx->fast_stream = false;
-    int32_t stream_K = 1;
-    if (ctx->fast_pair && want_pair_sys() && want_stream()) {
-      // every rating block of a superstep gets G item groups (one wave each), all resident at once
-      int cap = 1 << 30, simds = 1 << 30;
-      for (auto& s : ctx->shards) {
-        DeviceGuard g(s.device);
-        int cus = 0;
-        MF_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s.device));
-        cap = std::min(cap, sweep_stream_capacity(k));
-        simds = std::min(simds, 4 * cus);
-      }
-      if (const char* v = std::getenv("MFHIP_DEVICE_SHARERS"))
-        if (ctx->rank_mode && std::atoi(v) > 1) cap /= std::atoi(v);
-      int per_dev = 0;  // shards (local blocks) sharing one device
-      for (auto& s : ctx->shards) per_dev = std::max<int>(per_dev, static_cast<int>(std::count_if(
-          ctx->shards.begin(), ctx->shards.end(), [&](const Shard& o) { return o.device == s.device; })));
-      const int blocks_per_dev = std::max(1, per_dev) * ctx->c;
-      int32_t Gs = std::max(1, simds / blocks_per_dev);
-      if (const char* v = std::getenv("MFHIP_STREAM_G")) Gs = std::max(1, std::atoi(v));
-      if (ctx->P.fast_waves < 0) Gs = -ctx->P.fast_waves;
-      stream_K = 2;
-      if (const char* v = std::getenv("MFHIP_STREAM_K")) stream_K = std::max(2, std::atoi(v));
-      ctx->stream_ring = kStreamRing;
-      if (const char* v = std::getenv("MFHIP_STREAM_RING")) ctx->stream_ring = std::atoi(v);
-      ctx->stream_period = 4;
-      if (const char* v = std::getenv("MFHIP_STREAM_PUB")) ctx->stream_period = std::atoi(v);
-      MF_REQUIRE(stream_ring_supported(ctx->stream_ring, ctx->stream_period),
-                 "unsupported MFHIP_STREAM_RING / MFHIP_STREAM_PUB combination");
-      if (static_cast<int64_t>(Gs) * blocks_per_dev <= cap) {
-        ctx->fast_stream = true;
-        ctx->fast_sys = true;
-        ctx->G_fast = Gs;
-      }
-      if (std::getenv("MFHIP_DEBUG_PLAN"))
-        std::fprintf(stderr, "[mfhip] stream sweep %s: G %d K %d, %d blocks per device, capacity %d waves\n",
-                     ctx->fast_stream ? "on" : "off (capacity)", Gs, stream_K, blocks_per_dev, cap);
-    }
-    if (ctx->fast_pair && want_pair_sys() && !ctx->fast_stream) {
+    if (ctx->fast_pair && want_pair_sys()) {
       int cap = 1 << 30, simds = 1 << 30;
       for (auto& s : ctx->shards) {
         DeviceGuard g(s.device);
@@ -1211,7 +1133,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
             gb = choose_block_groups(size, device_block_tops(s.stream, dev_rb, ctx->rb, ctx->I), ctx->nb, ctx->c,
                                      s.index, simds);
           } else {
-            gb = choose_block_groups(ctx->rb, ctx->I, ctx->c, s.index, simds, ctx->P.fast_item_split);
+            gb = choose_block_groups(ctx->rb, ctx->I, ctx->c, s.index, simds, ctx->item_split);
           }
           for (int64_t b = 0; b < nb2; ++b)
             if (gb[b] > 0) block_groups[b] = gb[b];
@@ -1245,7 +1167,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
     // the per-cell emission and the pair records on the device (kernels_plan.hip) for the default
     // systolic pair sweep of one shard; MFHIP_DEVICE_PLAN=0 keeps them on the host
     const char* dpv = std::getenv("MFHIP_DEVICE_PLAN");
-    const bool dev_plan = ctx->fast_pair && ctx->fast_sys && !ctx->fast_stream && ctx->P.fast_item_split == 0 &&
+    const bool dev_plan = ctx->fast_pair && ctx->fast_sys && ctx->item_split == 0 &&
                           ctx->shards.size() == 1 && !(dpv && std::string(dpv) == "0");
     std::vector<FastBlockWork> entries;
     PairPlan dev_pp;
@@ -1271,10 +1193,8 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
       }
       build_fast_plan(fp, ctx->rb, ctx->U, ctx->I, ctx->G_fast, k, ctx->P.lambda,
                       static_cast<uint64_t>(ctx->P.seed) * 0x9E3779B97F4A7C15ULL + 1, dummy, nullptr,
-                      ctx->fast_stream ? 2 * ctx->stream_ring : ctx->fast_pair ? 2 * kPairRing : kHazardWindow,
-                      block_groups.empty() ? nullptr : &block_groups, ctx->P.fast_item_split,
-                      static_cast<uint32_t>(ctx->I.rows() + 1), ctx->fast_stream ? stream_K : 1, ctx->fast_stream,
-                      dev_plan ? &entries : nullptr);
+                      ctx->fast_pair ? 2 * kPairRing : kHazardWindow, block_groups.empty() ? nullptr : &block_groups,
+                      ctx->item_split, static_cast<uint32_t>(ctx->I.rows() + 1), dev_plan ? &entries : nullptr);
     }
     MF_REQUIRE(static_cast<uint64_t>(ctx->I.rows() + 1 + fp.scratch_rows) * k * 4 < (1ull << 32),
                "hot-item replica rows exceed the 32-bit item slab offsets");
@@ -1294,7 +1214,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
       for (int64_t b = 0; b < nb2; ++b)
         if (fp.cell_base[b] >= 0) {
           const int32_t* o = fp.cell_off.data() + fp.cell_base[b];
-          const int64_t gg = static_cast<int64_t>(fp.K) * fp.Gb[b] * fp.Gb[b];
+          const int64_t gg = static_cast<int64_t>(fp.Gb[b]) * fp.Gb[b];
           for (int64_t c2 = 0; c2 < gg; ++c2) cells += o[c2 + 1] > o[c2];
           recs += o[gg];
         }
@@ -1315,7 +1235,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
     {
       const char* ov = std::getenv("MFHIP_RING_OVERLAP");
       ctx->ring_overlap = ctx->fast_pair && ctx->fast_sys && ctx->G > 1 && ctx->c >= 2 &&
-                          ctx->P.fast_item_split == 0 && !(ov && std::string(ov) == "0");
+                          ctx->item_split == 0 && !(ov && std::string(ov) == "0");
     }
     for (auto& s : ctx->shards) {
       ensure_rows(ctx, s, kSideU, ctx->U.rows() + 2);
@@ -1339,37 +1259,6 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
       const size_t row_bytes = static_cast<size_t>(ctx->P.num_factors) * ctx->es;
       MF_HIP(hipMemset(s.uf.as<char>() + static_cast<size_t>(dummy) * row_bytes, 0, 2 * row_bytes));
       MF_HIP(hipMemset(s.itf.as<char>() + static_cast<size_t>(ctx->fast_dummy_i) * row_bytes, 0, row_bytes));
-      if (ctx->fast_stream) {
-        PairPlan pp;
-        build_stream_plan(pp, fp, ctx->nb, ctx->c, s.index, k, ctx->stream_ring);
-        if (std::getenv("MFHIP_DEBUG_PLAN")) {
-          std::string rep;
-          const int64_t bad = stream_protocol_deadlocks(pp, ctx->nb, &rep);
-          std::fprintf(stderr, "[mfhip] stream protocol replay: %lld stuck supersteps\n%s", (long long)bad, rep.c_str());
-        }
-        ctx->stats.pads += pp.noop_halves - fp.pads;
-        s.sm_bytes = pp.sm_bytes;
-        s.st_recs.alloc(std::max<size_t>(pp.recs.size(), 1) * sizeof(PairRec));
-        if (!pp.recs.empty())
-          MF_HIP(hipMemcpy(s.st_recs.get(), pp.recs.data(), pp.recs.size() * sizeof(PairRec), hipMemcpyHostToDevice));
-        s.st_stream.alloc(std::max<size_t>(pp.stream.size(), 1) * sizeof(StreamWave));
-        if (!pp.stream.empty())
-          MF_HIP(hipMemcpy(s.st_stream.get(), pp.stream.data(), pp.stream.size() * sizeof(StreamWave),
-                           hipMemcpyHostToDevice));
-        s.st_sys_off = pp.sys_off;
-        s.st_sys_block_off = pp.sys_block_off;
-        s.sys_base = 0;
-        s.sys_step = static_cast<uint32_t>(pp.max_pairs) + 2u;
-        int64_t max_waves = 1;
-        for (int32_t sm = 0; sm < ctx->nb; ++sm) max_waves = std::max(max_waves, pp.sys_off[sm + 1] - pp.sys_off[sm]);
-        s.fast_prog.alloc(static_cast<size_t>(max_waves) * kStreamProgStride * sizeof(int32_t));
-        MF_HIP(hipMemset(s.fast_prog.get(), 0, s.fast_prog.bytes()));
-        s.fast_err.alloc(16 + 32 * static_cast<size_t>(max_waves));  // flag + per-slot diagnostics and wait stats
-        MF_HIP(hipMemset(s.fast_err.get(), 0, s.fast_err.bytes()));
-        clk.lap("stream plan + H2D");
-        ctx->reaper.drop(pp.recs);
-        continue;
-      }
       if (ctx->fast_pair) {
         PairPlan pp;
         if (dev_plan) {
@@ -1505,6 +1394,12 @@ void consolidate(mf_ctx* ctx, Shard& dst) {
 // Rank mode: broadcast each item block from its holder so every rank has all items.
 void allgather_items(mf_ctx* ctx) {
   if (!ctx->rank_mode || ctx->G <= 1) return;
+  // The last superstep may still be running: with the ring overlap its second launch is on
+  // `aux` and the item block's send/recv on `comm`.  The broadcast below reads and writes item
+  // rows on `stream`, and two RCCL operations of one communicator must not run on unordered
+  // streams, so every stream of the rank drains first (and a sweep timeout surfaces here).
+  sync_all(ctx);
+  require_healthy(ctx);
   Shard& s = ctx->shards[0];
   DeviceGuard g(s.device);
   const size_t k = static_cast<size_t>(ctx->P.num_factors);
@@ -1816,7 +1711,14 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
     MF_HIP(hipMemcpyAsync(touched, sc.touched.get(), 8, hipMemcpyDeviceToHost, s.stream));
     MF_HIP(hipStreamSynchronize(s.stream));
     clk.lap("online: sweep (device)");
-    if (err) fail(MF_ERR_TIMEOUT, "online sweep: a ticket wait timed out");
+    if (err) {
+      // waves that gave up skipped the rest of their updates and the batch's new ids are already
+      // in the index: the model is partly updated, so the context refuses further work (as the
+      // DSGD sweeps do, sync_all) until a fit is prepared again
+      ctx->failed = "online sweep: a wave waited > 1 s for a user ticket (waves not co-resident?); "
+                    "set MFHIP_ONLINE_KERNEL=level";
+      fail(MF_ERR_TIMEOUT, ctx->failed);
+    }
     if (tu) *tu = touched[0];
     if (ti) *ti = touched[1];
     ctx->stats.kernel_launches += 1;
@@ -1910,7 +1812,6 @@ void mf_params_init(mf_params* p) {
   p->online_learning_rate = 0.01;  // SparkExample.scala:33 SGDUpdater(0.01)
   p->online_init = MF_INIT_PSEUDO_RANDOM;
   p->fast_waves = 0;
-  p->fast_item_split = 0;
 }
 
 const char* mf_last_error(void) { return g_last_error.c_str(); }
@@ -2356,8 +2257,7 @@ int mf_debug_fast_schedule(const int32_t* u, const int32_t* i, int64_t n, int32_
 namespace mfhip {
 namespace {
 int debug_fast_plan(const int32_t* u, const int32_t* i, int64_t n, int32_t n_blocks, int64_t seed, int32_t groups,
-                    int32_t blocking, int32_t window, int32_t item_split, int32_t ustride, bool gmajor,
-                    int32_t* block_out, int32_t* substep_out, int32_t* group_out, int64_t* pos_out,
+                    int32_t blocking, int32_t window, int32_t item_split, int32_t* block_out, int32_t* substep_out, int32_t* group_out, int64_t* pos_out,
                     int32_t* replica_out) {
   return guarded([&] {
     MF_REQUIRE(n >= 0 && n_blocks >= 1 && groups != 0 && item_split >= 0, "bad argument");
@@ -2377,21 +2277,20 @@ int debug_fast_plan(const int32_t* u, const int32_t* i, int64_t n, int32_t n_blo
     build_fast_plan(fp, rb, U, I, groups > 0 ? groups : 8, 1, 1.0,
                     static_cast<uint64_t>(seed) * 0x9E3779B97F4A7C15ULL + 1, static_cast<uint32_t>(U.rows()), &src,
                     window > 0 ? window : kHazardWindow, block_groups.empty() ? nullptr : &block_groups, item_split,
-                    scratch_base, ustride, gmajor);
+                    scratch_base);
     const int64_t nb2 = static_cast<int64_t>(n_blocks) * n_blocks;
     for (int64_t b = 0; b < nb2; ++b) {
       if (fp.rec_base[b] < 0) continue;
       const int32_t G = fp.Gb[b];
-      const int64_t T = static_cast<int64_t>(fp.K) * G;
-      const int64_t GG = T * G;
+      const int64_t GG = static_cast<int64_t>(G) * G;
       const int32_t* off = fp.cell_off.data() + fp.cell_base[b];
       for (int64_t cidx = 0; cidx < GG; ++cidx)
         for (int64_t x = off[cidx]; x < off[cidx + 1]; ++x) {
           if (src[fp.rec_base[b] + x] < 0) continue;  // padding
           const int64_t j = rb.src[src[fp.rec_base[b] + x]];
           block_out[j] = static_cast<int32_t>(b);
-          substep_out[j] = static_cast<int32_t>(gmajor ? cidx % T : cidx / G);
-          group_out[j] = static_cast<int32_t>(gmajor ? cidx / T : cidx % G);
+          substep_out[j] = static_cast<int32_t>(cidx / G);
+          group_out[j] = static_cast<int32_t>(cidx % G);
           pos_out[j] = x - off[cidx];
           if (replica_out) {  // 0: the item's own row; r: its replica r (scratch row)
             const uint32_t row = fp.recs[fp.rec_base[b] + x].i & ~kPadBit;
@@ -2413,44 +2312,13 @@ int debug_fast_plan(const int32_t* u, const int32_t* i, int64_t n, int32_t n_blo
 int mf_debug_fast_split(const int32_t* u, const int32_t* i, int64_t n, int32_t n_blocks, int64_t seed,
                         int32_t groups, int32_t blocking, int32_t window, int32_t item_split, int32_t* block_out,
                         int32_t* substep_out, int32_t* group_out, int64_t* pos_out, int32_t* replica_out) {
-  return mfhip::debug_fast_plan(u, i, n, n_blocks, seed, groups, blocking, window, item_split, 1, false, block_out,
+  return mfhip::debug_fast_plan(u, i, n, n_blocks, seed, groups, blocking, window, item_split, block_out,
                                 substep_out, group_out, pos_out, replica_out);
-}
-
-int mf_debug_fast_stream(const int32_t* u, const int32_t* i, int64_t n, int32_t n_blocks, int64_t seed,
-                         int32_t groups, int32_t ustride, int32_t window, int32_t* block_out, int32_t* substep_out,
-                         int32_t* group_out, int64_t* pos_out) {
-  if (ustride < 1 || groups < 1) return mfhip::guarded([] { MF_REQUIRE(false, "groups and ustride must be >= 1"); });
-  return mfhip::debug_fast_plan(u, i, n, n_blocks, seed, groups, MF_BLOCKING_REFERENCE, window, 0, ustride, true,
-                                block_out, substep_out, group_out, pos_out, nullptr);
-}
-
-int mf_debug_stream_protocol(const int32_t* u, const int32_t* i, int64_t n, int32_t n_blocks, int64_t seed,
-                             int32_t groups, int32_t ustride, int32_t k, int64_t* stuck_out) {
-  return mfhip::guarded([&] {
-    using namespace mfhip;
-    MF_REQUIRE(n >= 0 && n_blocks >= 1 && groups >= 1 && ustride >= 2 && stuck_out, "bad argument");
-    MF_REQUIRE(n == 0 || (u && i), "null argument");
-    SideLayout U, I;
-    build_side(U, u, n, n_blocks, seed, true);
-    build_side(I, i, n, n_blocks, seed, true);
-    std::vector<double> r(n, 1.0);
-    RatingBlocks rb;
-    build_rating_blocks(rb, U, I, u, i, r.data(), n, 0, n_blocks, false);
-    FastPlan fp;
-    build_fast_plan(fp, rb, U, I, groups, k, 1.0, static_cast<uint64_t>(seed) * 0x9E3779B97F4A7C15ULL + 1,
-                    static_cast<uint32_t>(U.rows()), nullptr, 2 * kStreamRing, nullptr, 0, 0, ustride, true);
-    PairPlan pp;
-    build_stream_plan(pp, fp, n_blocks, n_blocks, 0, k);
-    std::string rep;
-    *stuck_out = stream_protocol_deadlocks(pp, n_blocks, &rep);
-    if (*stuck_out && std::getenv("MFHIP_DEBUG_PLAN")) std::fprintf(stderr, "%s", rep.c_str());
-  });
 }
 
 const char* mf_fast_kernel_name(int32_t k) {
   switch (choose_fast_kernel(k)) {
-    case FastKernel::kPair: return want_pair_sys() ? (want_stream() ? "k_sweep_stream" : "k_sweep_pair_sys") : "k_sweep_pair";
+    case FastKernel::kPair: return want_pair_sys() ? "k_sweep_pair_sys" : "k_sweep_pair";
     case FastKernel::kPersistent: return "k_fast_superstep";
     default: return "k_fast_substep";
   }

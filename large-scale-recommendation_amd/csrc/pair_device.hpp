@@ -1,4 +1,4 @@
-// pair_device.hpp -- device helpers shared by the pair sweeps (kernels_pair.hip, kernels_stream.hip):
+// pair_device.hpp -- device helpers of the pair sweep (kernels_pair.hip):
 // wave reductions, raw-buffer row access, and the 64-B pair record chunks (plan.hpp PairRec).
 // Included inside namespace mfhip { namespace { ... } } of each kernel file.
 #pragma once
@@ -106,7 +106,6 @@ struct Chunk {
   uint32_t flags;
   float era, erb;           // eta * r
   float aa, ab, ba, bb;     // 1 - eta * ri, 1 - eta * ru (1 for no-op records)
-  uint32_t need;            // stream sweep: neighbour pairs required before this pair's loads
 };
 
 // A chunk's records as loaded (raw words, one pair per lane).  The next chunk is loaded a whole
@@ -141,6 +140,5 @@ __device__ __forceinline__ Chunk chunk_convert(const ChunkRaw& r, float eta) {
   ch.bb = fmaf(-eta, __uint_as_float(r.w3[0]), 1.f);
   ch.aa = fmaf(-eta, __uint_as_float(r.w3[1]), 1.f);
   ch.ab = fmaf(-eta, __uint_as_float(r.w3[2]), 1.f);
-  ch.need = r.w3[3];
   return ch;
 }

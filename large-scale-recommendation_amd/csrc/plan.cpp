@@ -558,16 +558,12 @@ inline uint32_t mix32(uint64_t x) {
 void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, const SideLayout& I,
                      int32_t G0, int32_t k, double lambda, uint64_t order_seed, uint32_t dummy_row,
                      std::vector<int64_t>* rec_src, int32_t window, const std::vector<int32_t>* block_groups,
-                     int32_t split_run, uint32_t scratch_base, int32_t ustride, bool gmajor,
-                     std::vector<FastBlockWork>* entries_out) {
+                     int32_t split_run, uint32_t scratch_base, std::vector<FastBlockWork>* entries_out) {
   const int64_t kHazardWindow = window;  // shadows the default for this plan
-  const int32_t K = std::max(ustride, 1);
   const uint32_t row_bytes = static_cast<uint32_t>(k) * 4u;
   const int32_t nb = rb.n_blocks;
   const int64_t nb2 = static_cast<int64_t>(nb) * nb;
   fp = FastPlan();
-  fp.K = K;
-  fp.gmajor = gmajor;
   fp.G = G0;
   fp.Gb.assign(nb2, G0);
   if (block_groups) {
@@ -626,8 +622,8 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
     BlockWork& W = work[bx];
     const int64_t b = blocks[bx];
     const int32_t G = fp.Gb[b];
-    const int64_t T = static_cast<int64_t>(K) * G;  // sub-steps = user groups
-    const int64_t GG = T * G;                        // cells
+    const int64_t T = G;       // sub-steps = user groups
+    const int64_t GG = T * G;  // cells
     const int32_t p = static_cast<int32_t>(b / nb), q = static_cast<int32_t>(b % nb);
     const int64_t ub = U.block_start[p], nu = U.block_start[p + 1] - ub;
     const int64_t ib = I.block_start[q], ni = I.block_start[q + 1] - ib;
@@ -683,9 +679,9 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
       std::vector<int32_t> cell_of(len);
       for (int64_t x = 0; x < len; ++x) {
         const int32_t g = gi[vil[x]], h = gu[ulx[x]];
-        const int64_t d = h - static_cast<int64_t>(K) * g;  // in (-T, T): h < T, K*g < K*G = T
+        const int64_t d = h - static_cast<int64_t>(g);  // in (-T, T)
         const int64_t t = d < 0 ? d + T : d;
-        cell_of[x] = static_cast<int32_t>(gmajor ? g * T + t : t * G + g);
+        cell_of[x] = static_cast<int32_t>(t * G + g);
         cstart[cell_of[x] + 1]++;
       }
       for (int64_t c = 0; c < GG; ++c) cstart[c + 1] += cstart[c];
@@ -702,7 +698,7 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
       for (int64_t c = 0; c < GG; ++c) {
         const int64_t c0 = cstart[c], m = cstart[c + 1] - c0;
         if (m < 2) continue;
-        const int32_t g = static_cast<int32_t>(gmajor ? c / T : c % G), ng = gsize[g];
+        const int32_t g = static_cast<int32_t>(c % G), ng = gsize[g];
         std::fill(bucket.begin(), bucket.begin() + ng + 1, 0);
         for (int64_t y = c0; y < c0 + m; ++y) bucket[irank[E[y].vil] + 1]++;
         for (int32_t r = 0; r < ng; ++r) bucket[r + 1] += bucket[r];
@@ -758,18 +754,16 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
     *entries_out = std::move(work);
     return;
   }
-  // Phase 2: emit.  Streams (a cell, or with gmajor one wave's K*G cells) are independent, so a
-  // block's cells are cut into chunks of whole streams of about kChunk entries, emitted in
-  // parallel and concatenated in cell order.
+  // Phase 2: emit.  Cells are independent, so a block's cells are cut into chunks of whole cells
+  // of about kChunk entries, emitted in parallel and concatenated in cell order.
   struct Chunk2 { int64_t bx, c0, c1; std::vector<FastRec> out; std::vector<int64_t> src; std::vector<int32_t> off; int64_t pads = 0; };
   std::vector<Chunk2> chunks;
   {
     constexpr int64_t kChunk = 1 << 17;
     for (int64_t bx = 0; bx < nblk; ++bx) {
       const BlockWork& W = work[bx];
-      const int64_t per = fp.gmajor ? W.T : 1;  // cells per stream
       int64_t c0 = 0;
-      for (int64_t c = per; c <= W.GG; c += per)
+      for (int64_t c = 1; c <= W.GG; ++c)
         if (c == W.GG || W.cstart[c] - W.cstart[c0] >= kChunk) {
           chunks.push_back(Chunk2{bx, c0, c, {}, {}, {}, 0});
           c0 = c;
@@ -789,8 +783,6 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
     const BlockWork& W = work[ck.bx];
     const int64_t b = blocks[ck.bx];
     const int64_t s = rb.start[b];
-    const int32_t G = fp.Gb[b];
-    const int64_t T = W.T;
     const uint32_t ub = static_cast<uint32_t>(W.ub);
     // Emit each cell as a sequence the kernel can run with a D-deep prefetch ring: every user
     // and every item row recurs either at the next position (the kernel forwards it in
@@ -802,7 +794,6 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
     // user row, current item).  last_*[x] = (stream, position) of the row's latest emission.
     // Groups are flat: an item group is a contiguous range of the cell's entries, a user group a
     // range of a per-cell CSR list (entries in cell order).
-    (void)G;
     std::vector<FastRec>& out = ck.out;
     std::vector<int64_t>& src = ck.src;
     std::vector<int32_t>& off = ck.off;
@@ -811,10 +802,8 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
     if (rec_src) src.reserve(n_in + n_in / 8 + 16);
     off.assign(ck.c1 - ck.c0, 0);  // end of each cell, relative to the chunk
     struct Last { int32_t sid, pos; };
-    // a stream that is one cell keeps its state per cell-local user / item slot (small, hot
-    // arrays); streams of several cells (gmajor) index it by local user / virtual item
-    const bool local = !gmajor;
-    std::vector<Last> last_u(local ? 0 : W.nu, Last{-1, 0}), last_i(local ? 0 : W.nv, Last{-1, 0});
+    // the emission state is kept per cell-local user / item slot (small, hot arrays)
+    std::vector<Last> last_u, last_i;
     std::vector<std::pair<int32_t, int32_t>> uslot(W.nu, {-1, 0});
     struct Ent { uint32_t ul, il; int32_t ug, ig; int64_t y; };
     struct Grp { int32_t beg = 0, end = 0, head = 0, left = 0; uint32_t row = 0; };  // [beg, end) of its list
@@ -823,19 +812,11 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
     std::vector<int32_t> ulist, ufill;  // user groups' entry lists (CSR over ugs)
     std::vector<uint8_t> taken;
     std::vector<int32_t> iorder;
-    // a stream (sid) is one cell, or with gmajor one wave's K*G cells in order: positions and the
-    // window count along the stream, and the last item of a cell is carried into the next one
-    int32_t cur_sid = -1;
-    int64_t stream_begin = 0;
-    uint32_t carry_il = UINT32_MAX, prev_irow = 0;
+    // positions and the window count from the start of the cell (sid = the cell)
     for (int64_t c = ck.c0; c < ck.c1; ++c) {
-      const int32_t sid = static_cast<int32_t>(gmajor ? c / T : c);
-      if (sid != cur_sid) {
-        cur_sid = sid;
-        stream_begin = static_cast<int64_t>(out.size());
-        carry_il = UINT32_MAX;
-        prev_irow = 0;
-      }
+      const int32_t sid = static_cast<int32_t>(c);
+      const int64_t stream_begin = static_cast<int64_t>(out.size());
+      uint32_t prev_irow = 0;
       ents.clear();
       igs.clear();
       ugs.clear();
@@ -854,10 +835,8 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
         ugs[us.second].end++;  // count for now
       }
       const int32_t m = static_cast<int32_t>(ents.size());
-      if (local) {  // slots of this cell start free
-        last_u.assign(ugs.size(), Last{-1, 0});
-        last_i.assign(igs.size(), Last{-1, 0});
-      }
+      last_u.assign(ugs.size(), Last{-1, 0});  // slots of this cell start free
+      last_i.assign(igs.size(), Last{-1, 0});
       {  // user groups: counts -> CSR ranges, entries in cell order
         int32_t acc = 0;
         for (auto& g2 : ugs) { const int32_t n2 = g2.end; g2.beg = g2.head = acc; acc += n2; g2.end = acc; }
@@ -876,15 +855,12 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
       });
       size_t iorder_head = 0;
       int32_t prev_ug = -1, prev_ig = -1;
-      if (carry_il != UINT32_MAX)  // the stream's last item has ratings here: continue its run
-        for (size_t g2 = 0; g2 < igs.size(); ++g2)
-          if (igs[g2].row == carry_il) { prev_ig = static_cast<int32_t>(g2); break; }
       int32_t left = m;
       while (left > 0) {
         const int32_t pos = static_cast<int32_t>(static_cast<int64_t>(out.size()) - stream_begin);
         auto free_at = [&](const Last& L) { return L.sid != sid || pos - L.pos >= kHazardWindow; };
-        auto ufree = [&](const Ent& en) { return free_at(local ? last_u[en.ug] : last_u[en.ul]); };
-        auto ifree = [&](int32_t ig, uint32_t il) { return free_at(local ? last_i[ig] : last_i[il]); };
+        auto ufree = [&](const Ent& en) { return free_at(last_u[en.ug]); };
+        auto ifree = [&](int32_t ig) { return free_at(last_i[ig]); };
         // the first untaken entries of a group's list (at most 4 * window of them) that pass ok
         auto scan = [&](Grp& g2, const int32_t* list, auto ok) -> int32_t {
           while (g2.head < g2.end && taken[list ? list[g2.head] : g2.head]) ++g2.head;
@@ -903,7 +879,7 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
         };
         auto try_user = [&]() -> int32_t {  // continue the user run
           if (prev_ug < 0 || ugs[prev_ug].left == 0) return -1;
-          return scan(ugs[prev_ug], ulist.data(), [&](const Ent& en) { return en.ig == prev_ig || ifree(en.ig, en.il); });
+          return scan(ugs[prev_ug], ulist.data(), [&](const Ent& en) { return en.ig == prev_ig || ifree(en.ig); });
         };
         const bool user_first = prev_ug >= 0 && prev_ig >= 0 && ugs[prev_ug].left > igs[prev_ig].left;
         int32_t pick = user_first ? try_user() : try_item();
@@ -915,7 +891,7 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
             Grp& g2 = igs[iorder[z]];
             if (g2.left == 0) continue;
             ++tried;
-            if (!ifree(iorder[z], g2.row)) continue;
+            if (!ifree(iorder[z])) continue;
             pick = scan(g2, nullptr, [&](const Ent& en) { return ufree(en); });
             if (pick >= 0) break;
           }
@@ -925,8 +901,7 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
                                 prev_irow | kPadBit, 0});
           if (rec_src) src.push_back(-1);
           ck.pads++;
-          if (prev_ig >= 0) (local ? last_i[prev_ig] : last_i[igs[prev_ig].row]) = Last{sid, pos};
-          else if (carry_il != UINT32_MAX && !local) last_i[carry_il] = Last{sid, pos};
+          if (prev_ig >= 0) last_i[prev_ig] = Last{sid, pos};
           prev_ug = -1;
           continue;
         }
@@ -935,11 +910,10 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
         --left;
         igs[en.ig].left--;
         ugs[en.ug].left--;
-        (local ? last_u[en.ug] : last_u[en.ul]) = Last{sid, pos};
-        (local ? last_i[en.ig] : last_i[en.il]) = Last{sid, pos};
+        last_u[en.ug] = Last{sid, pos};
+        last_i[en.ig] = Last{sid, pos};
         prev_ug = en.ug;
         prev_ig = en.ig;
-        carry_il = en.il;
         const uint32_t urow = en.ul + ub;
         prev_irow = W.vrow[en.il];
         out.push_back(FastRec{urow * row_bytes, prev_irow * row_bytes, W.e[en.y].r, W.regu[en.ul], W.regi[en.il], urow,
@@ -966,7 +940,7 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
     fp.rec_base[blocks[bx]] = total;
     fp.cell_base[blocks[bx]] = cells;
     total += blk_total[bx];
-    cells += static_cast<int64_t>(K) * fp.Gb[blocks[bx]] * fp.Gb[blocks[bx]] + 1;
+    cells += static_cast<int64_t>(fp.Gb[blocks[bx]]) * fp.Gb[blocks[bx]] + 1;
     fp.pads += pads[bx];
   }
   resize_huge(fp.recs, total);
@@ -1253,271 +1227,6 @@ void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, in
       pp.sys[sw.cell0 + cl.t] = pp.waves[w++];
     }
   }
-}
-
-// Stream schedule (plan.hpp StreamWave): the pair records of wave (sm, j, g) are its K*G cells'
-// records cut into pairs cell by cell (a pair never spans two cells, so every pair belongs to one
-// hand-off), with the forwarding flags of build_pair_plan computed along the whole stream (an item
-// run may continue across a cell boundary: kPairKeepQ, no store in between).  need of a pair of
-// cell t >= K = pairs of the neighbour's stream (item group g+1) through its cell t-K.
-void build_stream_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, int32_t shard, int32_t k,
-                       int32_t ring) {
-  if (!fp.gmajor) throw std::logic_error("build_stream_plan needs a g-major fast plan");
-  if (fp.K < 2) throw std::logic_error("the stream sweep needs K >= 2 user groups per item group");
-  pp = PairPlan();
-  pp.ring = ring;
-  const int32_t K = fp.K;
-  struct W { int64_t b; int32_t g, G; int64_t nbr_local; };
-  std::vector<W> ws;
-  pp.sys_off.assign(nb + 1, 0);
-  pp.sys_block_off.assign(static_cast<size_t>(nb) * (c + 1), 0);
-  std::vector<int64_t> first_of(static_cast<size_t>(nb) * c, 0);  // ws index of (sm, j, g = 0)
-  for (int32_t sm = 0; sm < nb; ++sm) {
-    pp.sys_off[sm] = static_cast<int64_t>(ws.size());
-    for (int32_t j = 0; j < c; ++j) {
-      const int32_t p = shard * c + j, q = (p + sm) % nb;
-      const int64_t b = static_cast<int64_t>(p) * nb + q;
-      const int32_t G = fp.cell_base[b] < 0 ? 0 : fp.Gb[b];
-      pp.sys_block_off[static_cast<size_t>(sm) * (c + 1) + j] = static_cast<int64_t>(ws.size()) - pp.sys_off[sm];
-      first_of[static_cast<size_t>(sm) * c + j] = static_cast<int64_t>(ws.size());
-      for (int32_t g = 0; g < G; ++g)
-        ws.push_back(W{b, g, G, static_cast<int64_t>(ws.size()) - pp.sys_off[sm] - g + (g + 1 == G ? 0 : g + 1)});
-    }
-    pp.sys_block_off[static_cast<size_t>(sm) * (c + 1) + c] = static_cast<int64_t>(ws.size()) - pp.sys_off[sm];
-  }
-  pp.sys_off[nb] = static_cast<int64_t>(ws.size());
-  const int64_t nw = static_cast<int64_t>(ws.size());
-  auto cell_range = [&](const W& w, int64_t t, const FastRec*& f, int64_t& len) {
-    const int64_t T = static_cast<int64_t>(K) * w.G;
-    const int32_t* off = fp.cell_off.data() + fp.cell_base[w.b];
-    const int64_t cid = static_cast<int64_t>(w.g) * T + t;
-    f = fp.recs.data() + fp.rec_base[w.b] + off[cid];
-    len = off[cid + 1] - off[cid];
-  };
-  // pass 1: pairs per cell, then no-op pairs appended where a cell t >= K would otherwise have
-  // fewer than kStreamRing - 1 pairs in its K-1 cells of slack (t-K, t): a wave blocked before
-  // cell t has computed and published all but its kStreamRing - 1 prefetched pairs, so with that
-  // many pairs of slack it has always finished the cells a waiter on it needs (no wait cycles).
-  std::vector<std::vector<int32_t>> pref(nw), cpad(nw);
-  parallel_tasks(nw, [&](int64_t x) {
-    const W& w = ws[x];
-    const int64_t T = static_cast<int64_t>(K) * w.G;
-    std::vector<int32_t> cnt(T, 0);
-    auto& pd = cpad[x];
-    pd.assign(T, 0);
-    for (int64_t t = 0; t < T; ++t) {
-      const FastRec* f;
-      int64_t len;
-      cell_range(w, t, f, len);
-      int32_t n = 0;
-      for (int64_t y = 0; y < len; ++n) y += (y + 1 < len && f[y + 1].u != f[y].u) ? 2 : 1;
-      cnt[t] = n;
-    }
-    for (int64_t t = T - 1; t >= K; --t) {  // descending: padding a cell makes it need slack of its own
-      if (cnt[t] + pd[t] == 0) continue;
-      int32_t slack = 0;
-      for (int64_t t2 = t - K + 1; t2 < t; ++t2) slack += cnt[t2] + pd[t2];
-      if (slack < ring - 1) pd[t - 1] += ring - 1 - slack;
-    }
-    auto& pr = pref[x];
-    pr.assign(T + 1, 0);
-    for (int64_t t = 0; t < T; ++t) pr[t + 1] = pr[t] + cnt[t] + pd[t];
-  });
-  pp.stream.resize(nw);
-  int64_t total = 0;
-  for (int64_t x = 0; x < nw; ++x) {
-    const int32_t np = pref[x].back();
-    pp.stream[x] = StreamWave{total, np, static_cast<int32_t>(ws[x].nbr_local)};
-    total += np;
-    pp.max_pairs = std::max<int64_t>(pp.max_pairs, np);
-  }
-  resize_huge(pp.recs, total);
-  std::vector<int64_t> noops(nw, 0);
-  std::vector<double> wbytes(nw, 0.0);
-  const double row_bytes = 4.0 * k;
-  auto item_of = [](const FastRec& f) { return f.i & ~kPadBit; };
-  auto is_pad = [](const FastRec& f) { return (f.i & kPadBit) != 0; };
-  parallel_tasks(nw, [&](int64_t x) {
-    const W& w = ws[x];
-    const int64_t T = static_cast<int64_t>(K) * w.G;
-    const int64_t sm0 = [&] { int64_t sm = 0; while (pp.sys_off[sm + 1] <= x) ++sm; return sm; }();
-    const std::vector<int32_t>& nbr_pref = pref[pp.sys_off[sm0] + w.nbr_local];
-    PairRec* const first = pp.recs.data() + pp.stream[x].base;
-    PairRec* out = first;
-    uint32_t last_u = kOffOOB, last_half = 0;
-    uint32_t prev_item = kOffOOB;  // item row of the stream's previous record
-    for (int64_t t = 0; t < T; ++t) {
-      const FastRec* f;
-      int64_t len;
-      cell_range(w, t, f, len);
-      const uint32_t need = t >= K ? static_cast<uint32_t>(nbr_pref[t - K + 1]) : 0u;
-      // the record after this cell in the stream (next non-empty cell), for the run-end store
-      const FastRec* after = nullptr;
-      for (int64_t t2 = t + 1; len > 0 && t2 < T && !after; ++t2) {
-        const FastRec* f2;
-        int64_t l2;
-        cell_range(w, t2, f2, l2);
-        if (l2 > 0) after = f2;
-      }
-      for (int64_t y = 0; y < len;) {
-        const FastRec& a = f[y];
-        const bool has_b = y + 1 < len && f[y + 1].u != a.u;
-        const int64_t ny = y + (has_b ? 2 : 1);
-        PairRec pr{};
-        uint32_t flags = 0;
-        const bool a_pad = is_pad(a);
-        if (!a_pad && last_u == a.u_off) flags |= last_half;
-        if (prev_item == item_of(a)) flags |= kPairKeepQ;
-        pr.ua = (a_pad || (flags & (kPairFwdA | kPairFwdB))) ? kOffOOB : a.u_off;
-        pr.ia = (flags & kPairKeepQ) ? kOffOOB : a.i_off;
-        pr.sa = a_pad ? kOffOOB : a.u_off;
-        pr.ra = a.r;
-        pr.rua = a.ru;
-        pr.ria = a.ri;
-        if (a_pad) noops[x]++;
-        pr.ib = pr.ub = pr.sb = pr.sia = kOffOOB;
-        const FastRec* tail = &a;
-        if (has_b) {
-          const FastRec& b2 = f[y + 1];
-          tail = &b2;
-          if (item_of(b2) != item_of(a)) {
-            flags |= kPairSplit;
-            pr.sia = a.i_off;
-            pr.ib = b2.i_off;
-          }
-          if (!is_pad(b2)) {
-            pr.ub = pr.sb = b2.u_off;
-            pr.rb = b2.r;
-            pr.rub = b2.ru;
-            pr.rib = b2.ri;
-          } else {
-            noops[x]++;
-          }
-        } else {
-          noops[x]++;
-        }
-        const FastRec* nxt = ny < len ? &f[ny] : after;
-        pr.si = (!nxt || item_of(*nxt) != item_of(*tail)) ? tail->i_off : kOffOOB;
-        pr.flags = flags;
-        pr.need = need;
-        *out++ = pr;
-        prev_item = item_of(*tail);
-        if (has_b) {
-          last_u = is_pad(f[y + 1]) ? kOffOOB : f[y + 1].u_off;
-          last_half = kPairFwdB;
-        } else {
-          last_u = a_pad ? kOffOOB : a.u_off;
-          last_half = kPairFwdA;
-        }
-        y = ny;
-      }
-      for (int32_t z = 0; z < cpad[x][t]; ++z) {  // slack padding: keeps the item run, touches no row
-        PairRec pr{};
-        pr.ua = pr.ub = pr.ia = pr.ib = pr.sa = pr.sb = pr.sia = pr.si = kOffOOB;
-        pr.flags = prev_item != kOffOOB ? kPairKeepQ : 0u;
-        pr.need = need;
-        *out++ = pr;
-        noops[x] += 2;
-        last_u = kOffOOB;
-      }
-    }
-    // one item run over the whole stream: the lean path
-    bool single = out > first && first[0].ia != kOffOOB && !(first[0].flags & (kPairKeepQ | kPairSplit));
-    int why = single ? 0 : 1;
-    for (const PairRec* r = first; single && r < out; ++r) {
-      single = !(r->flags & kPairSplit) && (r == first || (r->flags & kPairKeepQ)) && r->ub == r->sb &&
-               (r + 1 < out ? r->si == kOffOOB : r->si == first[0].ia);
-      if (!single) why = (r->flags & kPairSplit) ? 2 : !(r == first || (r->flags & kPairKeepQ)) ? 3 : r->ub != r->sb ? 4 : 5;
-    }
-    if (single) {  // a user row the lean path loads was stored at least `ring` pairs back
-      const int kR = ring - 1;
-      std::vector<std::array<uint32_t, 2>> rg(std::max(kR, 1), {kOffOOB, kOffOOB});
-      for (const PairRec* r = first; single && r < out; ++r) {
-        const int64_t j = r - first;
-        for (uint32_t o : {r->ua, r->ub}) {
-          if (o == kOffOOB) continue;
-          for (int z = 0; z < kR; ++z)
-            if (rg[z][0] == o || rg[z][1] == o) single = false;
-        }
-        if (kR > 0) {
-          rg[j % kR][0] = r->sa;
-          rg[j % kR][1] = r->sb;
-        }
-      }
-    }
-    if (single) pp.stream[x].nbr |= kStreamSingleRun;
-    else if (g_plan_debug && pp.stream[x].npairs > 4000) {
-      std::fprintf(stderr, "[mfhip] stream wave %lld (%d pairs) not single-run: reason %d\n", (long long)x,
-                   pp.stream[x].npairs, why);
-    }
-    int64_t rows = 0;
-    for (const PairRec* r = first; r < out; ++r) {
-      if (single) rows += (r->ua != kOffOOB) + 2 * (r->ub != kOffOOB) + (r->sa != kOffOOB);
-      else
-        for (uint32_t o : {r->ua, r->ub, r->ia, r->ib, r->sa, r->sb, r->sia, r->si}) rows += o != kOffOOB;
-    }
-    if (single) rows += 2;
-    wbytes[x] = 64.0 * static_cast<double>(out - first) + row_bytes * static_cast<double>(rows);
-  });
-  pp.sm_bytes.assign(nb, 0.0);
-  for (int32_t sm = 0; sm < nb; ++sm)
-    for (int64_t x = pp.sys_off[sm]; x < pp.sys_off[sm + 1]; ++x) {
-      pp.sm_bytes[sm] += wbytes[x];
-      pp.noop_halves += noops[x];
-    }
-}
-
-// Replays k_sweep_stream's hand-off protocol on the host, wave by wave in the kernel's order
-// (prologue gate for pairs 0..D-1; then compute j, publish j+1-D, gate pair j+D, compute j+1, ...;
-// a wave blocked at a gate first publishes every pair it has computed).  Returns the number of
-// supersteps whose waves cannot all finish (0: deadlock-free); `report` gets the first stuck state.
-int64_t stream_protocol_deadlocks(const PairPlan& pp, int32_t nb, std::string* report) {
-  const int64_t D = pp.ring;
-  int64_t bad = 0;
-  for (int32_t sm = 0; sm < nb; ++sm) {
-    const int64_t w0 = pp.sys_off[sm], nw = pp.sys_off[sm + 1] - w0;
-    std::vector<int64_t> comp(nw, 0), pub(nw, 0);
-    std::vector<char> gated(nw, 0);
-    bool moved = true;
-    int64_t done = 0;
-    while (moved) {
-      moved = false;
-      done = 0;
-      for (int64_t w = 0; w < nw; ++w) {
-        const StreamWave& sw = pp.stream[w0 + w];
-        const int64_t nbr = sw.nbr & ~kStreamSingleRun, n = sw.npairs;
-        const PairRec* R = pp.recs.data() + sw.base;
-        if (comp[w] >= n) { pub[w] = n; ++done; continue; }
-        while (comp[w] < n) {
-          if (!gated[w]) {
-            const int64_t p = comp[w] == 0 ? std::min<int64_t>(D, n) - 1 : comp[w] - 1 + D;
-            if (p < n && static_cast<int64_t>(R[p].need) > pub[nbr]) { pub[w] = std::max(pub[w], comp[w]); break; }
-            gated[w] = 1;
-          }
-          ++comp[w];
-          gated[w] = 0;
-          pub[w] = std::max(pub[w], comp[w] - D);
-          moved = true;
-        }
-        if (comp[w] >= n) pub[w] = n;
-      }
-    }
-    if (done != nw) {
-      if (report && bad == 0)
-        for (int64_t w = 0; w < nw; ++w) {
-          const StreamWave& sw = pp.stream[w0 + w];
-          if (comp[w] >= sw.npairs) continue;
-          const int64_t p = comp[w] == 0 ? std::min<int64_t>(D, sw.npairs) - 1 : comp[w] - 1 + D;
-          char line[200];
-          std::snprintf(line, sizeof line, "sm %d wave %lld (nbr %d): computed %lld of %d, gate pair %lld needs %u, nbr published %lld\n",
-                        sm, (long long)w, sw.nbr & ~kStreamSingleRun, (long long)comp[w], sw.npairs, (long long)p,
-                        pp.recs[sw.base + p].need, (long long)pub[sw.nbr & ~kStreamSingleRun]);
-          *report += line;
-        }
-      ++bad;
-    }
-  }
-  return bad;
 }
 
 void lpt_assign(const std::vector<int64_t>& load, int32_t G, std::vector<int32_t>& group) { lpt_groups(load, G, group); }

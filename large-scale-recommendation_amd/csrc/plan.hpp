@@ -221,12 +221,10 @@ struct FastBlockWork {
 
 struct FastPlan {
   int32_t G = 4;                       // rotation groups per rating block (the largest when per-block)
-  int32_t K = 1;                       // user groups per item group: a block has G item x K*G user groups
-  bool gmajor = false;                 // cell index g*(K*G) + t (stream order) instead of t*G + g
   std::vector<int32_t> Gb;             // per rating block (n*n): its rotation groups
   RecVec<FastRec> recs;                // all rating blocks of this shard, cell-major per block
   std::vector<int64_t> rec_base;       // per rating block (n*n), -1 if not on this shard
-  std::vector<int32_t> cell_off;       // per included rating block: K*Gb*Gb+1 relative offsets
+  std::vector<int32_t> cell_off;       // per included rating block: Gb*Gb+1 relative offsets
   std::vector<int64_t> cell_base;      // per rating block: index into cell_off (-1 if absent)
   int64_t pads = 0;                    // padding records inserted
   std::vector<SplitItem> splits;       // hot-item replicas, grouped by rating block
@@ -271,7 +269,7 @@ struct PairRec {
   uint32_t sa, sb, sia, si;  // stores: users A and B; A's item (split), the item after B (run end)
   uint32_t flags;
   float ra, rb, rua, rub, ria, rib;  // ratings and lambda/omega (0 for no-op records)
-  uint32_t need;  // stream sweep: neighbour pairs that must be complete before this pair's rows load
+  uint32_t pad_;  // keeps the record four 16-B words
 };
 static_assert(sizeof(PairRec) == 64, "PairRec is four 16-B words");
 // Systolic sweep wave: its G cells are PairPlan::sys[cell0 .. cell0+G), one per sub-step; it
@@ -282,28 +280,6 @@ struct SysWave {
   int32_t nbr;
 };
 static_assert(sizeof(SysWave) == 16, "SysWave is one 16-B word");
-
-// Stream sweep (k_sweep_stream, kernels_pair.hip): one launch per superstep, one wave per item
-// group g of each local rating block, sweeping its K*G cells t = 0..K*G-1 as ONE continuous pair
-// sequence (the prefetch ring and the record chunks run across cell boundaries).  With K*G user
-// groups, cell (g, t) takes user group (K*g + t) mod (K*G), so a user group is visited every K
-// sub-steps, by item groups g, g-1, g-2, ...: cell (g, t) depends only on cell (g+1 mod G, t-K).
-// Every pair of cell t carries `need` = the pair count of wave g+1's stream through its cell t-K;
-// a wave publishes how many of its pairs have completed stores, and loads a pair's rows only
-// once its neighbour's published count reaches the pair's need.  K >= 2 leaves K-1 cells of
-// slack between a hand-off and its use, so a wave normally never waits.
-constexpr int32_t kStreamSingleRun = 1 << 30;  // StreamWave::nbr flag: the stream is one item run
-// Default ring depth of the stream sweep (pairs prefetched ahead; the plan window is 2 * ring).  A
-// shallow ring keeps the window short, which small cells need (heavy users recur in them).
-// k_sweep_stream is built for depths 3, 5 and 7 (MFHIP_STREAM_RING).
-constexpr int kStreamRing = 3;
-constexpr int kStreamProgStride = 64;  // int32 words per wave's progress slot (one 256-B line pair)
-struct StreamWave {
-  int64_t base;    // first pair record
-  int32_t npairs;
-  int32_t nbr;     // neighbour wave (index within the superstep), | kStreamSingleRun
-};
-static_assert(sizeof(StreamWave) == 16, "StreamWave is one 16-B word");
 
 struct PairPlan {
   RecVec<PairRec> recs;
@@ -320,26 +296,14 @@ struct PairPlan {
   std::vector<int64_t> sys_block_off;  // nb * (c+1): first wave of local block j in superstep sm, relative to sys_off[sm]
   int64_t noop_halves = 0;       // pair halves that are no-ops (planner padding, repeated users)
   std::vector<double> sm_bytes;  // per superstep index: bytes the sweep requests (records + in-range rows)
-  // Stream tables (fp.gmajor): superstep sm's waves are stream[sys_off[sm] .. sys_off[sm+1]),
-  // local block j major (sys_block_off as above); max_pairs = the longest stream.
-  std::vector<StreamWave> stream;
-  int64_t max_pairs = 0;
-  int32_t ring = 0;  // stream sweep: its prefetch depth (the plan window is 2 * ring)
 };
 // The plan window must be >= 2 * kPairRing records.  substep_waves: order the cells (and
 // pp.waves / sub_off) per sub-step (sm, t), longest first, for the per-sub-step launches (needs a
 // uniform G); otherwise per superstep, and only the systolic tables are meaningful.
-// fp.gmajor: the stream tables instead (build_stream_plan).
 // cell_pairs (tables only): the pair count of every cell, indexed like fp.cell_off; the records
 // are then built elsewhere (kernels_plan.hip) and pp.recs stays empty, pp.waves[].cells generic.
 void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, int32_t shard, int32_t k,
                      bool substep_waves = true, const std::vector<int32_t>* cell_pairs = nullptr);
-// ring: the kernel's prefetch depth (kStreamRing or another depth k_sweep_stream is built for; the
-// fast plan's window must be 2 * ring).
-void build_stream_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, int32_t shard, int32_t k,
-                       int32_t ring = kStreamRing);
-// Host replay of k_sweep_stream's hand-off protocol on a built plan: supersteps that cannot finish.
-int64_t stream_protocol_deadlocks(const PairPlan& pp, int32_t nb, std::string* report = nullptr);
 
 int32_t choose_groups(int64_t avg_block_ratings, int32_t blocks_per_device, int32_t fast_waves,
                       double cell_target = 150.0, int32_t default_waves = 2048);
@@ -351,15 +315,11 @@ int32_t choose_groups(int64_t avg_block_ratings, int32_t blocks_per_device, int3
 // (the kernel's prefetch distance; kHazardWindow for kernels_fast.hip).
 // block_groups (optional, n*n): per rating block rotation groups (0 = G); otherwise G for all.
 // split_run > 0: hot-item replicas (SplitItem) with scratch item rows from scratch_base on.
-// ustride K >= 1: K*G user groups per block (cell (g, t) = user group (K*g + t) mod (K*G)).
-// gmajor: cells laid out wave by wave (index g*K*G + t) and each wave's cells planned as one
-// stream: the window holds across cell boundaries (k_sweep_stream); otherwise per cell.
 void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, const SideLayout& I,
                      int32_t G, int32_t k, double lambda, uint64_t order_seed, uint32_t dummy_row,
                      std::vector<int64_t>* rec_src = nullptr, int32_t window = kHazardWindow,
                      const std::vector<int32_t>* block_groups = nullptr, int32_t split_run = 0,
-                     uint32_t scratch_base = 0, int32_t ustride = 1, bool gmajor = false,
-                     std::vector<FastBlockWork>* entries_out = nullptr);
+                     uint32_t scratch_base = 0, std::vector<FastBlockWork>* entries_out = nullptr);
 
 // Longest-processing-time assignment of rows (by load) to G groups, as build_fast_plan's phase 1
 // does for the users and items of a rating block (kernels_plan.hip uses it on device counts).

@@ -1,4 +1,4 @@
-"""ctypes binding of libmfhip.so (include/mfhip.h).
+"""ctypes binding of libmfhip.so (include/mfhip.h; test hooks: include/mfhip_testing.h).
 
 This is the Python-side equivalent of the JNI shim in INTEGRATION.md: plain pointers and
 sizes, status codes mapped to exceptions.  The library has no CPU fallback; loading fails
@@ -66,8 +66,7 @@ class mf_params(C.Structure):
         ("online_init", C.c_int32),
         ("fast_waves", C.c_int32),
         ("fast_blocking", C.c_int32),
-        ("fast_item_split", C.c_int32),
-        ("reserved", C.c_int32 * 5),
+        ("reserved", C.c_int32 * 6),
     ]
 
 
@@ -94,10 +93,13 @@ EXPORTS = [
     "mf_get_factors", "mf_set_factors", "mf_predict", "mf_rmse", "mf_empirical_risk",
     "mf_block_update", "mf_online_update", "mf_lookup", "mf_set_profiling", "mf_get_stats",
     "mf_reset_stats", "mf_jvm_shuffle", "mf_jvm_block_of", "mf_jvm_random_factors",
-    "mf_learning_rate", "mf_debug_levels", "mf_debug_fast_schedule", "mf_debug_fast_split", "mf_fast_plan_window",
-    "mf_fast_kernel_name", "mf_get_params", "mf_read_ratings", "mf_save_model", "mf_load_model",
-    "mf_dsgd_restart", "mf_online_update_out", "mf_debug_ring_schedule", "mf_debug_fast_stream",
-    "mf_debug_stream_protocol", "mf_debug_plan_digest",
+    "mf_learning_rate", "mf_get_params", "mf_read_ratings", "mf_save_model", "mf_load_model",
+    "mf_dsgd_restart", "mf_online_update_out",
+]
+# The test hooks include/mfhip_testing.h declares (not product surface; same library).
+TESTING_EXPORTS = [
+    "mf_debug_levels", "mf_debug_fast_schedule", "mf_debug_fast_split", "mf_debug_ring_schedule",
+    "mf_debug_plan_digest", "mf_fast_plan_window", "mf_fast_kernel_name",
 ]
 
 _i32p = C.POINTER(C.c_int32)
@@ -157,10 +159,6 @@ def lib() -> C.CDLL:
                                              C.c_int32, _i32p, _i32p, _i32p, _i64p]),
         "mf_debug_fast_split": (C.c_int, [_i32p, _i32p, C.c_int64, C.c_int32, C.c_int64, C.c_int32, C.c_int32,
                                           C.c_int32, C.c_int32, _i32p, _i32p, _i32p, _i64p, _i32p]),
-        "mf_debug_fast_stream": (C.c_int, [_i32p, _i32p, C.c_int64, C.c_int32, C.c_int64, C.c_int32, C.c_int32,
-                                           C.c_int32, _i32p, _i32p, _i32p, _i64p]),
-        "mf_debug_stream_protocol": (C.c_int, [_i32p, _i32p, C.c_int64, C.c_int32, C.c_int64, C.c_int32, C.c_int32,
-                                               C.c_int32, _i64p]),
         "mf_fast_plan_window": (C.c_int, [C.c_int32, _i32p]),
         "mf_fast_kernel_name": (C.c_char_p, [C.c_int32]),
         "mf_get_params": (C.c_int, [C.c_void_p, C.POINTER(mf_params)]),

@@ -98,14 +98,16 @@ class PSOfflineOnlineMF:
         FactorInitializer on first touch (:247-252), and push deltas (Batch state, :322-330).
         Ratings arriving during a batch are queued and applied online after it (:221-226), which
         is what calling `process` after `batch` does.
-    Returned vectors are the model state after the call.  With emit_outputs (default) every
-    rating's worker output -- ps.output(user, userVec + deltaItemVec), userVec before the update
-    (:176), the reference's stream out of this operator -- is kept in `self.output` after each
-    call as (user ids, n x k vectors) in application order (mf_online_update_out)."""
+    Returned vectors are the model state after the call.  With emit_outputs=True every rating's
+    worker output -- ps.output(user, userVec + deltaItemVec), userVec before the update (:176), the
+    reference's stream out of this operator -- is kept in `self.output` after each call as (user
+    ids, n x k vectors) in application order (mf_online_update_out; a batch keeps all its passes,
+    iterations x n rows, as the reference emits them).  Off by default: per-rating records need
+    the level-by-level replay instead of the one-launch online sweep, and n x k f64 per call."""
 
     def __init__(self, num_factors: int, learning_rate: float = 0.01, iterations: int = 10,
                  init: str = "pseudo_random", seed: int = 0, mode: str = "deterministic",
-                 emit_outputs: bool = True):
+                 emit_outputs: bool = False):
         self.k = num_factors
         self.iterations = iterations
         self.emit_outputs = emit_outputs
@@ -143,7 +145,7 @@ class PSOfflineOnlineMF:
         ids, outs = [], []
         for u, i, r in passes:
             if self.emit_outputs:
-                uo, _ = ctx.online_update_out(u, i, r, L.ONLINE_DELTA)
+                uo, _ = ctx.online_update_out(u, i, r, L.ONLINE_DELTA, items=False)
                 ids.append(u)
                 outs.append(uo)
             else:

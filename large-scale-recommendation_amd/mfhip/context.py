@@ -151,19 +151,21 @@ class Context:
                                        flavour, num_partitions, C.byref(tu), C.byref(ti)))
         return tu.value, ti.value
 
-    def online_update_out(self, u, i, r, flavour: int = L.ONLINE_NEXT_FACTORS):
+    def online_update_out(self, u, i, r, flavour: int = L.ONLINE_NEXT_FACTORS, items: bool = True):
         """online_update plus the per-rating records the operators emit (mf_online_update_out):
         NEXT_FACTORS -> (user', item') per rating (FlinkOnlineMF.scala:131-135); DELTA ->
-        (userVec + deltaItemVec, deltaItemVec) per rating (PSOfflineOnlineMF.scala:174-176)."""
+        (userVec + deltaItemVec, deltaItemVec) per rating (PSOfflineOnlineMF.scala:174-176).
+        items=False: the item records are not produced (None; no n x k buffer, no copy back).
+        Per-rating records need the level-by-level replay, slower than online_update's sweep."""
         u, i, r = as_i32(u), as_i32(i), as_f64(r)
         n = same_length(u, i, r)
         uo = np.empty((max(n, 1), self.k), np.float64)
-        io = np.empty((max(n, 1), self.k), np.float64)
+        io = np.empty((max(n, 1), self.k), np.float64) if items else None
         tu, ti = C.c_int64(0), C.c_int64(0)
         check(L.lib().mf_online_update_out(self._h, ptr(u, C.c_int32), ptr(i, C.c_int32), ptr(r, C.c_double), n,
                                            flavour, 0, C.byref(tu), C.byref(ti), ptr(uo, C.c_double),
-                                           ptr(io, C.c_double)))
-        return uo[:n], io[:n]
+                                           ptr(io, C.c_double) if items else None))
+        return uo[:n], (io[:n] if items else None)
 
     # -- snapshots (TemporaryPath persistence, DSGDforMF.scala:291-296, 330-349) --
     def save(self, path: str) -> None:

@@ -113,15 +113,13 @@ class DSGDforMF:
     mode="deterministic" replays the reference's exact per-block update order in f64 (same
     seed => bit-identical factors); mode="fast" runs the f32 conflict-free rotation schedule.
     devices: GPU ids for an in-process multi-GPU fit (numBlocks must be a multiple of their count).
-    item_split: fast mode only, hot-item replicas (mf_params.fast_item_split; 0 = off).
     """
 
     def __init__(self, mode: str = "deterministic", devices: Optional[Sequence[int]] = None,
-                 fast_waves: int = 0, item_split: int = 0):
+                 fast_waves: int = 0):
         self.mode = mode
         self.devices = list(devices) if devices is not None else None
         self.fast_waves = fast_waves
-        self.item_split = item_split
         self.parameters = {
             "NumFactors": 10, "Lambda": 1.0, "Iterations": 10, "Blocks": None, "Seed": 0,
             "TemporaryPath": None, "LearningRate": 0.001, "LearningRateMethod": LearningRateMethod.Default,
@@ -156,7 +154,6 @@ class DSGDforMF:
         p.lr_arg = float(m.arg)
         p.mode = L.MODE_FAST_F32 if self.mode == "fast" else L.MODE_DETERMINISTIC_F64
         p.fast_waves = self.fast_waves
-        p.fast_item_split = self.item_split
         return p
 
     # FitOperation (DSGDforMF.scala:262-357)

@@ -8,8 +8,12 @@ Replaces the per-rating operators of the reference's streaming jobs:
   * OnlineSpark.buildModelWithMap (sp/OnlineSpark.scala:164-232): one
     OfflineSpark.offlineDSGDUpdatesOnly sweep per micro-batch (sp/OfflineSpark.scala:91-207).
   * The PS worker update (fl/mf/PSOfflineOnlineMF.scala:167-180): SGDUpdater.delta + "vec + delta".
-The batch is split on the host into dependency levels (no two updates of a level share a
-row); each level is one HIP launch, so the GPU result is the sequential result.
+A batch is ONE persistent launch (k_online_sweep): the updates of an item run in sequence order
+on one wave (the item row stays in registers), and an update whose user was updated earlier in
+the batch waits for that user's ticket, so the GPU result is the sequential result; the wave
+lists and tickets are built on the device (kernels_online.hip).  Per-rating output records
+(Context.online_update_out) use the level-by-level replay instead (one launch per dependency
+level: no two updates of a level share a row).
 """
 from __future__ import annotations
 

@@ -33,6 +33,10 @@ struct JNINativeInterface_ {
   jsize (*GetArrayLength)(JNIEnv*, jarray);
   jint* (*GetIntArrayElements)(JNIEnv*, jintArray, jboolean*);
   void (*ReleaseIntArrayElements)(JNIEnv*, jintArray, jint*, jint);
+  jdouble* (*GetDoubleArrayElements)(JNIEnv*, jdoubleArray, jboolean*);
+  void (*ReleaseDoubleArrayElements)(JNIEnv*, jdoubleArray, jdouble*, jint);
+  jbyte* (*GetByteArrayElements)(JNIEnv*, jbyteArray, jboolean*);
+  void (*ReleaseByteArrayElements)(JNIEnv*, jbyteArray, jbyte*, jint);
   jbyteArray (*NewByteArray)(JNIEnv*, jsize);
   void (*GetByteArrayRegion)(JNIEnv*, jbyteArray, jsize, jsize, jbyte*);
   void (*SetByteArrayRegion)(JNIEnv*, jbyteArray, jsize, jsize, const jbyte*);

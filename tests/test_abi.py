@@ -13,10 +13,11 @@ from mfhip import _lib as L
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "mfhip.h")
+TESTING_HEADER = os.path.join(ROOT, "include", "mfhip_testing.h")
 
 
-def declared_functions():
-    txt = open(HEADER).read()
+def declared_functions(path=HEADER):
+    txt = open(path).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
     return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\**\s+\**(mf_\w+)\s*\(", txt, flags=re.M)))
 
@@ -28,6 +29,19 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(lib, n), n
     assert sorted(L.EXPORTS) == names
+    hooks = declared_functions(TESTING_HEADER)
+    for n in hooks:
+        assert hasattr(lib, n), n
+    assert sorted(L.TESTING_EXPORTS) == hooks
+    assert not set(hooks) & set(names)
+
+
+def test_public_header_is_the_product_surface():
+    """include/mfhip.h holds the SURVEY 8b surface plus stats and I/O: no debug hooks, no
+    experiment knobs (those live in mfhip_testing.h / environment variables)."""
+    names = declared_functions()
+    assert not [n for n in names if n.startswith("mf_debug") or "fast_" in n]
+    assert "item_split" not in open(HEADER).read()
 
 
 def test_params_defaults_match_reference():

@@ -13,12 +13,11 @@ pytestmark = pytest.mark.gpu
 
 
 def params(k, iterations, nb, seed, mode=L.MODE_DETERMINISTIC_F64, lam=1.0, lr=0.001, fast_waves=0, has_seed=1,
-           blocking=L.BLOCKING_REFERENCE, item_split=0):
+           blocking=L.BLOCKING_REFERENCE):
     p = L.default_params()
     p.num_factors, p.iterations, p.num_blocks, p.seed, p.mode = k, iterations, nb, seed, mode
     p.lambda_, p.learning_rate, p.fast_waves, p.has_seed = lam, lr, fast_waves, has_seed
     p.fast_blocking = blocking
-    p.fast_item_split = item_split
     return p
 
 
@@ -284,14 +283,14 @@ def test_fast_kernel_equals_its_schedule(k, nb, G, hot):
 
 
 @pytest.mark.parametrize("k,nb,G,split", [(128, 1, 4, 60), (64, 2, 8, 40), (256, 1, 8, 100), (40, 2, 4, 50)])
-def test_hot_item_replicas_equal_their_schedule(k, nb, G, split):
-    """fast_item_split: fork (replica rows), the sweep over replica rows, and the averaging join
+def test_hot_item_replicas_equal_their_schedule(monkeypatch, k, nb, G, split):
+    """MFHIP_ITEM_SPLIT (experiment): fork (replica rows), the sweep over replica rows, and the averaging join
     == a sequential f64 replay of the same plan with the same fork/join."""
     d = hot_item_data(k)
     seed, lam, lr, iters = 3, 1.0, 0.002, 2
     uids, U, iids, I = fast_split_replay_reference(d, k, nb, seed, G, iters, lam, lr, split)
-    with mfhip.Context(params(k, iters, nb, seed, mode=L.MODE_FAST_F32, lam=lam, lr=lr, fast_waves=-G,
-                              item_split=split)) as ctx:
+    monkeypatch.setenv("MFHIP_ITEM_SPLIT", str(split))
+    with mfhip.Context(params(k, iters, nb, seed, mode=L.MODE_FAST_F32, lam=lam, lr=lr, fast_waves=-G)) as ctx:
         ctx.fit(d.u, d.i, d.r)
         a_ids, a_u = ctx.factors(0)
         b_ids, a_i = ctx.factors(1)
@@ -305,27 +304,29 @@ def test_hot_item_replicas_systolic_equals_substep(monkeypatch):
     d = synth.generate(20000, 3000, 400_000, seed=4)
     outs = []
     monkeypatch.setenv("MFHIP_BLOCK_GROUPS", "0")  # the same uniform G for both drivers
+    monkeypatch.setenv("MFHIP_ITEM_SPLIT", "300")
     for sys_on in ("1", "0"):
         monkeypatch.setenv("MFHIP_PAIR_SYS", sys_on)
-        with mfhip.Context(params(128, 2, 4, 1, mode=L.MODE_FAST_F32, item_split=300)) as ctx:
+        with mfhip.Context(params(128, 2, 4, 1, mode=L.MODE_FAST_F32)) as ctx:
             ctx.fit(d.u, d.i, d.r)
             outs.append((ctx.factors(0)[1], ctx.factors(1)[1], ctx.stats()["kernel_launches"]))
     assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
     assert outs[0][2] < outs[1][2]
 
 
-def test_hot_item_replicas_multi_shard_matches_single():
+def test_hot_item_replicas_multi_shard_matches_single(monkeypatch):
     """Replica rows are per-shard scratch outside the rotated item blocks: virtual shards agree."""
     d = synth.generate(3000, 600, 100_000, seed=12)
     outs = []
+    monkeypatch.setenv("MFHIP_ITEM_SPLIT", "200")
     for devs in ([0], [0, 0]):
-        with mfhip.Context(params(64, 2, 4, 1, mode=L.MODE_FAST_F32, item_split=200), devices=devs) as ctx:
+        with mfhip.Context(params(64, 2, 4, 1, mode=L.MODE_FAST_F32), devices=devs) as ctx:
             ctx.fit(d.u, d.i, d.r)
             outs.append((ctx.factors(0)[1], ctx.factors(1)[1]))
     assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
 
 
-def test_hot_item_replicas_rmse_within_one_percent_of_reference():
+def test_hot_item_replicas_rmse_within_one_percent_of_reference(monkeypatch):
     """Replicas relax the hot items' sequential chains, so they change the trajectory (averaged
     chains): an opt-in with a looser bar than the default fast mode -- held-out RMSE after 10
     epochs within 1% of the f64 reference order (measured: +0.73% here; on the NFLX-shaped
@@ -334,7 +335,8 @@ def test_hot_item_replicas_rmse_within_one_percent_of_reference():
     (tu, ti, tr), (eu, ei, er) = d.split()
     m = coracle.dsgd_fit(tu, ti, tr, k=64, iterations=10, n_blocks=4, seed=0, threads=4)
     ref, _ = m.rmse(eu, ei, er)
-    with mfhip.Context(params(64, 10, 4, 0, mode=L.MODE_FAST_F32, item_split=500)) as ctx:
+    monkeypatch.setenv("MFHIP_ITEM_SPLIT", "500")
+    with mfhip.Context(params(64, 10, 4, 0, mode=L.MODE_FAST_F32)) as ctx:
         ctx.fit(tu, ti, tr)
         fast, cnt = ctx.rmse(eu, ei, er)
     assert abs(fast - ref) / ref < 0.01, (fast, ref)
@@ -508,99 +510,6 @@ def test_device_blocking_equals_host_blocking(monkeypatch, mode, k, nb, seed):
     for s in (0, 1):
         assert np.array_equal(outs[0][s][0], outs[1][s][0])
         assert np.array_equal(outs[0][s][1], outs[1][s][1])
-
-
-def fast_stream_replay_reference(d, k, nb, seed, G, K, iterations, lam, lr):
-    """fast_replay_reference for the stream sweep's plan (K*G user groups, window 2 * kStreamRing)."""
-    from test_schedule import fast_stream_schedule
-    b, t, g, p = fast_stream_schedule(d.u, d.i, nb, seed, G, K, window=6)
-    uids = np.unique(d.u); iids = np.unique(d.i)
-    urow = np.searchsorted(uids, d.u).astype(np.int32)
-    irow = np.searchsorted(iids, d.i).astype(np.int32)
-    U = np.stack([O.random_factors(k, O.JavaRandom(int(x) ^ seed)) for x in uids])
-    I = np.stack([O.random_factors(k, O.JavaRandom(int(x) ^ seed)) for x in iids])
-    ru = lam / np.bincount(urow).astype(np.float64)
-    ri = lam / np.bincount(irow).astype(np.float64)
-    for s in range(1, iterations * nb + 1):
-        eta = O.learning_rate(0, lr, s // nb + 1, lam)
-        idx = np.where(((b // nb + s - 1) % nb) == (b % nb))[0]
-        order = idx[np.lexsort((p[idx], g[idx], b[idx], t[idx]))]
-        coracle.dsgd_apply(urow[order], irow[order], d.r[order], U, I, ru, ri, k, eta)
-    return uids, U, iids, I
-
-
-@pytest.mark.parametrize("k,nb,G,K,hot", [(64, 2, 8, 2, False), (128, 3, 4, 2, True), (128, 1, 8, 3, True),
-                                          (256, 2, 8, 2, False), (64, 4, 16, 2, True), (128, 2, 1, 2, False)])
-def test_stream_sweep_equals_its_schedule(monkeypatch, k, nb, G, K, hot):
-    """k_sweep_stream (one pair stream per item group, per-pair hand-offs through progress words,
-    rows prefetched across cell boundaries) == the sequential f64 replay of its plan."""
-    monkeypatch.setenv("MFHIP_STREAM", "1")
-    monkeypatch.setenv("MFHIP_STREAM_K", str(K))
-    d = hot_item_data(k) if hot else synth.generate(400, 120, 12000, seed=k)
-    seed, lam, lr, iters = 3, 1.0, 0.002, 2
-    uids, U, iids, I = fast_stream_replay_reference(d, k, nb, seed, G, K, iters, lam, lr)
-    with mfhip.Context(params(k, iters, nb, seed, mode=L.MODE_FAST_F32, lam=lam, lr=lr, fast_waves=-G,
-                              blocking=L.BLOCKING_REFERENCE)) as ctx:
-        ctx.fit(d.u, d.i, d.r)
-        assert ctx.stats()["kernel_launches"] <= iters * nb  # one stream launch per superstep
-        a_ids, a_u = ctx.factors(0)
-        b_ids, a_i = ctx.factors(1)
-    assert np.array_equal(a_ids, uids) and np.array_equal(b_ids, iids)
-    np.testing.assert_allclose(a_u, U, rtol=2e-4, atol=2e-5)
-    np.testing.assert_allclose(a_i, I, rtol=2e-4, atol=2e-5)
-
-
-@pytest.mark.parametrize("K", [2, 4])
-def test_stream_sweep_large_hot_item_equals_schedule(monkeypatch, K):
-    """400k ratings, one very hot item and a Zipf tail, G = 32: thousands of hand-offs per superstep
-    run concurrently; a stale user row read across a hand-off would break the replay equality."""
-    monkeypatch.setenv("MFHIP_STREAM", "1")
-    monkeypatch.setenv("MFHIP_STREAM_K", str(K))
-    n, k, nb, G = 400_000, 64, 2, 32
-    big = synth.generate(n // 20, 2000, n, seed=5)
-    hu = np.arange(0, n // 20, 2, dtype=np.int32)
-    d = big
-    d.u = np.concatenate([big.u, hu])
-    d.i = np.concatenate([big.i, np.full(len(hu), 7, np.int32)])
-    d.r = np.concatenate([big.r, np.ones(len(hu))])
-    seed, lam, lr, iters = 3, 1.0, 0.002, 1
-    uids, U, iids, I = fast_stream_replay_reference(d, k, nb, seed, G, K, iters, lam, lr)
-    with mfhip.Context(params(k, iters, nb, seed, mode=L.MODE_FAST_F32, lam=lam, lr=lr, fast_waves=-G,
-                              blocking=L.BLOCKING_REFERENCE)) as ctx:
-        ctx.fit(d.u, d.i, d.r)
-        a_u, a_i = ctx.factors(0)[1], ctx.factors(1)[1]
-    np.testing.assert_allclose(a_u, U, rtol=5e-4, atol=5e-5)
-    np.testing.assert_allclose(a_i, I, rtol=5e-4, atol=5e-5)
-
-
-@pytest.mark.parametrize("shards,nb", [(2, 4), (4, 8)])
-def test_stream_multi_shard_and_overlap_match_single(monkeypatch, shards, nb):
-    """Stream sweep on virtual shards (c = nb/shards >= 2: split launches with the ring step
-    overlapped) == one shard, bitwise."""
-    monkeypatch.setenv("MFHIP_STREAM", "1")
-    d = synth.generate(4000, 900, 120000, seed=31)
-    outs = []
-    for devs in ([0], [0] * shards):
-        with mfhip.Context(params(64, 2, nb, 5, mode=L.MODE_FAST_F32, fast_waves=-8), devices=devs) as ctx:
-            ctx.fit(d.u, d.i, d.r)
-            outs.append((ctx.factors(0)[1], ctx.factors(1)[1]))
-    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
-
-
-@pytest.mark.parametrize("K", [2, 3])
-def test_stream_rmse_within_half_percent_of_reference(monkeypatch, K):
-    """North-star fast-mode bar for the stream sweep (default G, K user groups per item group)."""
-    monkeypatch.setenv("MFHIP_STREAM", "1")
-    monkeypatch.setenv("MFHIP_STREAM_K", str(K))
-    d = synth.generate(20000, 3000, 1_000_000, seed=11)
-    (tu, ti, tr), (eu, ei, er) = d.split()
-    m = coracle.dsgd_fit(tu, ti, tr, k=64, iterations=10, n_blocks=4, seed=0, threads=4)
-    ref, _ = m.rmse(eu, ei, er)
-    with mfhip.Context(params(64, 10, 4, 0, mode=L.MODE_FAST_F32)) as ctx:
-        ctx.fit(tu, ti, tr)
-        assert L.lib().mf_fast_kernel_name(64) == b"k_sweep_stream"
-        fast, cnt = ctx.rmse(eu, ei, er)
-    assert abs(fast - ref) / ref < 0.005, (fast, ref)
 
 
 @pytest.mark.parametrize("k,nb,kind", [(64, 4, "zipf"), (128, 8, "zipf"), (128, 2, "hot"), (256, 4, "zipf"),

@@ -117,7 +117,7 @@ def test_ps_offline_online_matches_oracle():
     from mfhip.combined import PSOfflineOnlineMF
     d = synth.generate(90, 50, 1500, seed=13)
     k, lr, iters = 5, 0.02, 3
-    m = PSOfflineOnlineMF(k, lr, iterations=iters)
+    m = PSOfflineOnlineMF(k, lr, iterations=iters, emit_outputs=True)
     users, items, hist = {}, {}, []
     steps = ["o", "o", "b", "o", "o", "o", "b", "o"]
     x = 0

@@ -78,7 +78,7 @@ def fast_schedule_split(u, i, nb, seed, G, item_split, blocking=L.BLOCKING_REFER
 
 @pytest.mark.parametrize("nb,G,split", [(1, 8, 50), (2, 8, 30), (3, -64, 40), (2, 16, 7)])
 def test_hot_item_replicas_split_and_stay_conflict_free(nb, G, split):
-    """fast_item_split: an item with m > split ratings in a rating block is swept as
+    """MFHIP_ITEM_SPLIT (experiment): an item with m > split ratings in a rating block is swept as
     R = ceil(m / split) chains of at most `split` ratings (round-robin), each chain its own
     physical row, and within a (stratum, sub-step) no physical row appears in two cells."""
     d = synth.generate(500, 200, 20000, seed=2)
@@ -155,77 +155,3 @@ def test_fast_rotation_is_conflict_free(nb, G, window):
         items_in_order = d.i[m[np.argsort(pos)]]
         runs += int(np.sum(items_in_order[1:] == items_in_order[:-1]))
     assert runs > 0
-
-
-def fast_stream_schedule(u, i, nb, seed, G, K, window=0):
-    """mf_debug_fast_stream: (block, sub-step t in [0, K*G), item group g, position in the cell)."""
-    n = len(u)
-    b = np.empty(n, np.int32); t = np.empty(n, np.int32); g = np.empty(n, np.int32); p = np.empty(n, np.int64)
-    L.check(L.lib().mf_debug_fast_stream(L.ptr(L.as_i32(u), C.c_int32), L.ptr(L.as_i32(i), C.c_int32), n, nb, seed,
-                                         G, K, window, L.ptr(b, C.c_int32), L.ptr(t, C.c_int32), L.ptr(g, C.c_int32),
-                                         L.ptr(p, C.c_int64)))
-    return b, t, g, p
-
-
-@pytest.mark.parametrize("nb,G,K", [(1, 4, 1), (2, 8, 2), (3, 4, 3), (4, 16, 2), (2, 1, 4)])
-def test_stream_plan_user_groups_rotate_by_K(nb, G, K):
-    """Stream plan (k_sweep_stream): K*G user groups per rating block, cell (g, t) holds user group
-    (K*g + t) mod (K*G).  So every user keeps one residue (K*g + t) mod (K*G) over all its ratings
-    of a block, consecutive visits of its group are K sub-steps apart with item group g-1 (the
-    hand-off the kernel gates on: cell (g, t) after cell (g+1, t-K)), and within a (stratum,
-    sub-step) no user or item row is in two cells."""
-    d = synth.generate(600, 240, 24000, seed=nb + K)
-    b, t, g, p = fast_stream_schedule(d.u, d.i, nb, 3, G, K, window=6)
-    T = K * G
-    assert t.min() >= 0 and t.max() < T and g.min() >= 0 and g.max() < G
-    res = (K * g.astype(np.int64) + t) % T
-    for x in np.unique(b):
-        m = b == x
-        for uu in np.unique(d.u[m]).tolist():
-            assert len(set(res[m & (d.u == uu)].tolist())) == 1  # one user group per user
-        for it in np.unique(d.i[m]).tolist():
-            assert len(set(g[m & (d.i == it)].tolist())) == 1  # one item group per item
-        # a user group's visits, in sub-step order: t advances by K, g steps down by 1 (mod G)
-        for grp in np.unique(res[m]).tolist():
-            sel = m & (res == grp)
-            visits = sorted({(int(tt), int(gg)) for tt, gg in zip(t[sel], g[sel])})
-            for (t0, g0), (t1, g1) in zip(visits, visits[1:]):
-                assert (t1 - t0) % K == 0 and g1 == (g0 - (t1 - t0) // K) % G
-    for s in range(nb):
-        in_stratum = ((b // nb + s) % nb) == (b % nb)
-        for tt in np.unique(t[in_stratum]):
-            mm = in_stratum & (t == tt)
-            cell = b[mm].astype(np.int64) * G + g[mm]
-            for ids in (d.u[mm], d.i[mm]):
-                owner = {}
-                for x, c in zip(ids.tolist(), cell.tolist()):
-                    assert owner.setdefault(x, c) == c
-
-
-def test_stream_plan_window_holds_along_each_stream():
-    """Along a wave's stream (its cells t = 0..K*G-1 in order) a user or item row recurs only at the
-    next position (forwarded in registers) or >= window positions later -- across cell boundaries
-    too, since the stream kernel's row ring does not stop at them."""
-    d = synth.generate(400, 60, 30000, seed=7)  # few items: item rows recur across cells all the time
-    nb, G, K, win = 2, 4, 2, 6
-    b, t, g, p = fast_stream_schedule(d.u, d.i, nb, 3, G, K, window=win)
-    for x in np.unique(b):
-        for gg in range(G):
-            m = np.where((b == x) & (g == gg))[0]
-            if len(m) == 0:
-                continue
-            order = m[np.lexsort((p[m], t[m]))]
-            # inside a cell positions count the padding records too: gaps are exact there
-            for tt in np.unique(t[order]).tolist():
-                c = order[t[order] == tt]
-                for ids in (d.u[c], d.i[c]):
-                    last = {}
-                    for pos, x2 in zip(p[c].tolist(), ids.tolist()):
-                        if x2 in last:
-                            assert pos - last[x2] == 1 or pos - last[x2] >= win, (pos, last[x2])
-                        last[x2] = pos
-            # users never recur across cells of one stream (each cell is a different user group)
-            cells_of_user = {}
-            for uu, tt in zip(d.u[order].tolist(), t[order].tolist()):
-                cells_of_user.setdefault(uu, set()).add(tt)
-            assert all(len(v) == 1 for v in cells_of_user.values())

@@ -49,91 +49,6 @@ int main(int argc, char** argv) {
   RatingBlocks rb;
   build_rating_blocks(rb, U, I, u.data(), i.data(), r.data(), n, 0, nb, false);
   std::printf("rating blocks %.3f s\n", lap());
-  const int Gs = argc > 5 ? std::atoi(argv[5]) : 0, Ks = argc > 6 ? std::atoi(argv[6]) : 0;
-  if (Ks > 0) {  // stream plan: uniform G = Gs per block, K = Ks user groups per item group
-    FastPlan fp;
-    const int win = std::getenv("PROBE_WINDOW") ? std::atoi(std::getenv("PROBE_WINDOW")) : 2 * kPairRing;
-    const uint64_t oseed = static_cast<uint64_t>(pseed) * 0x9E3779B97F4A7C15ULL + 1;  // as mf_dsgd_prepare
-    build_fast_plan(fp, rb, U, I, Gs, k, 1.0, oseed, static_cast<uint32_t>(U.rows()), nullptr, win, nullptr, 0, 0,
-                    Ks, true);
-    std::printf("fast plan (stream, G %d K %d) %.3f s\n", Gs, Ks, lap());
-    PairPlan pp;
-    build_stream_plan(pp, fp, nb, nb, 0, k);
-    std::printf("stream plan %.3f s: pads %lld noop halves %lld pairs %zu max stream %lld\n", lap(), (long long)fp.pads,
-                (long long)pp.noop_halves, pp.recs.size(), (long long)pp.max_pairs);
-    {  // protocol simulation, in the kernel's order: prologue gate (pairs 0..D-1), then compute j,
-       // publish j+1-D, gate pair j+D (load its rows), compute j+1, ...; a wave blocked at a gate
-       // first publishes every pair it has computed.  Reports any deadlock.
-      const int D = kStreamRing;
-      for (int sm = 0; sm < nb; ++sm) {
-        const int64_t w0 = pp.sys_off[sm], nw = pp.sys_off[sm + 1] - w0;
-        std::vector<int64_t> comp(nw, 0), pub(nw, 0);
-        std::vector<char> gated(nw, 0);  // the gate in front of the next compute has passed
-        bool moved = true;
-        int64_t done = 0;
-        while (moved) {
-          moved = false;
-          done = 0;
-          for (int64_t w = 0; w < nw; ++w) {
-            const StreamWave& sw = pp.stream[w0 + w];
-            const int nbr = sw.nbr & ~kStreamSingleRun;
-            const PairRec* R = pp.recs.data() + sw.base;
-            const int64_t n = sw.npairs;
-            if (comp[w] >= n) { pub[w] = n; ++done; continue; }
-            if (!gated[w]) {
-              // the gate before computing pair comp: prologue (comp == 0) or pair comp - 1 + D
-              const int64_t p = comp[w] == 0 ? std::min<int64_t>(D, n) - 1 : comp[w] - 1 + D;
-              if (p >= n || static_cast<int64_t>(R[p].need) <= pub[nbr]) { gated[w] = 1; moved = true; }
-              else { pub[w] = std::max(pub[w], comp[w]); continue; }
-            }
-            ++comp[w];
-            gated[w] = 0;
-            pub[w] = std::max(pub[w], comp[w] - D);
-            moved = true;
-          }
-        }
-        if (done != nw) {
-          std::printf("DEADLOCK sm %d: %lld of %lld waves done\n", sm, (long long)done, (long long)nw);
-          for (int64_t w = 0; w < nw && w < 16; ++w) {
-            const StreamWave& sw = pp.stream[w0 + w];
-            const int64_t p = comp[w] == 0 ? std::min<int64_t>(D, sw.npairs) - 1 : comp[w] - 1 + D;
-            std::printf("  wave %lld nbr %d computed %lld/%d gate pair %lld need %u pub(nbr) %lld\n", (long long)w,
-                        sw.nbr & ~kStreamSingleRun, (long long)comp[w], sw.npairs, (long long)p,
-                        p < sw.npairs ? pp.recs[sw.base + p].need : 0u, (long long)pub[sw.nbr & ~kStreamSingleRun]);
-          }
-        }
-      }
-    }
-    if (const char* dw = std::getenv("PROBE_DUMP")) {  // "wave,from,to": per pair need and flags
-      int w = 0, a0 = 0, a1 = 0;
-      std::sscanf(dw, "%d,%d,%d", &w, &a0, &a1);
-      const StreamWave& sw = pp.stream[w];
-      std::printf("wave %d: %d pairs, nbr %d\n", w, sw.npairs, sw.nbr & ~kStreamSingleRun);
-      for (int x = a0; x < a1 && x < sw.npairs; ++x) {
-        const PairRec& r = pp.recs[sw.base + x];
-        std::printf("  pair %d need %u flags %08x ua %08x ub %08x\n", x, r.need, r.flags, r.ua, r.ub);
-      }
-    }
-    const double t_mixed = argc > 7 ? std::atof(argv[7]) : 250.0, t_run = argc > 8 ? std::atof(argv[8]) : 127.0;
-    double total_us = 0;
-    for (int sm = 0; sm < nb; ++sm) {
-      double worst = 0;
-      int64_t singles = 0, sum = 0, n = 0;
-      for (int64_t w = pp.sys_off[sm]; w < pp.sys_off[sm + 1]; ++w) {
-        const StreamWave& sw = pp.stream[w];
-        const bool single = sw.nbr & kStreamSingleRun;
-        singles += single;
-        sum += sw.npairs;
-        ++n;
-        worst = std::max(worst, sw.npairs * (single ? t_run : t_mixed) * 1e-3);
-      }
-      total_us += worst;
-      std::printf("sm %d waves %lld singles %lld mean pairs %.0f longest wave %.1f us\n", sm, (long long)n,
-                  (long long)singles, n ? double(sum) / n : 0.0, worst);
-    }
-    std::printf("modelled epoch (longest wave per superstep, no hand-off cost) %.2f ms\n", total_us * 1e-3);
-    return 0;
-  }
   const auto Gb = choose_block_groups(rb, I, nb, 0, waves);
   std::printf("block groups %.3f s\n", lap());
   FastPlan fp;

@@ -25,6 +25,10 @@ def main():
     ap.add_argument("--fast-waves", type=int, default=0,
                     help="fast mode, -G: uniform groups; the reference is then an in-process context with one "
                          "virtual shard per rank (same plan), compared bitwise")
+    ap.add_argument("--k", type=int, default=32, help="rank (64 / 128 / 256: the pair sweep, whose ring overlaps)")
+    ap.add_argument("--staged", action="store_true",
+                    help="prepare + run + evaluate with no sync in between (the JNI dsgdPrepare / dsgdRun path): "
+                         "evaluation must wait for the last superstep's overlapped launch and ring step itself")
     a = ap.parse_args()
     import torch.distributed as dist
     import mfhip
@@ -41,14 +45,18 @@ def main():
     data = mfhip.synth.generate(3000, 800, 60000)
     (tu, ti, tr), (eu, ei, er) = data.split()
     p = L.default_params()
-    p.num_factors, p.num_blocks, p.iterations, p.seed, p.has_seed = 32, a.blocks, 3, 5, 1
+    p.num_factors, p.num_blocks, p.iterations, p.seed, p.has_seed = a.k, a.blocks, 3, 5, 1
     p.mode = L.MODE_DETERMINISTIC_F64 if a.mode == "det" else L.MODE_FAST_F32
     p.fast_waves = a.fast_waves
     obj = [mfhip.Context.unique_id() if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0)
     dev = local % max(1, mfhip.device_count())
     ctx = mfhip.Context(p, rank=(dev, world, rank, obj[0]))
-    ctx.fit(tu, ti, tr)
+    if a.staged:
+        ctx.prepare(tu, ti, tr)
+        ctx.run(p.iterations * p.num_blocks)  # asynchronous: rmse / factors right behind it
+    else:
+        ctx.fit(tu, ti, tr)
     rm, cnt = ctx.rmse(eu, ei, er)
     uids, uf = ctx.factors(L.SIDE_USER)
     iids, itf = ctx.factors(L.SIDE_ITEM)

@@ -20,7 +20,7 @@ d = synth.generate(int(nu * scale), int(ni * scale), int(nr * scale))
 p = L.default_params()
 p.num_factors, p.num_blocks, p.seed, p.has_seed, p.iterations = k, nb, 0, 1, epochs
 p.mode = L.MODE_FAST_F32
-p.fast_item_split = split
+os.environ["MFHIP_ITEM_SPLIT"] = str(split)
 ctx = mfhip.Context(p)
 ctx.prepare(tu, ti, tr)
 for e in range(epochs):
