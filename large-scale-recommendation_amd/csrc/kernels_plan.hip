@@ -775,7 +775,7 @@ void device_fast_schedule(hipStream_t st, const DevRatingBlocks& dr, const Ratin
   const int32_t nb = rb.n_blocks;
   const int64_t nb2 = static_cast<int64_t>(nb) * nb;
   const int64_t n = dr.total;
-  MF_REQUIRE(n == rb.start[nb2] && n < (int64_t{1} << 31), "device schedule: rating blocks do not match");
+  MF_REQUIRE(n > 0 && n == rb.start[nb2] && n < (int64_t{1} << 31), "device schedule: rating blocks do not match (or none)");
   PlanBlocks pb;
   std::vector<int64_t> uoffb(nb2, 0), ioffb(nb2, 0), cbase(nb2, 0);
   std::vector<int32_t> Gblk(nb2, 1);

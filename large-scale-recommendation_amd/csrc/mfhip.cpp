@@ -1167,8 +1167,10 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
     // the per-cell emission and the pair records on the device (kernels_plan.hip) for the default
     // systolic pair sweep of one shard; MFHIP_DEVICE_PLAN=0 keeps them on the host
     const char* dpv = std::getenv("MFHIP_DEVICE_PLAN");
+    // (a rank whose user blocks hold no rating -- the reference's blocking can leave a block
+    // empty -- plans on the host: its schedule is empty)
     const bool dev_plan = ctx->fast_pair && ctx->fast_sys && ctx->item_split == 0 &&
-                          ctx->shards.size() == 1 && !(dpv && std::string(dpv) == "0");
+                          ctx->shards.size() == 1 && ctx->rb.start[nb2] > 0 && !(dpv && std::string(dpv) == "0");
     std::vector<FastBlockWork> entries;
     PairPlan dev_pp;
     DevBuf dev_pairs;

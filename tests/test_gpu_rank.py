@@ -18,11 +18,15 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("mode,extra", [("fast", ["--fast-waves", "-8", "--k", "64"]), ("det", [])])
+@pytest.mark.parametrize("mode,extra", [
+    ("fast", ["--fast-waves", "-8", "--k", "64"]),                       # rank 0 holds no rating
+    ("fast", ["--fast-waves", "-8", "--k", "128", "--users", "30000"]),  # both ranks sweep, ring overlap
+    ("det", []),
+    ("det", ["--users", "30000"])])
 def test_rank_mode_staged_eval_matches_single_context(mode, extra):
     env = dict(os.environ, MFHIP_FAKE_HOSTS="1", MFHIP_DEVICE_SHARERS="2", NCCL_DEBUG="WARN",
                MFHIP_RING_OVERLAP="1")
-    port = 29611 if mode == "fast" else 29612
+    port = 29611 + len(extra) + (10 if mode == "det" else 0)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "tools", "rank_check.py"),
            "--mode", mode, "--blocks", "4", "--staged"] + extra

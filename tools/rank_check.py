@@ -25,6 +25,9 @@ def main():
     ap.add_argument("--fast-waves", type=int, default=0,
                     help="fast mode, -G: uniform groups; the reference is then an in-process context with one "
                          "virtual shard per rank (same plan), compared bitwise")
+    ap.add_argument("--users", type=int, default=3000,
+                    help="distinct users (3000: the reference's blocking puts every user into 2 of 4 blocks, so "
+                         "one of 2 ranks holds no rating -- the empty-rank edge)")
     ap.add_argument("--k", type=int, default=32, help="rank (64 / 128 / 256: the pair sweep, whose ring overlaps)")
     ap.add_argument("--staged", action="store_true",
                     help="prepare + run + evaluate with no sync in between (the JNI dsgdPrepare / dsgdRun path): "
@@ -42,7 +45,7 @@ def main():
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     local = int(os.environ.get("LOCAL_RANK", rank))
-    data = mfhip.synth.generate(3000, 800, 60000)
+    data = mfhip.synth.generate(a.users, 800, 60000)
     (tu, ti, tr), (eu, ei, er) = data.split()
     p = L.default_params()
     p.num_factors, p.num_blocks, p.iterations, p.seed, p.has_seed = a.k, a.blocks, 3, 5, 1
