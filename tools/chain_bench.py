@@ -42,7 +42,7 @@ def run(u, i, groups, label, kern):
 
 
 users = np.arange(n, dtype=np.int32)
-for kern in ("substep", "persistent"):
+for kern in ("substep",):
     run(users, np.zeros(n, np.int32), 1, "chain (1 item, 1 wave)", kern)
     run(users, (users // 64).astype(np.int32), 1, "runs of 64 (1 wave)", kern)
     rng = np.random.default_rng(0)

@@ -36,7 +36,7 @@ def run(H, B, groups, kern, nb=1):
     ctx.close()
 
 
-for kern in ("substep", "persistent"):
+for kern in ("substep",):
     run(20000, 0, 64, kern)
     run(20000, 200000, 64, kern)
     run(20000, 2000000, 64, kern)

@@ -35,4 +35,16 @@ for sm in np.unique(a[:, 1]):
     xm = waves[int(np.argmax(per_wave))]
     print(f"superstep {sm}: span {span / 1e3:.0f} us, busiest wave {xm} busy {max(per_wave) / 1e3:.0f} us "
           f"({int(w[w[:, 3] == xm, 4].sum())} pairs), median wave busy {np.median(per_wave) / 1e3:.0f} us")
+    # the busiest wave's time split: in cells (fixed cost + pairs) and between cells (hand-off waits)
+    c = w[w[:, 3] == xm]
+    c = c[np.argsort(c[:, 2])]
+    d = (c[:, 7] - c[:, 6]) * 10.0
+    g = (c[1:, 6] - c[:-1, 7]) * 10.0
+    pairs = c[:, 4].sum()
+    nz = c[:, 4] > 0
+    fit = np.linalg.lstsq(np.stack([np.ones(nz.sum()), c[nz, 4]], 1), d[nz], rcond=None)[0] if nz.sum() > 2 else [0, 0]
+    print(f"    busiest wave: {len(c)} cells (kinds {sorted(set(c[:, 5].tolist()))}), first start +"
+          f"{(c[0, 6] - w[:, 6].min()) * 10.0 / 1e3:.1f} us, in cells {d.sum() / 1e3:.0f} us = {d.sum() / max(pairs, 1):.0f} "
+          f"ns/pair (fit: {fit[0]:.0f} ns/cell + {fit[1]:.1f} ns/pair), between cells {g.sum() / 1e3:.0f} us "
+          f"(median {np.median(g) if len(g) else 0:.0f} ns)")
 print(f"sum of superstep spans {tot / 1e6:.2f} ms")
