@@ -219,7 +219,7 @@ template <int KPL, int D>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_sweep_pair_sys(
     const SysWave* __restrict__ sw, const WaveDesc* __restrict__ sys, int nw, int lbase, const u4v* __restrict__ recs,
     float* __restrict__ U, float* __restrict__ I, uint64_t u_bytes, uint64_t i_bytes, float eta,
-    int32_t* __restrict__ prog, uint32_t base, int32_t* __restrict__ err, uint64_t* __restrict__ trace) {
+    int32_t* __restrict__ prog, uint32_t base, int32_t* __restrict__ err, uint64_t* __restrict__ trace, int prio) {
   const int lane = threadIdx.x;
   // blocks b and b+8 share an XCD: give each XCD a contiguous range of waves, so most hand-offs
   // (g+1 -> g) stay inside one L2 (speed only; correctness does not depend on it).  XCD x holds
@@ -232,8 +232,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   const SysWave w = sw[L];
   const WaveDesc* my = sys + w.cell0;
   int32_t* my_prog = prog + static_cast<int64_t>(lbase + L) * kProgStride;
-  int32_t* nb_prog = prog + static_cast<int64_t>(w.nbr) * kProgStride;
+  int32_t* nb_prog = prog + static_cast<int64_t>(w.nbr & ~kSysCritical) * kProgStride;
   const __amdgpu_buffer_rsrc_t urs = raw_rsrc(U, u_bytes), irs = raw_rsrc(I, i_bytes);
+  // issue priority on the critical path (MFHIP_HOT_PRIO): 1 = single-run cells, 2 = the superstep's
+  // busiest wave; VALU issue between two waves of a SIMD goes by priority, then age
+  if (prio == 2 && (w.nbr & kSysCritical)) __builtin_amdgcn_s_setprio(3);
   for (int t = 0; t < w.G; ++t) {
     const WaveDesc d = my[t];
     if (t > 0 && w.G > 1) {
@@ -254,15 +257,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
       }
     }
     const uint64_t c_start = __builtin_amdgcn_s_memrealtime();
+    const uint64_t c_clk = trace ? __builtin_amdgcn_s_memtime() : 0;
+    const bool hot = prio == 1 && d.cells == kWaveSingleRun;
+    if (hot) __builtin_amdgcn_s_setprio(3);
     if (d.steps > 0) pair_cell<KPL, D, kSC1>(d, recs, urs, irs, eta, lane);
+    if (hot) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): every user-row store of this wave has landed
     if (lane == 0)
       __hip_atomic_store(my_prog, static_cast<int32_t>(base + static_cast<uint32_t>(t) + 1u), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
-    if (trace && lane == 0) {
-      uint64_t* tr = trace + 2 * (w.cell0 + t);
+    if (trace && lane == 0) {  // {start, end} on the 100 MHz clock, then the shader clock (s_memtime)
+      uint64_t* tr = trace + 4 * (w.cell0 + t);
       tr[0] = c_start;
       tr[1] = __builtin_amdgcn_s_memrealtime();
+      tr[2] = c_clk;
+      tr[3] = __builtin_amdgcn_s_memtime();
     }
   }
 }
@@ -278,10 +287,10 @@ void dispatch(hipStream_t st, const WaveDesc* waves, int nwaves, const PairRec* 
 template <int KPL>
 void dispatch_sys(hipStream_t st, const SysWave* sw, const WaveDesc* sys, int nw, int lbase, const PairRec* recs,
                   float* U, float* I, uint64_t ub, uint64_t ib, float eta, int32_t* prog, uint32_t base, int32_t* err,
-                  uint64_t* trace, hipEvent_t ev0, hipEvent_t ev1) {
+                  uint64_t* trace, hipEvent_t ev0, hipEvent_t ev1, int prio) {
   hipExtLaunchKernelGGL((k_sweep_pair_sys<KPL, kPairRing>), dim3(static_cast<unsigned>(nw)), dim3(64), 0, st, ev0, ev1,
                         0, sw, sys, nw, lbase, reinterpret_cast<const u4v*>(recs), U, I, ub, ib, eta, prog, base, err,
-                        trace);
+                        trace, prio);
 }
 
 template <int KPL>
@@ -309,9 +318,10 @@ int sweep_pair_sys_capacity(int k) {
 
 void launch_sweep_pair_sys(hipStream_t st, const SysWave* sw, const WaveDesc* sys, int nw, int lbase,
                            const PairRec* recs, float* U, float* I, uint64_t u_bytes, uint64_t i_bytes, int k, float eta,
-                           int32_t* prog, uint32_t base, int32_t* err, uint64_t* trace, hipEvent_t ev0, hipEvent_t ev1) {
+                           int32_t* prog, uint32_t base, int32_t* err, uint64_t* trace, hipEvent_t ev0, hipEvent_t ev1,
+                           int prio) {
   if (nw <= 0) return;
-#define MF_SYS(KPL) dispatch_sys<KPL>(st, sw, sys, nw, lbase, recs, U, I, u_bytes, i_bytes, eta, prog, base, err, trace, ev0, ev1)
+#define MF_SYS(KPL) dispatch_sys<KPL>(st, sw, sys, nw, lbase, recs, U, I, u_bytes, i_bytes, eta, prog, base, err, trace, ev0, ev1, prio)
   switch (k) {
     case 64: MF_SYS(1); break;
     case 128: MF_SYS(2); break;

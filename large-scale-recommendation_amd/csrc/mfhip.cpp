@@ -147,6 +147,7 @@ struct mf_ctx {
   // MFHIP_ITEM_SPLIT=m sweeps an item with more than m ratings in one rating block as ceil(r / m)
   // chains averaged when the superstep ends (read at prepare; 0 / unset = off)
   int32_t item_split = 0;
+  int32_t hot_prio = 0;  // MFHIP_HOT_PRIO (experiment): raised issue priority on the critical path
   std::vector<int64_t> fast_rb_size;  // per rating block (fast mode)
   mf_stats stats{};
   bool profiling = false;
@@ -376,6 +377,8 @@ void collect_profile(mf_ctx* ctx) {
 
 // MFHIP_WAVE_TRACE=<file>: per wave of the per-cell schedules "shard sm t wave steps cells start
 // end" (100 MHz clock) of the last time every sub-step ran; written when the context is destroyed.
+// The systolic sweep adds a 9th column: the cell's shader-clock cycles (s_memtime), so the clock
+// the wave actually ran at is cycles / ((end - start) x 10 ns).
 void dump_wave_trace(mf_ctx* ctx) {
   const char* path = std::getenv("MFHIP_WAVE_TRACE");
   if (!path) return;
@@ -383,7 +386,7 @@ void dump_wave_trace(mf_ctx* ctx) {
   for (auto& s : ctx->shards) {
     if (s.st_trace.get() && !s.st_sys_host.empty()) {  // systolic: one row per cell, wave = index in superstep
       DeviceGuard g(s.device);
-      std::vector<uint64_t> tr(s.st_sys_host.size() * 2);
+      std::vector<uint64_t> tr(s.st_sys_host.size() * 4);
       MF_HIP(hipMemcpy(tr.data(), s.st_trace.get(), tr.size() * 8, hipMemcpyDeviceToHost));
       if (!f) f = std::fopen(path, "w");
       if (!f) return;
@@ -392,9 +395,9 @@ void dump_wave_trace(mf_ctx* ctx) {
           const SysWave& sw = s.st_sysw_host[w];
           for (int32_t t = 0; t < sw.G; ++t) {
             const int64_t x = sw.cell0 + t;
-            std::fprintf(f, "%d %d %d %lld %d %d %llu %llu\n", s.index, sm, t, (long long)(w - s.st_sys_off[sm]),
-                         s.st_sys_host[x].steps, s.st_sys_host[x].cells, (unsigned long long)tr[2 * x],
-                         (unsigned long long)tr[2 * x + 1]);
+            std::fprintf(f, "%d %d %d %lld %d %d %llu %llu %llu\n", s.index, sm, t, (long long)(w - s.st_sys_off[sm]),
+                         s.st_sys_host[x].steps, s.st_sys_host[x].cells, (unsigned long long)tr[4 * x],
+                         (unsigned long long)tr[4 * x + 1], (unsigned long long)(tr[4 * x + 3] - tr[4 * x + 2]));
           }
         }
       continue;
@@ -631,7 +634,7 @@ void fast_superstep(mf_ctx* ctx, Shard& s, int64_t superstep, double eta) {
                             static_cast<int>(a), s.st_recs.as<PairRec>(), s.uf.as<float>(), s.itf.as<float>(),
                             s.uf.bytes(), s.itf.bytes(), ctx->P.num_factors, static_cast<float>(eta),
                             s.fast_prog.as<int32_t>(), s.sys_base, s.fast_err.as<int32_t>(),
-                            s.st_trace.get() ? s.st_trace.as<uint64_t>() : nullptr, tm.start(), tm.stop());
+                            s.st_trace.get() ? s.st_trace.as<uint64_t>() : nullptr, tm.start(), tm.stop(), ctx->hot_prio);
       ctx->stats.kernel_launches += 1;
     };
     if (ctx->ring_overlap) {
@@ -1063,6 +1066,8 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
   PhaseClock clk;
   ctx->item_split = 0;
   if (const char* v = std::getenv("MFHIP_ITEM_SPLIT")) ctx->item_split = std::max(0, std::atoi(v));
+  ctx->hot_prio = 0;
+  if (const char* v = std::getenv("MFHIP_HOT_PRIO")) ctx->hot_prio = std::atoi(v);
   ctx->reaper.join();
   DevRatingBlocks dev_rb;  // the device copy of the rating blocks (full device schedule only)
   ctx->nb = std::max(1, ctx->P.num_blocks);
@@ -1286,6 +1291,15 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
           s.st_sys.alloc(std::max<size_t>(pp.sys.size(), 1) * sizeof(WaveDesc));
           if (!pp.sys.empty())
             MF_HIP(hipMemcpy(s.st_sys.get(), pp.sys.data(), pp.sys.size() * sizeof(WaveDesc), hipMemcpyHostToDevice));
+          for (int32_t sm = 0; sm < ctx->nb; ++sm) {  // each superstep's busiest wave (kSysCritical)
+            int64_t best = -1, most = -1;
+            for (int64_t w = pp.sys_off[sm]; w < pp.sys_off[sm + 1]; ++w) {
+              int64_t pairs = 0;
+              for (int32_t t = 0; t < pp.sys_waves[w].G; ++t) pairs += pp.sys[pp.sys_waves[w].cell0 + t].steps;
+              if (pairs > most) { most = pairs; best = w; }
+            }
+            if (best >= 0) pp.sys_waves[best].nbr |= kSysCritical;
+          }
           s.st_sysw.alloc(std::max<size_t>(pp.sys_waves.size(), 1) * sizeof(SysWave));
           if (!pp.sys_waves.empty())
             MF_HIP(hipMemcpy(s.st_sysw.get(), pp.sys_waves.data(), pp.sys_waves.size() * sizeof(SysWave),
@@ -1304,8 +1318,9 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
         ctx->reaper.drop(pp.recs);
         if (std::getenv("MFHIP_WAVE_TRACE")) {
           const size_t n = ctx->fast_sys ? pp.sys.size() : pp.waves.size();
-          s.st_trace.alloc(std::max<size_t>(n, 1) * 16);
-          MF_HIP(hipMemset(s.st_trace.get(), 0, std::max<size_t>(n, 1) * 16));
+          const size_t per = ctx->fast_sys ? 32 : 16;  // systolic: realtime and shader-clock stamps
+          s.st_trace.alloc(std::max<size_t>(n, 1) * per);
+          MF_HIP(hipMemset(s.st_trace.get(), 0, std::max<size_t>(n, 1) * per));
           if (ctx->fast_sys) {
             s.st_sys_host = pp.sys;
             s.st_sysw_host = pp.sys_waves;

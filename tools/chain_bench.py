@@ -17,9 +17,12 @@ from mfhip import _lib as L
 
 k = int(sys.argv[1]) if len(sys.argv) > 1 else 128
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 100000
+only = sys.argv[3] if len(sys.argv) > 3 else ""  # run only cases whose label starts with this
 
 
 def run(u, i, groups, label, kern):
+    if only and not label.startswith(only):
+        return
     os.environ["MFHIP_FAST_KERNEL"] = kern
     p = L.default_params()
     p.num_factors, p.num_blocks, p.mode, p.fast_waves, p.iterations = k, 1, L.MODE_FAST_F32, -groups, 1

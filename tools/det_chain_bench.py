@@ -1,0 +1,38 @@
+"""Per-update latency of the deterministic f64 sweep (k_det_sweep) on its critical path: one hot
+item, n distinct users, one rating block (nb=1) -- a single wave applying n chained updates
+(DSGDforMF.scala:395-415 in the reference's shuffled order).  Optional background ratings on other
+items (other waves, B of them) show the in-situ cost beside a loaded chip.
+
+    python tools/det_chain_bench.py [k] [n] [background]
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "large-scale-recommendation_amd"))
+import numpy as np
+
+import mfhip
+from mfhip import _lib as L
+
+k = int(sys.argv[1]) if len(sys.argv) > 1 else 128
+n = int(sys.argv[2]) if len(sys.argv) > 2 else 30000
+bg = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+
+rng = np.random.default_rng(5)
+nu = max(n, bg // 8 + 1)
+u = np.concatenate([rng.permutation(nu)[:n], rng.integers(0, nu, bg)]).astype(np.int32)
+i = np.concatenate([np.zeros(n, np.int32), rng.integers(1, 20000, bg).astype(np.int32)])
+p = L.default_params()
+p.num_factors, p.num_blocks, p.mode, p.iterations, p.seed = k, 1, L.MODE_DETERMINISTIC_F64, 1, 0
+with mfhip.Context(p) as ctx:
+    ctx.prepare(u, i, np.full(len(u), 3.0))
+    ctx.run(1)
+    ctx.sync()
+    ctx.reset_stats()
+    ctx.set_profiling(True)
+    ctx.run(3)
+    ctx.sync()
+    st = ctx.stats()
+per = st["kernel_ms"] / 3
+print(f"det chain k={k} hot={n} background={bg}: superstep {per:.3f} ms, {per * 1e6 / n:.1f} ns per hot update, "
+      f"launches {st['kernel_launches']}", flush=True)

@@ -6,8 +6,9 @@ import sys
 
 import numpy as np
 
-a = np.loadtxt(sys.argv[1], dtype=np.int64)
+a = np.loadtxt(sys.argv[1], dtype=np.int64, ndmin=2)
 a = a[a[:, 6] > 0]
+clk = a.shape[1] > 8  # 9th column: shader-clock cycles of the cell (s_memtime)
 dur = (a[:, 7] - a[:, 6]) * 10.0
 for kind in (1, 2):
     m = (a[:, 5] == kind) & (a[:, 4] > 0)
@@ -46,5 +47,8 @@ for sm in np.unique(a[:, 1]):
     print(f"    busiest wave: {len(c)} cells (kinds {sorted(set(c[:, 5].tolist()))}), first start +"
           f"{(c[0, 6] - w[:, 6].min()) * 10.0 / 1e3:.1f} us, in cells {d.sum() / 1e3:.0f} us = {d.sum() / max(pairs, 1):.0f} "
           f"ns/pair (fit: {fit[0]:.0f} ns/cell + {fit[1]:.1f} ns/pair), between cells {g.sum() / 1e3:.0f} us "
-          f"(median {np.median(g) if len(g) else 0:.0f} ns)")
+          f"(median {np.median(g) if len(g) else 0:.0f} ns)"
+          + (f", shader clock {c[:, 8].sum() / max(d.sum(), 1):.2f} GHz vs all waves "
+             f"{w[:, 8].sum() / max(((w[:, 7] - w[:, 6]) * 10.0).sum(), 1):.2f} GHz, {c[:, 8].sum() / max(pairs, 1):.0f} "
+             f"cycles/pair" if clk else ""))
 print(f"sum of superstep spans {tot / 1e6:.2f} ms")
