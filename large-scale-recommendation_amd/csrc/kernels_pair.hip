@@ -30,6 +30,9 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <string>
+
 #include "kernels.hpp"
 
 namespace mfhip {
@@ -38,19 +41,22 @@ namespace {
 #include "pair_device.hpp"
 
 // One cell (WaveDesc d) of the pair schedule, swept by the calling wave.  UP = cache policy of
-// the user-row loads and stores.
+// the user-row loads and stores.  L0 / L1: the cell's first two record chunks, loaded by the
+// caller (the systolic sweep loads them while the previous cell's stores drain).
 template <int KPL, int D, int UP>
-__device__ __forceinline__ void pair_cell(const WaveDesc d, const u4v* __restrict__ recs, __amdgpu_buffer_rsrc_t urs,
+__device__ __forceinline__ void pair_cell(const WaveDesc d, const ChunkRaw& L0, const ChunkRaw& L1,
+                                          const u4v* __restrict__ recs, __amdgpu_buffer_rsrc_t urs,
                                           __amdgpu_buffer_rsrc_t irs, float eta, int lane) {
   constexpr int NV = Row<KPL>::NV;
   constexpr int CH = kPairChunk;
   static_assert(CH % D == 0, "ring slots must repeat every chunk");
   const int npairs = d.steps;
-  const u4v* R = recs + 4 * d.base;
+  const __amdgpu_buffer_rsrc_t RR = cell_records(recs, d.base, npairs);
+  const uint32_t vlane = static_cast<uint32_t>(lane) * 64u;
   const uint32_t voff = static_cast<uint32_t>(lane) * KPL * 4u;
 
-  Chunk C0 = chunk_convert(chunk_load(R, 0, npairs, lane), eta);  // current chunk
-  ChunkRaw C1 = chunk_load(R, 1, npairs, lane);                     // next chunk, as loaded
+  Chunk C0 = chunk_convert(L0, eta);  // current chunk
+  ChunkRaw C1 = L1;                   // next chunk, as loaded
   Row<KPL> plA, plB;  // the previous pair's updated user rows (forwarding)
 #pragma unroll
   for (int e = 0; e < NV; ++e) plA.v[e] = plB.v[e] = f2{0.f, 0.f};
@@ -107,7 +113,7 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const u4v* __restric
         RB[slot] = ld<KPL, UP>(urs, voff, ob[slot]);
       }
       C0 = chunk_convert(C1, eta);
-      C1 = chunk_load(R, c + 2, npairs, lane);
+      C1 = chunk_load(RR, c + 2, vlane);
     }
   run_done:
     st<KPL>(irs, voff, item_off, q);
@@ -184,7 +190,7 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const u4v* __restric
         QB[slot] = ld<KPL>(irs, voff, nib);
       }
       C0 = chunk_convert(C1, eta);
-      C1 = chunk_load(R, c + 2, npairs, lane);
+      C1 = chunk_load(RR, c + 2, vlane);
     }
 #undef MF_PREFETCH
   }
@@ -196,7 +202,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     const WaveDesc* __restrict__ waves, const u4v* __restrict__ recs, float* __restrict__ U, float* __restrict__ I,
     uint64_t u_bytes, uint64_t i_bytes, float eta, uint64_t* __restrict__ trace) {
   const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-  pair_cell<KPL, D, 0>(waves[blockIdx.x], recs, raw_rsrc(U, u_bytes), raw_rsrc(I, i_bytes), eta, threadIdx.x);
+  const WaveDesc d = waves[blockIdx.x];
+  const __amdgpu_buffer_rsrc_t rr = cell_records(recs, d.base, d.steps);
+  const uint32_t vlane = threadIdx.x * 64u;
+  pair_cell<KPL, D, 0>(d, chunk_load(rr, 0, vlane), chunk_load(rr, 1, vlane), recs, raw_rsrc(U, u_bytes),
+                       raw_rsrc(I, i_bytes), eta, threadIdx.x);
   if (trace && threadIdx.x == 0) {
     trace[2 * blockIdx.x] = t_start;
     trace[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
@@ -215,7 +225,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
 // agent-scope relaxed loads (sc1).  Progress words are monotonic across launches (base), so
 // they are never reset.  Every wave must be resident at once (the host checks occupancy); a
 // poll that exceeds ~1 s sets err[0] and the wave gives up (the host then fails loudly).
-template <int KPL, int D>
+// PRE: the next cell's first two record chunks and the neighbour's progress word are loaded right
+// after a cell's last stores are issued, so they arrive while those stores drain (vmcnt(9) waits
+// for the stores only): a cell no longer starts with a record fetch and a progress poll on its
+// critical path (an empty cell's, or past the last cell the last cell's again: loaded, unused).
+template <int KPL, int D, bool PRE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_sweep_pair_sys(
     const SysWave* __restrict__ sw, const WaveDesc* __restrict__ sys, int nw, int lbase, const u4v* __restrict__ recs,
     float* __restrict__ U, float* __restrict__ I, uint64_t u_bytes, uint64_t i_bytes, float eta,
@@ -237,9 +251,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   // issue priority on the critical path (MFHIP_HOT_PRIO): 1 = single-run cells, 2 = the superstep's
   // busiest wave; VALU issue between two waves of a SIMD goes by priority, then age
   if (prio == 2 && (w.nbr & kSysCritical)) __builtin_amdgcn_s_setprio(3);
+  const uint32_t vlane = static_cast<uint32_t>(lane) * 64u;
+  auto first_chunks = [&](const WaveDesc& c, ChunkRaw& A, ChunkRaw& B) {  // an empty cell reads nothing
+    const __amdgpu_buffer_rsrc_t rr = cell_records(recs, c.base, c.steps);
+    A = chunk_load(rr, 0, vlane);
+    B = chunk_load(rr, 1, vlane);
+  };
+  WaveDesc d = my[0];
+  ChunkRaw L0, L1;
+  if (PRE) first_chunks(d, L0, L1);
+  int32_t pv = 0;  // PRE: the neighbour's progress word as read during the previous cell's drain
   for (int t = 0; t < w.G; ++t) {
-    const WaveDesc d = my[t];
-    if (t > 0 && w.G > 1) {
+    const WaveDesc dn = my[t + 1 < w.G ? t + 1 : t];  // scalar load, used after this cell
+    if (t > 0 && w.G > 1 &&
+        !(PRE && static_cast<int32_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(pv)) -
+                                      (base + static_cast<uint32_t>(t))) >= 0)) {
       const uint32_t want = base + static_cast<uint32_t>(t);
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       for (;;) {
@@ -260,9 +286,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     const uint64_t c_clk = trace ? __builtin_amdgcn_s_memtime() : 0;
     const bool hot = prio == 1 && d.cells == kWaveSingleRun;
     if (hot) __builtin_amdgcn_s_setprio(3);
-    if (d.steps > 0) pair_cell<KPL, D, kSC1>(d, recs, urs, irs, eta, lane);
+    if (!PRE && d.steps > 0) first_chunks(d, L0, L1);
+    if (d.steps > 0) pair_cell<KPL, D, kSC1>(d, L0, L1, recs, urs, irs, eta, lane);
     if (hot) __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): every user-row store of this wave has landed
+    if (PRE) {
+      first_chunks(dn, L0, L1);
+      pv = __hip_atomic_load(nb_prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_s_waitcnt(0x0F79);  // vmcnt(9): the 9 loads above may fly, every older store has landed
+    } else {
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): every user-row store of this wave has landed
+    }
     if (lane == 0)
       __hip_atomic_store(my_prog, static_cast<int32_t>(base + static_cast<uint32_t>(t) + 1u), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
@@ -273,6 +306,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
       tr[2] = c_clk;
       tr[3] = __builtin_amdgcn_s_memtime();
     }
+    d = dn;
   }
 }
 
@@ -284,13 +318,24 @@ void dispatch(hipStream_t st, const WaveDesc* waves, int nwaves, const PairRec* 
                         0, waves, reinterpret_cast<const u4v*>(recs), U, I, ub, ib, eta, trace);
 }
 
+// MFHIP_CELL_PRELOAD=0: the cell's records and the progress poll at the cell's start (A/B)
+bool cell_preload() {
+  static const bool on = [] { const char* v = std::getenv("MFHIP_CELL_PRELOAD"); return !(v && std::string(v) == "0"); }();
+  return on;
+}
+
 template <int KPL>
 void dispatch_sys(hipStream_t st, const SysWave* sw, const WaveDesc* sys, int nw, int lbase, const PairRec* recs,
                   float* U, float* I, uint64_t ub, uint64_t ib, float eta, int32_t* prog, uint32_t base, int32_t* err,
                   uint64_t* trace, hipEvent_t ev0, hipEvent_t ev1, int prio) {
-  hipExtLaunchKernelGGL((k_sweep_pair_sys<KPL, kPairRing>), dim3(static_cast<unsigned>(nw)), dim3(64), 0, st, ev0, ev1,
-                        0, sw, sys, nw, lbase, reinterpret_cast<const u4v*>(recs), U, I, ub, ib, eta, prog, base, err,
-                        trace, prio);
+  if (cell_preload())
+    hipExtLaunchKernelGGL((k_sweep_pair_sys<KPL, kPairRing, true>), dim3(static_cast<unsigned>(nw)), dim3(64), 0, st,
+                          ev0, ev1, 0, sw, sys, nw, lbase, reinterpret_cast<const u4v*>(recs), U, I, ub, ib, eta, prog,
+                          base, err, trace, prio);
+  else
+    hipExtLaunchKernelGGL((k_sweep_pair_sys<KPL, kPairRing, false>), dim3(static_cast<unsigned>(nw)), dim3(64), 0, st,
+                          ev0, ev1, 0, sw, sys, nw, lbase, reinterpret_cast<const u4v*>(recs), U, I, ub, ib, eta, prog,
+                          base, err, trace, prio);
 }
 
 template <int KPL>
@@ -298,8 +343,11 @@ int sys_capacity() {
   int dev = 0, cus = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sweep_pair_sys<KPL, kPairRing>, 64, 0) != hipSuccess)
+  int a = 0, b = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, k_sweep_pair_sys<KPL, kPairRing, true>, 64, 0) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_sweep_pair_sys<KPL, kPairRing, false>, 64, 0) != hipSuccess)
     return 0;
+  per_cu = std::min(a, b);
   return cus * per_cu;
 }
 

@@ -122,11 +122,22 @@ struct ChunkRaw {
   u4v w0, w1, w2, w3;
 };
 
-__device__ __forceinline__ ChunkRaw chunk_load(const u4v* __restrict__ R, int c, int npairs, int lane) {
-  const int64_t x = min(c * kPairChunk + lane, npairs - 1);
-  // records are read once: non-temporal, so they do not push factor rows out of L2 / MALL
-  return ChunkRaw{__builtin_nontemporal_load(R + 4 * x), __builtin_nontemporal_load(R + 4 * x + 1),
-                  __builtin_nontemporal_load(R + 4 * x + 2), __builtin_nontemporal_load(R + 4 * x + 3)};
+// A cell's pair records as a raw buffer of exactly its records: a lane past the cell's last pair
+// reads zeros (no clamp, no per-cell vector address arithmetic: the cell is an SGPR base and size,
+// the lane a constant voffset), which only the prefetch of rows for pairs past the end consumes.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t cell_records(const u4v* recs, int64_t base, int npairs) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<u4v*>(recs + 4 * base), 0,
+                                           static_cast<uint32_t>(npairs > 0 ? npairs : 0) * 64u, 0x00020000);
+}
+// Chunk c of the cell: pair c * kPairChunk + lane in lane `lane` (vlane = lane * 64).  Records are
+// read once: non-temporal (cache policy nt), so they do not push factor rows out of L2 / MALL.
+__device__ __forceinline__ ChunkRaw chunk_load(__amdgpu_buffer_rsrc_t rr, int c, uint32_t vlane) {
+  const uint32_t so = static_cast<uint32_t>(c) * kPairChunk * 64u;
+  constexpr int kNT = 2;
+  return ChunkRaw{__builtin_amdgcn_raw_buffer_load_b128(rr, vlane, so, kNT),
+                  __builtin_amdgcn_raw_buffer_load_b128(rr, vlane + 16u, so, kNT),
+                  __builtin_amdgcn_raw_buffer_load_b128(rr, vlane + 32u, so, kNT),
+                  __builtin_amdgcn_raw_buffer_load_b128(rr, vlane + 48u, so, kNT)};
 }
 
 __device__ __forceinline__ Chunk chunk_convert(const ChunkRaw& r, float eta) {

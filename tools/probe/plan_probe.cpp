@@ -4,6 +4,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "plan.hpp"
@@ -49,6 +50,45 @@ int main(int argc, char** argv) {
   RatingBlocks rb;
   build_rating_blocks(rb, U, I, u.data(), i.data(), r.data(), n, 0, nb, false);
   std::printf("rating blocks %.3f s\n", lap());
+  if (argc > 5 && std::string(argv[5]) == "scale") {
+    // Strong-scaling model of the systolic sweep on G GPUs (rank mode, n = nb blocks, c = nb / G
+    // user blocks per rank, `waves` resident waves per GPU): per rank and superstep the busiest
+    // wave's single-run / mixed pairs and cells, from the plan mf_dsgd_prepare builds for that
+    // rank.  Printed per G; tools/scaling_model.py turns it into times.
+    for (int G = 1; G <= nb; G *= 2) {
+      if (nb % G) continue;
+      const int c = nb / G;
+      std::vector<int32_t> Gall(static_cast<size_t>(nb) * nb, 0);
+      for (int g = 0; g < G; ++g) {
+        const auto gb = choose_block_groups(rb, I, c, g, waves);
+        for (size_t b = 0; b < gb.size(); ++b) if (gb[b] > 0) Gall[b] = gb[b];
+      }
+      FastPlan fp;
+      build_fast_plan(fp, rb, U, I, 128, k, 1.0, 0 * 0x9E3779B97F4A7C15ULL + 1, static_cast<uint32_t>(U.rows()),
+                      nullptr, 2 * kPairRing, &Gall);
+      for (int g = 0; g < G; ++g) {
+        PairPlan pp;
+        build_pair_plan(pp, fp, nb, c, g, k, false);
+        for (int sm = 0; sm < nb; ++sm) {
+          // every wave of this rank's superstep: cells, single-run pairs, mixed pairs
+          for (int64_t w = pp.sys_off[sm]; w < pp.sys_off[sm + 1]; ++w) {
+            const SysWave& sw = pp.sys_waves[w];
+            int64_t runp = 0, mixp = 0, cells = 0;
+            for (int t = 0; t < sw.G; ++t) {
+              const WaveDesc& d = pp.sys[sw.cell0 + t];
+              if (d.steps == 0) continue;
+              ++cells;
+              (d.cells == kWaveSingleRun ? runp : mixp) += d.steps;
+            }
+            std::printf("SCALE G %d rank %d sm %d wave %lld cells %lld run %lld mix %lld\n", G, g, sm,
+                        (long long)(w - pp.sys_off[sm]), (long long)cells, (long long)runp, (long long)mixp);
+          }
+        }
+      }
+      std::fflush(stdout);
+    }
+    return 0;
+  }
   const auto Gb = choose_block_groups(rb, I, nb, 0, waves);
   std::printf("block groups %.3f s\n", lap());
   FastPlan fp;
