@@ -225,10 +225,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
 // agent-scope relaxed loads (sc1).  Progress words are monotonic across launches (base), so
 // they are never reset.  Every wave must be resident at once (the host checks occupancy); a
 // poll that exceeds ~1 s sets err[0] and the wave gives up (the host then fails loudly).
-// PRE: the next cell's first two record chunks and the neighbour's progress word are loaded right
-// after a cell's last stores are issued, so they arrive while those stores drain (vmcnt(9) waits
-// for the stores only): a cell no longer starts with a record fetch and a progress poll on its
-// critical path (an empty cell's, or past the last cell the last cell's again: loaded, unused).
+// PRE: the next cell's first two record chunks are loaded right after a cell's last stores are
+// issued, so they arrive while those stores drain (vmcnt(8) waits for the stores only): a cell no
+// longer starts with a record fetch on its critical path (an empty cell reads nothing; past the
+// last cell the last cell's records are read again, unused).  The neighbour's progress is polled
+// after the drain, as late as possible (read before the drain it was too often not yet there: an
+// extra poll round trip, ML20M 5.98 vs 5.60 ms per epoch).
 template <int KPL, int D, bool PRE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_sweep_pair_sys(
     const SysWave* __restrict__ sw, const WaveDesc* __restrict__ sys, int nw, int lbase, const u4v* __restrict__ recs,
@@ -260,12 +262,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   WaveDesc d = my[0];
   ChunkRaw L0, L1;
   if (PRE) first_chunks(d, L0, L1);
-  int32_t pv = 0;  // PRE: the neighbour's progress word as read during the previous cell's drain
   for (int t = 0; t < w.G; ++t) {
     const WaveDesc dn = my[t + 1 < w.G ? t + 1 : t];  // scalar load, used after this cell
-    if (t > 0 && w.G > 1 &&
-        !(PRE && static_cast<int32_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(pv)) -
-                                      (base + static_cast<uint32_t>(t))) >= 0)) {
+    if (t > 0 && w.G > 1) {
       const uint32_t want = base + static_cast<uint32_t>(t);
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       for (;;) {
@@ -291,8 +290,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     if (hot) __builtin_amdgcn_s_setprio(0);
     if (PRE) {
       first_chunks(dn, L0, L1);
-      pv = __hip_atomic_load(nb_prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_s_waitcnt(0x0F79);  // vmcnt(9): the 9 loads above may fly, every older store has landed
+      __builtin_amdgcn_s_waitcnt(0x0F78);  // vmcnt(8): the 8 loads above may fly, every older store has landed
     } else {
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): every user-row store of this wave has landed
     }

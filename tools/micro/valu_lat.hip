@@ -9,6 +9,8 @@ constexpr int kIters = 512;
 
 template <int T>
 __global__ void k(float* out, unsigned long long* t, float a) {
+  __shared__ float lds[256];
+  if (T == 17 || T == 18) { for (int x = threadIdx.x; x < 256; x += blockDim.x) lds[x] = 0.f; __syncthreads(); }
   float v0 = threadIdx.x * 1e-3f, v1 = v0 + 1, v2 = v0 + 2, v3 = v0 + 3, v4 = v0 + 4, v5 = v0 + 5, v6 = v0 + 6, v7 = v0 + 7;
   int s = 0;
   const unsigned long long c0 = clock64(), r0 = wall_clock64();
@@ -45,6 +47,18 @@ __global__ void k(float* out, unsigned long long* t, float a) {
       asm volatile(R16("s_nop 1\n\tv_add_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t") : "+v"(v0));
     } else if constexpr (T == 13) {  // ds_swizzle / bpermute chain
       asm volatile(R16("ds_swizzle_b32 %0, %0 offset:swizzle(SWAP,1)\n\ts_waitcnt lgkmcnt(0)\n\t") : "+v"(v0));
+    } else if constexpr (T == 14) {  // dependent v_add_f64
+      asm volatile(R16("v_add_f64 %0, %0, %1\n\t") : "+v"(*(double*)&v0) : "v"(*(double*)&v2));
+    } else if constexpr (T == 15) {  // dependent v_fma_f64
+      asm volatile(R16("v_fma_f64 %0, %0, %1, %2\n\t") : "+v"(*(double*)&v0) : "v"(*(double*)&v2), "v"(*(double*)&v4));
+    } else if constexpr (T == 16) {  // 4 independent v_add_f64 chains
+      asm volatile(R16("v_add_f64 v[20:21], v[20:21], v[28:29]\n\tv_add_f64 v[22:23], v[22:23], v[28:29]\n\tv_add_f64 v[24:25], v[24:25], v[28:29]\n\tv_add_f64 v[26:27], v[26:27], v[28:29]\n\t")
+                   ::: "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27");
+    } else if constexpr (T == 17) {  // LDS broadcast b128 read -> use (latency), address from the data
+      asm volatile(R16("ds_read_b128 v[20:23], %0\n\ts_waitcnt lgkmcnt(0)\n\tv_mov_b32 %0, v20\n\t") : "+v"(s) :: "v20", "v21", "v22", "v23");
+    } else if constexpr (T == 18) {  // 8 independent broadcast b128 reads then wait (throughput)
+      asm volatile(R16("ds_read_b128 v[20:23], %0\n\tds_read_b128 v[24:27], %0 offset:16\n\tds_read_b128 v[28:31], %0 offset:32\n\tds_read_b128 v[32:35], %0 offset:48\n\tds_read_b128 v[36:39], %0 offset:64\n\tds_read_b128 v[40:43], %0 offset:80\n\tds_read_b128 v[44:47], %0 offset:96\n\tds_read_b128 v[48:51], %0 offset:112\n\ts_waitcnt lgkmcnt(0)\n\t")
+                   :: "v"(0) : "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51");
     }
   }
   const unsigned long long c1 = clock64(), r1 = wall_clock64();
@@ -85,6 +99,11 @@ int main() {
   run<8>("4 indep readlanes", 4, 1);
   run<5>("permlane32 swap + add (pair)", 1, 1);
   run<13>("ds_swizzle + wait (pair)", 1, 1);
+  run<14>("dep v_add_f64", 1, 1);
+  run<15>("dep v_fma_f64", 1, 1);
+  run<16>("4 indep v_add_f64", 4, 1);
+  run<17>("ds_read_b128 bcast latency (+mov)", 1, 1);
+  run<18>("8 ds_read_b128 bcast, one wait", 8, 1);
   run<0>("dep v_add_f32", 1, 4);
   run<0>("dep v_add_f32", 1, 8);
   return 0;
