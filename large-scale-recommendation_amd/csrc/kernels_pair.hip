@@ -316,17 +316,22 @@ void dispatch(hipStream_t st, const WaveDesc* waves, int nwaves, const PairRec* 
                         0, waves, reinterpret_cast<const u4v*>(recs), U, I, ub, ib, eta, trace);
 }
 
-// MFHIP_CELL_PRELOAD=0: the cell's records and the progress poll at the cell's start (A/B)
-bool cell_preload() {
-  static const bool on = [] { const char* v = std::getenv("MFHIP_CELL_PRELOAD"); return !(v && std::string(v) == "0"); }();
-  return on;
+// Record preload across the cell boundary (PRE): on for k >= 128 (NFLX 22.49-22.67 vs 22.56-22.81 ms
+// per epoch, A/B/A/B), off for k = 64 (ML20M 5.86-5.98 vs 5.59-5.60 ms: its cells are short and its
+// waves tightly coupled).  MFHIP_CELL_PRELOAD=0/1 overrides (A/B).
+bool cell_preload(int kpl) {
+  static const int env = [] {
+    const char* v = std::getenv("MFHIP_CELL_PRELOAD");
+    return v ? std::atoi(v) : -1;
+  }();
+  return env >= 0 ? env != 0 : kpl >= 2;
 }
 
 template <int KPL>
 void dispatch_sys(hipStream_t st, const SysWave* sw, const WaveDesc* sys, int nw, int lbase, const PairRec* recs,
                   float* U, float* I, uint64_t ub, uint64_t ib, float eta, int32_t* prog, uint32_t base, int32_t* err,
                   uint64_t* trace, hipEvent_t ev0, hipEvent_t ev1, int prio) {
-  if (cell_preload())
+  if (cell_preload(KPL))
     hipExtLaunchKernelGGL((k_sweep_pair_sys<KPL, kPairRing, true>), dim3(static_cast<unsigned>(nw)), dim3(64), 0, st,
                           ev0, ev1, 0, sw, sys, nw, lbase, reinterpret_cast<const u4v*>(recs), U, I, ub, ib, eta, prog,
                           base, err, trace, prio);

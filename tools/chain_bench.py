@@ -45,6 +45,8 @@ def run(u, i, groups, label, kern):
 
 
 users = np.arange(n, dtype=np.int32)
+if os.environ.get("CHAIN_USERS"):  # a small user set cycled in order: rows stay cache-resident
+    users = (users % int(os.environ["CHAIN_USERS"])).astype(np.int32)
 for kern in ("substep",):
     run(users, np.zeros(n, np.int32), 1, "chain (1 item, 1 wave)", kern)
     run(users, (users // 64).astype(np.int32), 1, "runs of 64 (1 wave)", kern)

@@ -20,7 +20,10 @@ bg = int(sys.argv[3]) if len(sys.argv) > 3 else 0
 
 rng = np.random.default_rng(5)
 nu = max(n, bg // 8 + 1)
-u = np.concatenate([rng.permutation(nu)[:n], rng.integers(0, nu, bg)]).astype(np.int32)
+hot_u = rng.permutation(nu)[:n]
+if os.environ.get("CHAIN_USERS"):  # a small user set cycled in order: rows stay cache-resident
+    hot_u = np.arange(n) % int(os.environ["CHAIN_USERS"])
+u = np.concatenate([hot_u, rng.integers(0, nu, bg)]).astype(np.int32)
 i = np.concatenate([np.zeros(n, np.int32), rng.integers(1, 20000, bg).astype(np.int32)])
 p = L.default_params()
 p.num_factors, p.num_blocks, p.mode, p.iterations, p.seed = k, 1, L.MODE_DETERMINISTIC_F64, 1, 0
