@@ -25,6 +25,9 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <string>
+
 #include "kernels.hpp"
 
 namespace mfhip {
@@ -277,12 +280,162 @@ __global__ __launch_bounds__(64) void k_det_sweep(const DetWave* __restrict__ wa
   publish(pend, pend_val, lane);
 }
 
+// k_det_sweep2: the same schedule, entry order and arithmetic as k_det_sweep (bitwise the same
+// factors), with a deeper pipeline for the per-item chains (the hot item's wave is the superstep's
+// critical path: ~26k chained updates per NFLX superstep):
+//   * entries in chunks of kDetChunk with the entry index inside a chunk a compile-time constant
+//     (unrolled), so every field is a v_readlane with a constant lane and the body is straight-line
+//     code whose wait counts the compiler tracks exactly;
+//   * rows prefetched TWO entries ahead (slot s % 2), issued after the current entry's stores, so
+//     a prefetched item row always sees this wave's own earlier store; the user row of entry j+2 is
+//     loaded only if its ticket -- polled two entries earlier still -- was already ready, else the
+//     entry waits and loads when it runs (the rare slow path);
+//   * a ticket is published TWO entries late: entry j waits only for entry j-2's stores
+//     (vmcnt(6 KPL + 7): the operations issued after them), so a store's write-through latency
+//     overlaps two entries of compute.  A wave publishes every pending ticket before it blocks on
+//     one, so the no-deadlock argument of k_det_sweep holds unchanged.
+constexpr int kDetChunk = 16;
+
+template <int KPL>
+__global__ __launch_bounds__(64) void k_det_sweep2(const DetWave* __restrict__ waves, const uint32_t* __restrict__ eu,
+                                                   const uint32_t* __restrict__ ei, const uint32_t* __restrict__ eq,
+                                                   const double* __restrict__ er, double* U, double* I,
+                                                   uint64_t u_bytes, uint64_t i_bytes, const double* __restrict__ regU,
+                                                   const double* __restrict__ regI, int k, double eta,
+                                                   int32_t* ticket, int32_t* dummy_ticket, int32_t* err) {
+  constexpr int CH = kDetChunk;
+  constexpr int NW = 6 * KPL + 7;  // operations issued after an entry's stores until its ticket is published
+  static_assert(NW < 64, "vmcnt range");
+  __shared__ double lds[64 * KPL];
+  const int lane = threadIdx.x;
+  const DetWave d = waves[blockIdx.x];
+  const int64_t cnt = d.count;
+  if (cnt == 0) return;
+  dummy_ticket += 16 * static_cast<int64_t>(blockIdx.x);  // this wave's own scratch line
+  const __amdgpu_buffer_rsrc_t urs = raw_rsrc(U, u_bytes), irs = raw_rsrc(I, i_bytes);
+  uint32_t voff[KPL];
+#pragma unroll
+  for (int c = 0; c < KPL; ++c) voff[c] = lane + 64 * c < k ? static_cast<uint32_t>(lane + 64 * c) * 8u : 0x80000000u;
+  const uint32_t rowb = static_cast<uint32_t>(k) * 8u;
+  // chunk c: entry begin + CH c + (lane % CH) in every lane (entry arrays are padded past a wave's end)
+  auto chunk = [&](int64_t c) { return det_chunk(eu, ei, eq, er, d.begin + c * CH + (lane & (CH - 1))); };
+  DetChunk C0 = chunk(0), C1 = chunk(1);
+  // field of entry s + dj of chunk C0 (C1 past the chunk), s + dj < 2 CH
+  auto fu = [&](int s) { return s < CH ? rl(C0.u, s) : rl(C1.u, s - CH); };
+  auto fi = [&](int s) { return s < CH ? rl(C0.i, s) : rl(C1.i, s - CH); };
+  auto fq = [&](int s) { return s < CH ? rl(C0.q, s) : rl(C1.q, s - CH); };
+
+  DRow<KPL> P[2], Q[2];
+  double RU[2], RI[2];
+  int32_t okP[2];  // the slot's user row was prefetched (its ticket was ready)
+  int32_t tk[2];   // ticket polls, two entries ahead of the prefetch that reads them
+  // prologue: entries 0 and 1 now (their tickets polled and read here), polls of entries 2 and 3
+#pragma unroll
+  for (int x = 0; x < 2; ++x) {
+    const bool live = x < cnt;
+    const uint32_t u = fu(x), i = fi(x), q = fq(x);
+    okP[x] = !live || poll(ticket + u) == static_cast<int32_t>(q & kDetUseqMask);
+    P[x] = ldrow<KPL>(urs, voff, live && okP[x] ? u * rowb : kOOB);
+    Q[x] = ldrow<KPL>(irs, voff, live && !(x > 0 && (q & kDetKeepQ)) ? i * rowb : kOOB);
+    RU[x] = ld_sc1(regU + (live ? u : 0u));
+    RI[x] = ld_sc1(regI + (live ? i : 0u));
+  }
+#pragma unroll
+  for (int x = 0; x < 2; ++x) tk[x] = poll_issue(x + 2 < cnt ? ticket + fu(x + 2) : dummy_ticket);
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  int32_t* pend0 = dummy_ticket;  // entry j-2's ticket word and value
+  int32_t pv0 = 0;
+  int32_t* pend1 = dummy_ticket;  // entry j-1's
+  int32_t pv1 = 0;
+  double q[KPL];
+#pragma unroll
+  for (int c = 0; c < KPL; ++c) q[c] = 0.0;
+
+  for (int64_t c0 = 0;; c0 += CH) {
+#pragma unroll
+    for (int s = 0; s < CH; ++s) {
+      const int64_t j = c0 + s;
+      if (j >= cnt) goto done;
+      const int slot = s & 1;
+      const uint32_t u = fu(s), i = fi(s), qf = fq(s);
+      const double r = rld(s < CH ? C0.r : C1.r, s);
+      const int32_t useq = static_cast<int32_t>(qf & kDetUseqMask);
+      const uint32_t u2 = fu(s + 2), i2 = fi(s + 2), q2 = fq(s + 2), u4 = fu(s + 4);
+      // 1. the user row, when its ticket was not ready at prefetch time (rare): publish every
+      //    pending ticket (after its stores), wait for ours, load now
+      if (!okP[slot]) {
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        publish(pend0, pv0, lane);
+        publish(pend1, pv1, lane);
+        pend0 = pend1 = dummy_ticket;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // bounded wait (100 MHz clock)
+        while (poll(ticket + u) != useq) {
+          if (poll(err) != 0) return;
+          if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {  // ~1 s: a producer never ran
+            if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        P[slot] = ldrow<KPL>(urs, voff, u * rowb);
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+      }
+      // 2. compute entry j (DSGDforMF.scala:405-410, the reference's rounding, no FMA)
+      if (!(qf & kDetKeepQ)) {
+#pragma unroll
+        for (int c = 0; c < KPL; ++c) q[c] = Q[slot].v[c];
+      }
+      const double ru = uniform(RU[slot]), ri = uniform(RI[slot]);
+      double pr[KPL], pn[KPL];
+#pragma unroll
+      for (int c = 0; c < KPL; ++c) pr[c] = P[slot].v[c] * q[c];
+      const double e = r - seq_dot<KPL>(pr, k, lds, lane);  // :405
+#pragma unroll
+      for (int c = 0; c < KPL; ++c) {
+        pn[c] = P[slot].v[c] - eta * (ru * P[slot].v[c] - e * q[c]);  // :407-408
+        q[c] = q[c] - eta * (ri * q[c] - e * P[slot].v[c]);           // :409-410 (old p)
+      }
+      // 3. entry j-2's stores have landed (NW younger operations may still fly): publish its ticket
+      wait_vmcnt<NW>();
+      publish(pend0, pv0, lane);
+      pend0 = pend1;
+      pv0 = pv1;
+      pend1 = ticket + u;
+      pv1 = useq + 1;
+      // 4. entry j's stores
+      strow<KPL>(urs, voff, u * rowb, pn);
+      strow<KPL>(irs, voff, (qf & kDetDeferQ) ? kOOB : i * rowb, q);
+      // 5. prefetch entry j+2 into this slot (after the stores: a reload of an item row this wave
+      //    just stored sees it); its user row only if its ticket (polled at entry j-2) was ready
+      const bool live2 = j + 2 < cnt;
+      const int32_t okN = !live2 || __builtin_amdgcn_readfirstlane(tk[slot]) == static_cast<int32_t>(q2 & kDetUseqMask);
+      P[slot] = ldrow<KPL>(urs, voff, live2 && okN ? u2 * rowb : kOOB);
+      Q[slot] = ldrow<KPL>(irs, voff, live2 && !(q2 & kDetKeepQ) ? i2 * rowb : kOOB);
+      RU[slot] = ld_sc1(regU + (live2 ? u2 : 0u));
+      RI[slot] = ld_sc1(regI + (live2 ? i2 : 0u));
+      okP[slot] = okN;
+      // 6. poll entry j+4's ticket (read at entry j+2)
+      tk[slot] = poll_issue(j + 4 < cnt ? ticket + u4 : dummy_ticket);
+    }
+    C0 = C1;
+    C1 = chunk(c0 / CH + 2);
+  }
+done:
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  publish(pend0, pv0, lane);
+  publish(pend1, pv1, lane);
+}
+
 template <int KPL>
 int det_capacity() {
   int dev = 0, cus = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_det_sweep<KPL>, 64, 0) != hipSuccess) return 0;
+  int a = 0, b = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, k_det_sweep<KPL>, 64, 0) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_det_sweep2<KPL>, 64, 0) != hipSuccess)
+    return 0;
+  per_cu = a < b ? a : b;
   return cus * per_cu;
 }
 
@@ -301,9 +454,17 @@ void launch_det_sweep(hipStream_t st, const DetWave* waves, int nw, const uint32
                       int32_t* dummy_ticket, int32_t* err, hipEvent_t ev0, hipEvent_t ev1) {
   if (nw <= 0) return;
   const dim3 g(static_cast<unsigned>(nw)), b(64);
-#define MF_DET(KPL)                                                                                              \
-  hipExtLaunchKernelGGL((k_det_sweep<KPL>), g, b, 0, st, ev0, ev1, 0, waves, eu, ei, eq, er, U, I, u_bytes, i_bytes, \
-                        regU, regI, k, eta, ticket, dummy_ticket, err)
+  // MFHIP_DET_SWEEP=1: the one-entry-deep pipeline (k_det_sweep), for A/B
+  static const bool deep = [] { const char* v = std::getenv("MFHIP_DET_SWEEP"); return !(v && std::string(v) == "1"); }();
+#define MF_DET(KPL)                                                                                                  \
+  do {                                                                                                               \
+    if (deep)                                                                                                        \
+      hipExtLaunchKernelGGL((k_det_sweep2<KPL>), g, b, 0, st, ev0, ev1, 0, waves, eu, ei, eq, er, U, I, u_bytes,     \
+                            i_bytes, regU, regI, k, eta, ticket, dummy_ticket, err);                                 \
+    else                                                                                                             \
+      hipExtLaunchKernelGGL((k_det_sweep<KPL>), g, b, 0, st, ev0, ev1, 0, waves, eu, ei, eq, er, U, I, u_bytes,      \
+                            i_bytes, regU, regI, k, eta, ticket, dummy_ticket, err);                                 \
+  } while (0)
   if (k <= 64) MF_DET(1);
   else if (k <= 128) MF_DET(2);
   else if (k <= 256) MF_DET(4);
