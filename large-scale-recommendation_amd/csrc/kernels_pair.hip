@@ -46,7 +46,8 @@ namespace {
 template <int KPL, int D, int UP>
 __device__ __forceinline__ void pair_cell(const WaveDesc d, const ChunkRaw& L0, const ChunkRaw& L1,
                                           const u4v* __restrict__ recs, __amdgpu_buffer_rsrc_t urs,
-                                          __amdgpu_buffer_rsrc_t irs, float eta, int lane) {
+                                          __amdgpu_buffer_rsrc_t irs, float eta, int lane, uint64_t& wait_clk) {
+  (void)wait_clk;
   constexpr int NV = Row<KPL>::NV;
   constexpr int CH = kPairChunk;
   static_assert(CH % D == 0, "ring slots must repeat every chunk");
@@ -83,6 +84,13 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const ChunkRaw& L0, 
       for (int s = 0; s < CH; ++s) {
         if (c * CH + s >= npairs) goto run_done;
         const int slot = s % DS;
+#ifdef MFHIP_WAITPROBE
+        {  // experiment build: shader cycles spent waiting for this pair's prefetched user rows
+          const uint64_t a = __builtin_amdgcn_s_memtime();
+          __builtin_amdgcn_s_waitcnt((4 * (DS - 1)) & 15 | (((4 * (DS - 1)) >> 4) << 14) | 0x0F70 & ~0xF);
+          wait_clk += __builtin_amdgcn_s_memtime() - a;
+        }
+#endif
         const uint32_t fl = rl(C0.flags, s), osa = rl(C0.sa, s);
         // the ring's next offsets (pair s + DS), also named up front
         const uint32_t noa = s + DS < CH ? rl(C0.ua, s + DS) : rl(C1.w0[0], s + DS - CH);
@@ -141,6 +149,13 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const ChunkRaw& L0, 
       for (int s = 0; s < CH; ++s) {
         if (c * CH + s >= npairs) return;
         const int slot = s % D;
+#ifdef MFHIP_WAITPROBE
+        {  // experiment build: shader cycles spent waiting for this pair's prefetched rows
+          const uint64_t a = __builtin_amdgcn_s_memtime();
+          __builtin_amdgcn_s_waitcnt((8 * (D - 1)) & 15 | (((8 * (D - 1)) >> 4) << 14) | 0x0F70 & ~0xF);
+          wait_clk += __builtin_amdgcn_s_memtime() - a;
+        }
+#endif
         const uint32_t fl = rl(C0.flags, s);
         // store offsets named up front: the scheduler then reads them early instead of right
         // before each store (a v_readlane feeding a buffer store's soffset costs an s_nop 4)
@@ -205,8 +220,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   const WaveDesc d = waves[blockIdx.x];
   const __amdgpu_buffer_rsrc_t rr = cell_records(recs, d.base, d.steps);
   const uint32_t vlane = threadIdx.x * 64u;
+  uint64_t wait_clk = 0;
   pair_cell<KPL, D, 0>(d, chunk_load(rr, 0, vlane), chunk_load(rr, 1, vlane), recs, raw_rsrc(U, u_bytes),
-                       raw_rsrc(I, i_bytes), eta, threadIdx.x);
+                       raw_rsrc(I, i_bytes), eta, threadIdx.x, wait_clk);
   if (trace && threadIdx.x == 0) {
     trace[2 * blockIdx.x] = t_start;
     trace[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
@@ -282,11 +298,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
       }
     }
     const uint64_t c_start = __builtin_amdgcn_s_memrealtime();
-    const uint64_t c_clk = trace ? __builtin_amdgcn_s_memtime() : 0;
+    uint64_t c_clk = trace ? __builtin_amdgcn_s_memtime() : 0;
+    uint64_t wait_clk = 0;
     const bool hot = prio == 1 && d.cells == kWaveSingleRun;
     if (hot) __builtin_amdgcn_s_setprio(3);
     if (!PRE && d.steps > 0) first_chunks(d, L0, L1);
-    if (d.steps > 0) pair_cell<KPL, D, kSC1>(d, L0, L1, recs, urs, irs, eta, lane);
+    if (d.steps > 0) pair_cell<KPL, D, kSC1>(d, L0, L1, recs, urs, irs, eta, lane, wait_clk);
     if (hot) __builtin_amdgcn_s_setprio(0);
     if (PRE) {
       first_chunks(dn, L0, L1);
@@ -301,8 +318,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
       uint64_t* tr = trace + 4 * (w.cell0 + t);
       tr[0] = c_start;
       tr[1] = __builtin_amdgcn_s_memrealtime();
-      tr[2] = c_clk;
       tr[3] = __builtin_amdgcn_s_memtime();
+#ifdef MFHIP_WAITPROBE
+      c_clk = tr[3] - wait_clk;  // experiment build: the trace's clock column carries the wait cycles
+#endif
+      tr[2] = c_clk;
     }
     d = dn;
   }
