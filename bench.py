@@ -158,6 +158,28 @@ def rmse_reference(a, arrays):
     return rec
 
 
+def det_kernel_name():
+    return "k_det_sweep" if os.environ.get("MFHIP_DET_SWEEP") == "1" else "k_det_sweep2"
+
+
+def det_roofline(a, k, sp):
+    """The deterministic sweep against the HBM roofline: algorithmic bytes B_f64(k) = 32k+24 per
+    update over its profiled launch time, and the committed PMC traffic of the same
+    kernel (profiles/r*_traffic_<config>_det.json).  The kernel is bound by its per-item f64 chains
+    (the sequential ddot fold), not by bytes: the fraction says how far from the roofline that is."""
+    if sp["kernel_ms"] <= 0:
+        return None
+    launches = max(sp["kernel_launches"], 1)
+    ksec = sp["kernel_ms"] / 1e3
+    alg = sp["updates"] * (32 * k + 24) / ksec / 1e9
+    da = argparse.Namespace(**{**vars(a), "mode": "det"})
+    traffic, src = pmc_traffic(da, k, 0, det_kernel_name())
+    return {"bound": "hbm", "achieved": round(alg, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(alg / HBM_PEAK_GBS, 4), "bytes_model": "algorithmic B_f64(k) = 32k+24 per update",
+            "avg_launch_us": round(sp["kernel_ms"] * 1e3 / launches, 2), "traffic": traffic, "traffic_source": src,
+            "traffic_frac": round(traffic / (ksec / launches) / 1e9 / HBM_PEAK_GBS, 4) if traffic else None}
+
+
 def det_leg(a, k, nb, train, test, ref, stream):
     """The deterministic f64 mode on the same data: DSGDforMF.scala:378-418's exact update order
     (JVM shuffle, F2J ddot fold, no FMA), one persistent sweep per superstep.  Timed epochs after
@@ -195,8 +217,9 @@ def det_leg(a, k, nb, train, test, ref, stream):
         online = online_leg(ctx, stream, a) if stream is not None else None
     return {"metric": "SGD rating updates/sec, deterministic f64 (the reference's exact update order)",
             "value": round(st["updates"] / el, 1), "unit": "updates/s", "dtype": "f64", "epochs": a.det_epochs,
-            "ms_per_step": round(el * 1e3 / a.det_epochs, 3), "kernel": "k_det_sweep",
+            "ms_per_step": round(el * 1e3 / a.det_epochs, 3), "kernel": det_kernel_name(),
             "avg_launch_us": round(sp["kernel_ms"] * 1e3 / max(sp["kernel_launches"], 1), 2),
+            "roofline": det_roofline(a, k, sp),
             "launches_per_epoch": sp["kernel_launches"], "prepare_s": round(t_prep, 2),
             "rmse": round(rmse, 9), "rmse_ref": round(ref["oracle_rmse"], 9) if ref else None,
             "rmse_equal_to_ref": (abs(rmse - ref["oracle_rmse"]) <= 1e-12 * ref["oracle_rmse"]) if ref else None,
@@ -336,7 +359,7 @@ def main():
         launches = st_p["kernel_launches"]
         ksec = st_p["kernel_ms"] / 1e3
         achieved = st_p["moved_bytes"] / ksec / 1e9  # GB/s, this rank's sweep kernel
-        kname = L.lib().mf_fast_kernel_name(k).decode() if a.mode == "fast" else "k_level"
+        kname = L.lib().mf_fast_kernel_name(k).decode() if a.mode == "fast" else det_kernel_name()
         # the committed PMC summaries are one-GPU runs: a rank of an N-GPU ring runs other launches
         traffic, traffic_src = pmc_traffic(a, k, st["groups"], kname) if D.world == 1 else (None, None)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

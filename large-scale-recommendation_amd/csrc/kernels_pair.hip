@@ -314,15 +314,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     if (lane == 0)
       __hip_atomic_store(my_prog, static_cast<int32_t>(base + static_cast<uint32_t>(t) + 1u), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
-    if (trace && lane == 0) {  // {start, end} on the 100 MHz clock, then the shader clock (s_memtime)
+    if (trace && lane == 0) {  // {start, end} on the 100 MHz clock, shader-clock cycles, placement
       uint64_t* tr = trace + 4 * (w.cell0 + t);
       tr[0] = c_start;
       tr[1] = __builtin_amdgcn_s_memrealtime();
-      tr[3] = __builtin_amdgcn_s_memtime();
 #ifdef MFHIP_WAITPROBE
-      c_clk = tr[3] - wait_clk;  // experiment build: the trace's clock column carries the wait cycles
+      tr[2] = wait_clk;  // experiment build: the trace's clock column carries the wait cycles
+#else
+      tr[2] = __builtin_amdgcn_s_memtime() - c_clk;
 #endif
-      tr[2] = c_clk;
+      // where the wave runs: XCC_ID (hwreg 20) and HW_ID (hwreg 4: wave, SIMD, CU, SH, SE)
+      tr[3] = (static_cast<uint64_t>(__builtin_amdgcn_s_getreg((15 << 11) | 20)) << 32) |
+              static_cast<uint32_t>(__builtin_amdgcn_s_getreg((31 << 11) | 4));
     }
     d = dn;
   }

@@ -378,7 +378,8 @@ void collect_profile(mf_ctx* ctx) {
 // MFHIP_WAVE_TRACE=<file>: per wave of the per-cell schedules "shard sm t wave steps cells start
 // end" (100 MHz clock) of the last time every sub-step ran; written when the context is destroyed.
 // The systolic sweep adds a 9th column: the cell's shader-clock cycles (s_memtime), so the clock
-// the wave actually ran at is cycles / ((end - start) x 10 ns).
+// the wave actually ran at is cycles / ((end - start) x 10 ns), and a 10th: where the wave ran,
+// XCC_ID << 32 | HW_ID (SIMD bits 5:4, CU 11:8, SH 12, SE 15:13).
 void dump_wave_trace(mf_ctx* ctx) {
   const char* path = std::getenv("MFHIP_WAVE_TRACE");
   if (!path) return;
@@ -395,9 +396,10 @@ void dump_wave_trace(mf_ctx* ctx) {
           const SysWave& sw = s.st_sysw_host[w];
           for (int32_t t = 0; t < sw.G; ++t) {
             const int64_t x = sw.cell0 + t;
-            std::fprintf(f, "%d %d %d %lld %d %d %llu %llu %llu\n", s.index, sm, t, (long long)(w - s.st_sys_off[sm]),
+            std::fprintf(f, "%d %d %d %lld %d %d %llu %llu %llu %llu\n", s.index, sm, t, (long long)(w - s.st_sys_off[sm]),
                          s.st_sys_host[x].steps, s.st_sys_host[x].cells, (unsigned long long)tr[4 * x],
-                         (unsigned long long)tr[4 * x + 1], (unsigned long long)(tr[4 * x + 3] - tr[4 * x + 2]));
+                         (unsigned long long)tr[4 * x + 1], (unsigned long long)tr[4 * x + 2],
+                         (unsigned long long)tr[4 * x + 3]);
           }
         }
       continue;

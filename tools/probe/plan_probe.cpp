@@ -133,6 +133,39 @@ int main(int argc, char** argv) {
     }
     std::printf("single-run cells %lld: with forwarding %lld; pairs with forwarding %lld, with a no-op B %lld\n",
                 (long long)run_cells, (long long)fwd_cells, (long long)fwd_pairs, (long long)pad_b);
+    // blocks of BP pairs of single-run cells: forwarding inside a block, at its first pair, and
+    // users shared with the previous block (a row prefetched one block ahead would be stale)
+    for (int BP : {4, 7, 8}) {
+      int64_t blocks = 0, fwd_in = 0, fwd_first = 0, shared_prev = 0, shared_rows = 0, clean = 0;
+      for (const WaveDesc& w : pp.waves) {
+        if (w.cells != kWaveSingleRun) continue;
+        std::vector<uint32_t> prev;
+        for (int64_t x0 = w.base; x0 < w.base + w.steps; x0 += BP) {
+          ++blocks;
+          std::vector<uint32_t> cur;
+          bool fi = false, ff = false;
+          for (int64_t x = x0; x < std::min<int64_t>(x0 + BP, w.base + w.steps); ++x) {
+            const PairRec& r = pp.recs[x];
+            if (r.flags & (kPairFwdA | kPairFwdB)) (x == x0 ? ff : fi) = true;
+            if (r.sa != kOffOOB) cur.push_back(r.sa);
+            if (r.sb != kOffOOB) cur.push_back(r.sb);
+          }
+          int sh = 0;
+          for (uint32_t o : cur)
+            for (uint32_t q : prev) sh += o == q;
+          fwd_in += fi;
+          fwd_first += ff;
+          shared_prev += sh > 0;
+          shared_rows += sh;
+          clean += !fi && !ff && sh == 0;
+          prev = cur;
+        }
+      }
+      std::printf("single-run blocks of %d pairs: %lld, forwarding inside %lld, at the first pair %lld, sharing a user "
+                  "with the previous block %lld (%lld rows), clean %lld (%.1f%%)\n", BP, (long long)blocks,
+                  (long long)fwd_in, (long long)fwd_first, (long long)shared_prev, (long long)shared_rows,
+                  (long long)clean, 100.0 * clean / std::max<int64_t>(blocks, 1));
+    }
   }
   {  // fingerprint of the plans (FNV-1a over the records, cell offsets and pair records)
     uint64_t h = 1469598103934665603ull;

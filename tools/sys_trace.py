@@ -2,6 +2,7 @@
 """Summarise an MFHIP_WAVE_TRACE dump of the systolic pair sweep (rows: shard sm t wave steps kind
 start end, one per cell, 100 MHz): per-kind cell cost fit, the gaps between a wave's consecutive
 cells (neighbour wait + hand-off), and each superstep's span."""
+import collections
 import sys
 
 import numpy as np
@@ -51,4 +52,20 @@ for sm in np.unique(a[:, 1]):
           + (f", shader clock {c[:, 8].sum() / max(d.sum(), 1):.2f} GHz vs all waves "
              f"{w[:, 8].sum() / max(((w[:, 7] - w[:, 6]) * 10.0).sum(), 1):.2f} GHz, {c[:, 8].sum() / max(pairs, 1):.0f} "
              f"cycles/pair" if clk else ""))
+    if a.shape[1] > 9:  # 10th column: XCC_ID << 32 | HW_ID of the wave (the first cell's)
+        loc = {}
+        for x in waves:
+            h = int(w[w[:, 3] == x, 9][0])
+            xcc, hw = h >> 32, h & 0xFFFFFFFF
+            cu = (xcc & 0xF, (hw >> 13) & 7, (hw >> 12) & 1, (hw >> 8) & 0xF)  # xcc, se, sh, cu
+            loc[x] = (cu, (hw >> 4) & 3)
+        cu_m, simd_m = loc[xm]
+        same_cu = [x for x in waves if x != xm and loc[x][0] == cu_m]
+        same_simd = [x for x in same_cu if loc[x][1] == simd_m]
+        per_simd = collections.Counter(loc.values())
+        busy = dict(zip(waves, per_wave))
+        print(f"    placement: busiest wave on xcc/se/sh/cu {cu_m} simd {simd_m}; {len(same_cu)} other waves on its CU "
+              f"(busy {[round(busy[x] / 1e3) for x in same_cu]} us), {len(same_simd)} on its SIMD; SIMDs holding 1/2/3+ "
+              f"waves: {sum(v == 1 for v in per_simd.values())}/{sum(v == 2 for v in per_simd.values())}/"
+              f"{sum(v >= 3 for v in per_simd.values())}")
 print(f"sum of superstep spans {tot / 1e6:.2f} ms")
