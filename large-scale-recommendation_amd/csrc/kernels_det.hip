@@ -50,25 +50,8 @@ __device__ __forceinline__ T seq_dot(const T (&prod)[KPL], int k) {
   return acc;
 }
 
-// seq_dot's order with the products through a wave-private LDS row, read back by every lane as
-// broadcast reads: the dependent add chain takes its operands from VGPRs (no v_readlane and
-// hazard nop per add).  Bitwise seq_dot.
-template <typename T, int KPL>
-__device__ __forceinline__ T seq_dot_lds(const T (&prod)[KPL], int k, T* lds, int lane) {
-#pragma unroll
-  for (int c = 0; c < KPL; ++c) lds[64 * c + lane] = prod[c];
-  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the wave's own LDS writes are done
-  __builtin_amdgcn_wave_barrier();
-  T acc = T(0);
-  if (k == 64 * KPL) {
-#pragma unroll
-    for (int x = 0; x < 64 * KPL; ++x) acc = acc + lds[x];
-  } else {
-    for (int x = 0; x < k; ++x) acc = acc + lds[x];
-  }
-  __builtin_amdgcn_wave_barrier();  // the next call's writes stay behind these reads
-  return acc;
-}
+#include "seq_fold.hpp"
+#include "ticket_wait.hpp"
 
 template <typename T, int KPL, int ARITH>
 __global__ __launch_bounds__(256) void k_level(const DetEntry* __restrict__ ent, int64_t n,
@@ -136,20 +119,6 @@ __global__ __launch_bounds__(64) void k_online_sweep(const int64_t* __restrict__
     const int f = lane + 64 * c;
     return FULL || f < k ? __hip_atomic_load(row + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : T(0);
   };
-  auto wait_ticket = [&](uint32_t ur, int32_t q) -> bool {
-    if (q == 0) return true;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(ticket + ur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != q) {
-      if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
-        return false;  // another wave gave up
-      if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {  // 100 MHz clock: ~1 s
-        if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return false;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    return true;
-  };
   // loads ahead: every lane issues one load per c (clamped address), so the vmcnt count of a row
   // loaded ahead is exactly KPL; lanes past k are zeroed where the row is used (not here, which
   // would wait for the load at once)
@@ -176,7 +145,7 @@ __global__ __launch_bounds__(64) void k_online_sweep(const int64_t* __restrict__
   bool ha = false, hb = false;
   bool have_q = false;
   uint32_t cur_i = 0;
-  auto step = [&](int64_t j, T (&slot)[KPL], bool& have, T (&oslot)[KPL], bool& ohave) -> bool {
+  auto step = [&](int64_t j, T (&slot)[KPL], bool& have, T (&oslot)[KPL], bool& ohave) {
     const uint32_t ur = ent[j].u, ir = ent[j].i;
     const int32_t q = static_cast<int32_t>(useq[j]);
     const T r = static_cast<T>(ent[j].r);
@@ -191,7 +160,7 @@ __global__ __launch_bounds__(64) void k_online_sweep(const int64_t* __restrict__
         if (lane == 0) __hip_atomic_store(ticket + pend_u, pend_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         has_pend = false;
       }
-      if (!wait_ticket(ur, q)) return false;
+      if (q != 0) wait_ticket_or_fail(ticket + ur, q, err, lane);  // no early return (ticket_wait.hpp)
 #pragma unroll
       for (int c = 0; c < KPL; ++c) pv[c] = ld(p, c);
     }
@@ -214,7 +183,7 @@ __global__ __launch_bounds__(64) void k_online_sweep(const int64_t* __restrict__
     const int32_t t2 = __hip_atomic_load(ticket + (n2 ? u2 : ur), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
     for (int c = 0; c < KPL; ++c) pr[c] = pv[c] * qv[c];
-    const T e = r - seq_dot_lds<T, KPL>(pr, k, lds, lane);
+    const T e = r - seq_fold<T, KPL>(pr, k, lds, lane);
     // the tickets are looked at before the stores (so no wait for them lands behind the stores)
     const bool g1 = n1 && u1 != ur && (q1 == 0 || __builtin_amdgcn_readfirstlane(t1) == q1);
     const bool g2 = n2 && u2 != ur && (q2 == 0 || __builtin_amdgcn_readfirstlane(t2) == q2);
@@ -274,12 +243,15 @@ __global__ __launch_bounds__(64) void k_online_sweep(const int64_t* __restrict__
       else __builtin_amdgcn_s_waitcnt(0x0F70);
       if (lane == 0) __hip_atomic_store(ticket + ur, q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    return true;
   };
-  for (int64_t j = j0; j < j1; j += 2) {
-    if (!step(j, sa, ha, sb, hb)) return;
-    if (j + 1 < j1 && !step(j + 1, sb, hb, sa, ha)) return;
+  // whole pairs of steps, then an odd last one: no exit test between the steps of the loop body
+  // (a join there makes the compiler's wait counts conservative, ticket_wait.hpp)
+  const int64_t jp = j0 + ((j1 - j0) & ~int64_t(1));
+  for (int64_t j = j0; j < jp; j += 2) {
+    step(j, sa, ha, sb, hb);
+    step(j + 1, sb, hb, sa, ha);
   }
+  if (jp < j1) step(jp, sa, ha, sb, hb);
   if (has_pend) {
     __builtin_amdgcn_s_waitcnt(0x0F70);
     if (lane == 0) __hip_atomic_store(ticket + pend_u, pend_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

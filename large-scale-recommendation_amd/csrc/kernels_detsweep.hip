@@ -51,37 +51,8 @@ __device__ __forceinline__ void st_sc1(double* p, double v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// ((0 + x0) + x1) + ... over f = 0..k-1 (F2jBLAS.ddot / Scala foldLeft order); lane l holds
-// element l + 64c in prod[c].  The products go through a wave-private LDS row and every lane
-// reads them back in order as broadcast 16-B reads, so the dependent f64 add chain takes its
-// operands from VGPRs (a v_readlane per element would add a readlane + hazard nop per add).
-template <int KPL>
-__device__ __forceinline__ double seq_dot(const double (&prod)[KPL], int k, double* lds, int lane) {
-#pragma unroll
-  for (int c = 0; c < KPL; ++c) lds[64 * c + lane] = prod[c];
-  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the wave's own LDS writes are done
-  __builtin_amdgcn_wave_barrier();
-  double acc = 0.0;
-  const double2* l2 = reinterpret_cast<const double2*>(lds);
-  if (k == 64 * KPL) {
-#pragma unroll
-    for (int x = 0; x < 32 * KPL; ++x) {
-      const double2 v = l2[x];
-      acc = acc + v.x;
-      acc = acc + v.y;
-    }
-  } else {
-    const int half = k >> 1;
-    for (int x = 0; x < half; ++x) {
-      const double2 v = l2[x];
-      acc = acc + v.x;
-      acc = acc + v.y;
-    }
-    if (k & 1) acc = acc + lds[k - 1];
-  }
-  __builtin_amdgcn_wave_barrier();  // every lane has read before the next entry rewrites the row
-  return acc;
-}
+#include "seq_fold.hpp"
+#include "ticket_wait.hpp"
 
 // Entry fields of a wave's entry list, 64 per lane-register chunk (the host pads every entry
 // array by 64, so a chunk load never needs a bounds branch).
@@ -170,7 +141,7 @@ __global__ __launch_bounds__(64) void k_det_sweep(const DetWave* __restrict__ wa
                                                   uint64_t u_bytes, uint64_t i_bytes, const double* __restrict__ regU,
                                                   const double* __restrict__ regI, int k, double eta,
                                                   int32_t* ticket, int32_t* dummy_ticket, int32_t* err) {
-  __shared__ double lds[64 * KPL];
+  __shared__ __attribute__((aligned(16))) double lds[64 * KPL];
   const int lane = threadIdx.x;
   const DetWave d = waves[blockIdx.x];
   const int64_t cnt = d.count;
@@ -254,7 +225,7 @@ __global__ __launch_bounds__(64) void k_det_sweep(const DetWave* __restrict__ wa
       double pr[KPL], pn[KPL];
 #pragma unroll
       for (int c = 0; c < KPL; ++c) pr[c] = P.v[c] * q[c];
-      const double e = r - seq_dot<KPL>(pr, k, lds, lane);  // :405
+      const double e = r - seq_fold<double, KPL>(pr, k, lds, lane);  // :405
 #pragma unroll
       for (int c = 0; c < KPL; ++c) {
         pn[c] = P.v[c] - eta * (ru * P.v[c] - e * q[c]);  // :407-408
@@ -296,6 +267,7 @@ __global__ __launch_bounds__(64) void k_det_sweep(const DetWave* __restrict__ wa
 //     one, so the no-deadlock argument of k_det_sweep holds unchanged.
 constexpr int kDetChunk = 16;
 
+
 template <int KPL>
 __global__ __launch_bounds__(64) void k_det_sweep2(const DetWave* __restrict__ waves, const uint32_t* __restrict__ eu,
                                                    const uint32_t* __restrict__ ei, const uint32_t* __restrict__ eq,
@@ -306,7 +278,7 @@ __global__ __launch_bounds__(64) void k_det_sweep2(const DetWave* __restrict__ w
   constexpr int CH = kDetChunk;
   constexpr int NW = 6 * KPL + 7;  // operations issued after an entry's stores until its ticket is published
   static_assert(NW < 64, "vmcnt range");
-  __shared__ double lds[64 * KPL];
+  __shared__ __attribute__((aligned(16))) double lds[64 * KPL];
   const int lane = threadIdx.x;
   const DetWave d = waves[blockIdx.x];
   const int64_t cnt = d.count;
@@ -351,71 +323,87 @@ __global__ __launch_bounds__(64) void k_det_sweep2(const DetWave* __restrict__ w
 #pragma unroll
   for (int c = 0; c < KPL; ++c) q[c] = 0.0;
 
-  for (int64_t c0 = 0;; c0 += CH) {
-#pragma unroll
-    for (int s = 0; s < CH; ++s) {
-      const int64_t j = c0 + s;
-      if (j >= cnt) goto done;
-      const int slot = s & 1;
-      const uint32_t u = fu(s), i = fi(s), qf = fq(s);
-      const double r = rld(s < CH ? C0.r : C1.r, s);
-      const int32_t useq = static_cast<int32_t>(qf & kDetUseqMask);
-      const uint32_t u2 = fu(s + 2), i2 = fi(s + 2), q2 = fq(s + 2), u4 = fu(s + 4);
-      // 1. the user row, when its ticket was not ready at prefetch time (rare): publish every
-      //    pending ticket (after its stores), wait for ours, load now
-      if (!okP[slot]) {
-        __builtin_amdgcn_s_waitcnt(0x0F70);
-        publish(pend0, pv0, lane);
-        publish(pend1, pv1, lane);
-        pend0 = pend1 = dummy_ticket;
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // bounded wait (100 MHz clock)
-        while (poll(ticket + u) != useq) {
-          if (poll(err) != 0) return;
-          if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {  // ~1 s: a producer never ran
-            if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-        P[slot] = ldrow<KPL>(urs, voff, u * rowb);
-        __builtin_amdgcn_s_waitcnt(0x0F70);
-      }
-      // 2. compute entry j (DSGDforMF.scala:405-410, the reference's rounding, no FMA)
-      if (!(qf & kDetKeepQ)) {
-#pragma unroll
-        for (int c = 0; c < KPL; ++c) q[c] = Q[slot].v[c];
-      }
-      const double ru = uniform(RU[slot]), ri = uniform(RI[slot]);
-      double pr[KPL], pn[KPL];
-#pragma unroll
-      for (int c = 0; c < KPL; ++c) pr[c] = P[slot].v[c] * q[c];
-      const double e = r - seq_dot<KPL>(pr, k, lds, lane);  // :405
-#pragma unroll
-      for (int c = 0; c < KPL; ++c) {
-        pn[c] = P[slot].v[c] - eta * (ru * P[slot].v[c] - e * q[c]);  // :407-408
-        q[c] = q[c] - eta * (ri * q[c] - e * P[slot].v[c]);           // :409-410 (old p)
-      }
-      // 3. entry j-2's stores have landed (NW younger operations may still fly): publish its ticket
-      wait_vmcnt<NW>();
+  // one entry (chunk-relative s, a compile-time constant once unrolled)
+#ifdef MFHIP_DET_PROBE
+  uint64_t pc[4] = {0, 0, 0, 0};  // experiment build: shader cycles per phase, printed by wave 0
+  uint64_t pt = __builtin_amdgcn_s_memtime();
+  auto stamp = [&](int x) { const uint64_t n = __builtin_amdgcn_s_memtime(); pc[x] += n - pt; pt = n; };
+#else
+  auto stamp = [](int) {};
+#endif
+  auto entry = [&](const int s, const int64_t j) {
+    const int slot = s & 1;
+    const uint32_t u = fu(s), i = fi(s), qf = fq(s);
+    const double r = rld(s < CH ? C0.r : C1.r, s);
+    const int32_t useq = static_cast<int32_t>(qf & kDetUseqMask);
+    const uint32_t u2 = fu(s + 2), i2 = fi(s + 2), q2 = fq(s + 2), u4 = fu(s + 4);
+    // 1. the user row, when its ticket was not ready at prefetch time (rare): publish every
+    //    pending ticket (after its stores), wait for ours, load now
+    if (!okP[slot]) {
+      __builtin_amdgcn_s_waitcnt(0x0F70);
       publish(pend0, pv0, lane);
-      pend0 = pend1;
-      pv0 = pv1;
-      pend1 = ticket + u;
-      pv1 = useq + 1;
-      // 4. entry j's stores
-      strow<KPL>(urs, voff, u * rowb, pn);
-      strow<KPL>(irs, voff, (qf & kDetDeferQ) ? kOOB : i * rowb, q);
-      // 5. prefetch entry j+2 into this slot (after the stores: a reload of an item row this wave
-      //    just stored sees it); its user row only if its ticket (polled at entry j-2) was ready
-      const bool live2 = j + 2 < cnt;
-      const int32_t okN = !live2 || __builtin_amdgcn_readfirstlane(tk[slot]) == static_cast<int32_t>(q2 & kDetUseqMask);
-      P[slot] = ldrow<KPL>(urs, voff, live2 && okN ? u2 * rowb : kOOB);
-      Q[slot] = ldrow<KPL>(irs, voff, live2 && !(q2 & kDetKeepQ) ? i2 * rowb : kOOB);
-      RU[slot] = ld_sc1(regU + (live2 ? u2 : 0u));
-      RI[slot] = ld_sc1(regI + (live2 ? i2 : 0u));
-      okP[slot] = okN;
-      // 6. poll entry j+4's ticket (read at entry j+2)
-      tk[slot] = poll_issue(j + 4 < cnt ? ticket + u4 : dummy_ticket);
+      publish(pend1, pv1, lane);
+      pend0 = pend1 = dummy_ticket;
+      wait_ticket_or_fail(ticket + u, useq, err, lane);  // no early return (ticket_wait.hpp)
+      P[slot] = ldrow<KPL>(urs, voff, u * rowb);
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+    }
+    // 2. compute entry j (DSGDforMF.scala:405-410, the reference's rounding, no FMA)
+    if (!(qf & kDetKeepQ)) {
+#pragma unroll
+      for (int c = 0; c < KPL; ++c) q[c] = Q[slot].v[c];
+    }
+    const double ru = uniform(RU[slot]), ri = uniform(RI[slot]);
+    double pr[KPL], pn[KPL];
+#pragma unroll
+    for (int c = 0; c < KPL; ++c) pr[c] = P[slot].v[c] * q[c];
+    stamp(0);
+    const double e = r - seq_fold<double, KPL>(pr, k, lds, lane);  // :405
+    stamp(1);
+#pragma unroll
+    for (int c = 0; c < KPL; ++c) {
+      pn[c] = P[slot].v[c] - eta * (ru * P[slot].v[c] - e * q[c]);  // :407-408
+      q[c] = q[c] - eta * (ri * q[c] - e * P[slot].v[c]);           // :409-410 (old p)
+    }
+    // 3. entry j-2's stores have landed (NW younger operations may still fly): publish its ticket
+    wait_vmcnt<NW>();
+    publish(pend0, pv0, lane);
+    pend0 = pend1;
+    pv0 = pv1;
+    pend1 = ticket + u;
+    pv1 = useq + 1;
+    // 4. entry j's stores
+    strow<KPL>(urs, voff, u * rowb, pn);
+    strow<KPL>(irs, voff, (qf & kDetDeferQ) ? kOOB : i * rowb, q);
+    stamp(2);
+    // 5. prefetch entry j+2 into this slot (after the stores: a reload of an item row this wave
+    //    just stored sees it); its user row only if its ticket (polled at entry j-2) was ready
+    const bool live2 = j + 2 < cnt;
+    const int32_t okN = !live2 || __builtin_amdgcn_readfirstlane(tk[slot]) == static_cast<int32_t>(q2 & kDetUseqMask);
+    P[slot] = ldrow<KPL>(urs, voff, live2 && okN ? u2 * rowb : kOOB);
+    Q[slot] = ldrow<KPL>(irs, voff, live2 && !(q2 & kDetKeepQ) ? i2 * rowb : kOOB);
+    RU[slot] = ld_sc1(regU + (live2 ? u2 : 0u));
+    RI[slot] = ld_sc1(regI + (live2 ? i2 : 0u));
+    okP[slot] = okN;
+    // 6. poll entry j+4's ticket (read at entry j+2)
+    tk[slot] = poll_issue(j + 4 < cnt ? ticket + u4 : dummy_ticket);
+    stamp(3);
+  };
+  // Full chunks run their CH entries with no exit test in between: a per-entry "j >= cnt" exit
+  // makes every entry's start a join with the path that skipped the previous entry, and the
+  // compiler's wait counts then treat the rows loaded two entries back as just issued (vmcnt(3):
+  // every entry waited for the previous entry's loads, a full memory round trip per update).
+  // Only the last, partial chunk tests every entry.
+  for (int64_t c0 = 0;; c0 += CH) {
+    if (c0 + CH <= cnt) {
+#pragma unroll
+      for (int s = 0; s < CH; ++s) entry(s, c0 + s);
+    } else {
+#pragma unroll
+      for (int s = 0; s < CH; ++s) {
+        if (c0 + s >= cnt) goto done;
+        entry(s, c0 + s);
+      }
     }
     C0 = C1;
     C1 = chunk(c0 / CH + 2);
@@ -424,6 +412,11 @@ done:
   __builtin_amdgcn_s_waitcnt(0x0F70);
   publish(pend0, pv0, lane);
   publish(pend1, pv1, lane);
+#ifdef MFHIP_DET_PROBE
+  if (blockIdx.x == 0 && lane == 0)
+    printf("[det probe] wave 0: %lld entries, cycles per entry: pre-fold %.0f fold %.0f post-fold %.0f prefetch %.0f\n",
+           (long long)cnt, double(pc[0]) / cnt, double(pc[1]) / cnt, double(pc[2]) / cnt, double(pc[3]) / cnt);
+#endif
 }
 
 template <int KPL>
