@@ -251,16 +251,19 @@ template <int KPL, int D, bool PRE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_sweep_pair_sys(
     const SysWave* __restrict__ sw, const WaveDesc* __restrict__ sys, int nw, int lbase, const u4v* __restrict__ recs,
     float* __restrict__ U, float* __restrict__ I, uint64_t u_bytes, uint64_t i_bytes, float eta,
-    int32_t* __restrict__ prog, uint32_t base, int32_t* __restrict__ err, uint64_t* __restrict__ trace, int prio) {
+    int32_t* __restrict__ prog, uint32_t base, int32_t* __restrict__ err, uint64_t* __restrict__ trace, int prio,
+    const int32_t* __restrict__ place) {
   const int lane = threadIdx.x;
   // blocks b and b+8 share an XCD: give each XCD a contiguous range of waves, so most hand-offs
   // (g+1 -> g) stay inside one L2 (speed only; correctness does not depend on it).  XCD x holds
   // nw/8 blocks, plus one when x < nw%8: a bijection for any nw.  sw = this launch's waves, the
   // superstep's waves from lbase on (progress words and SysWave::nbr count from the superstep's
   // first wave).
+  // place (host-made, sys_placement): the same XCD ranges, permuted inside an XCD so that the
+  // heaviest waves get the CUs with the fewest other waves (blocks k, k+32, k+64 of an XCD share a CU)
   const int b = static_cast<int>(blockIdx.x);
   const int x = b % 8, per = nw / 8, extra = nw % 8;
-  const int L = x * per + min(x, extra) + b / 8;
+  const int L = place ? place[b] : x * per + min(x, extra) + b / 8;
   const SysWave w = sw[L];
   const WaveDesc* my = sys + w.cell0;
   int32_t* my_prog = prog + static_cast<int64_t>(lbase + L) * kProgStride;
@@ -353,15 +356,15 @@ bool cell_preload(int kpl) {
 template <int KPL>
 void dispatch_sys(hipStream_t st, const SysWave* sw, const WaveDesc* sys, int nw, int lbase, const PairRec* recs,
                   float* U, float* I, uint64_t ub, uint64_t ib, float eta, int32_t* prog, uint32_t base, int32_t* err,
-                  uint64_t* trace, hipEvent_t ev0, hipEvent_t ev1, int prio) {
+                  uint64_t* trace, hipEvent_t ev0, hipEvent_t ev1, int prio, const int32_t* place) {
   if (cell_preload(KPL))
     hipExtLaunchKernelGGL((k_sweep_pair_sys<KPL, kPairRing, true>), dim3(static_cast<unsigned>(nw)), dim3(64), 0, st,
                           ev0, ev1, 0, sw, sys, nw, lbase, reinterpret_cast<const u4v*>(recs), U, I, ub, ib, eta, prog,
-                          base, err, trace, prio);
+                          base, err, trace, prio, place);
   else
     hipExtLaunchKernelGGL((k_sweep_pair_sys<KPL, kPairRing, false>), dim3(static_cast<unsigned>(nw)), dim3(64), 0, st,
                           ev0, ev1, 0, sw, sys, nw, lbase, reinterpret_cast<const u4v*>(recs), U, I, ub, ib, eta, prog,
-                          base, err, trace, prio);
+                          base, err, trace, prio, place);
 }
 
 template <int KPL>
@@ -393,9 +396,9 @@ int sweep_pair_sys_capacity(int k) {
 void launch_sweep_pair_sys(hipStream_t st, const SysWave* sw, const WaveDesc* sys, int nw, int lbase,
                            const PairRec* recs, float* U, float* I, uint64_t u_bytes, uint64_t i_bytes, int k, float eta,
                            int32_t* prog, uint32_t base, int32_t* err, uint64_t* trace, hipEvent_t ev0, hipEvent_t ev1,
-                           int prio) {
+                           int prio, const int32_t* place) {
   if (nw <= 0) return;
-#define MF_SYS(KPL) dispatch_sys<KPL>(st, sw, sys, nw, lbase, recs, U, I, u_bytes, i_bytes, eta, prog, base, err, trace, ev0, ev1, prio)
+#define MF_SYS(KPL) dispatch_sys<KPL>(st, sw, sys, nw, lbase, recs, U, I, u_bytes, i_bytes, eta, prog, base, err, trace, ev0, ev1, prio, place)
   switch (k) {
     case 64: MF_SYS(1); break;
     case 128: MF_SYS(2); break;

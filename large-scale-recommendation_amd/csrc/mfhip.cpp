@@ -93,6 +93,7 @@ struct Shard {
   std::vector<int64_t> st_sub_off;
   std::vector<WaveDesc> st_waves_host;  // kept only when tracing
   DevBuf st_sys, st_sysw;               // systolic pair tables (PairPlan::sys, sys_waves)
+  DevBuf st_place;                      // per systolic wave slot: block -> wave of its launch (sys_placement)
   std::vector<int64_t> st_sys_off;      // PairPlan::sys_off
   std::vector<WaveDesc> st_sys_host;    // kept only when tracing
   std::vector<SysWave> st_sysw_host;    // kept only when tracing
@@ -612,6 +613,47 @@ void det_superstep(mf_ctx* ctx, Shard& s, int64_t superstep, int32_t iteration, 
   ctx->stats.moved_bytes += static_cast<double>(lp.entries.size()) * (32.0 * ctx->P.num_factors + 32.0);
 }
 
+// Block -> wave map of one systolic launch (waves [a, z) of a superstep whose waves start at w0 in
+// pp.sys_waves), written to place[w0 + a + b].  Measured (profiles/r03_placement_NFLX.txt): the
+// dispatcher deals a launch's blocks round-robin over the 8 XCDs (b % 8) and, inside an XCD, over
+// its 32 CUs in block order, so the XCD's blocks k, k + 32, k + 64 (k = b / 8) share a CU -- every
+// one of 4768 block pairs (b, b + 256) in two traced fits did.  And a wave's pair step slows with
+// every other busy wave on its CU (NFLX single-run pairs: 127 ns alone, 173 ns with one other
+// wave, 206 ns with two; mixed pairs 214 / 248 ns): the CU's shared vector-memory path, not the
+// SIMD (no two waves ever shared one).  So each XCD keeps its contiguous wave range (the hand-offs
+// stay in one L2), and inside it the heaviest waves (modelled time) take the CUs that hold the
+// fewest waves, with the lightest waves as their partners.  Placement only: results are
+// identical (tests compare with the per-sub-step launches bit for bit).  MFHIP_SYS_PLACE=0: the
+// plain XCD-contiguous map.
+void sys_placement(const PairPlan& pp, int64_t w0, int64_t a, int64_t z, std::vector<int32_t>& place) {
+  const int64_t nw = z - a;
+  if (nw <= 0) return;
+  std::vector<double> load(nw, 0.0);
+  for (int64_t L = 0; L < nw; ++L) {
+    const SysWave& sw = pp.sys_waves[w0 + a + L];
+    for (int32_t t = 0; t < sw.G; ++t) {
+      const WaveDesc& d = pp.sys[sw.cell0 + t];
+      if (d.steps > 0) load[L] += 2000.0 + d.steps * (d.cells == kWaveSingleRun ? 171.0 : 218.0);
+    }
+  }
+  const int64_t per = nw / 8, extra = nw % 8;
+  for (int64_t x = 0; x < 8; ++x) {
+    const int64_t n = per + (x < extra ? 1 : 0), base = x * per + std::min(x, extra);
+    if (n == 0) continue;
+    std::vector<int64_t> byload(n);  // this XCD's waves, heaviest first
+    std::iota(byload.begin(), byload.end(), base);
+    std::stable_sort(byload.begin(), byload.end(), [&](int64_t u, int64_t v) { return load[u] > load[v]; });
+    std::vector<int64_t> cus(std::min<int64_t>(n, 32));  // CU slots, fewest waves first
+    std::iota(cus.begin(), cus.end(), 0);
+    auto members = [&](int64_t c) { return (n - c + 31) / 32; };
+    std::stable_sort(cus.begin(), cus.end(), [&](int64_t u, int64_t v) { return members(u) < members(v); });
+    int64_t hi = 0, lo = n - 1;
+    for (int64_t c : cus)
+      for (int64_t kk = c, m = 0; kk < n; kk += 32, ++m)
+        place[w0 + a + x + 8 * kk] = static_cast<int32_t>(m == 0 ? byload[hi++] : byload[lo--]);
+  }
+}
+
 void fast_superstep(mf_ctx* ctx, Shard& s, int64_t superstep, double eta) {
   const int32_t n = ctx->nb;
   const int64_t smod = (superstep - 1) % n;
@@ -636,7 +678,8 @@ void fast_superstep(mf_ctx* ctx, Shard& s, int64_t superstep, double eta) {
                             static_cast<int>(a), s.st_recs.as<PairRec>(), s.uf.as<float>(), s.itf.as<float>(),
                             s.uf.bytes(), s.itf.bytes(), ctx->P.num_factors, static_cast<float>(eta),
                             s.fast_prog.as<int32_t>(), s.sys_base, s.fast_err.as<int32_t>(),
-                            s.st_trace.get() ? s.st_trace.as<uint64_t>() : nullptr, tm.start(), tm.stop(), ctx->hot_prio);
+                            s.st_trace.get() ? s.st_trace.as<uint64_t>() : nullptr, tm.start(), tm.stop(), ctx->hot_prio,
+                            s.st_place.get() ? s.st_place.as<int32_t>() + w0 + a : nullptr);
       ctx->stats.kernel_launches += 1;
     };
     if (ctx->ring_overlap) {
@@ -1308,6 +1351,23 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
                              hipMemcpyHostToDevice));
           s.st_sys_off = pp.sys_off;
           s.st_sys_block_off = pp.sys_block_off;
+          s.st_place.release();
+          if (!(std::getenv("MFHIP_SYS_PLACE") && std::string(std::getenv("MFHIP_SYS_PLACE")) == "0") &&
+              !pp.sys_waves.empty()) {
+            std::vector<int32_t> place(pp.sys_waves.size(), 0);
+            for (int32_t sm = 0; sm < ctx->nb; ++sm) {
+              const int64_t w0 = pp.sys_off[sm], nw = pp.sys_off[sm + 1] - w0;
+              if (ctx->ring_overlap) {  // the two launches of fast_superstep
+                const int64_t split = pp.sys_block_off[static_cast<size_t>(sm) * (ctx->c + 1) + ctx->c - 1];
+                sys_placement(pp, w0, 0, split, place);
+                sys_placement(pp, w0, split, nw, place);
+              } else {
+                sys_placement(pp, w0, 0, nw, place);
+              }
+            }
+            s.st_place.alloc(place.size() * sizeof(int32_t));
+            MF_HIP(hipMemcpy(s.st_place.get(), place.data(), place.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+          }
           s.sys_step = static_cast<uint32_t>(fp.G) + 1u;
           int64_t max_waves = 1;
           for (int32_t sm = 0; sm < ctx->nb; ++sm) max_waves = std::max(max_waves, pp.sys_off[sm + 1] - pp.sys_off[sm]);
