@@ -91,7 +91,7 @@ void launch_split_join(hipStream_t st, const SplitItem* sp, int n, float* I, int
 void launch_sweep_pair_sys(hipStream_t st, const SysWave* sw, const WaveDesc* sys, int nw, int lbase,
                            const PairRec* recs, float* U, float* I, uint64_t u_bytes, uint64_t i_bytes, int k, float eta,
                            int32_t* prog, uint32_t base, int32_t* err, uint64_t* trace, hipEvent_t ev0, hipEvent_t ev1,
-                           int prio = 0, const int32_t* place = nullptr);
+                           const int32_t* place = nullptr);
 
 // Deterministic persistent sweep (kernels_detsweep.hip): one launch per superstep, nw waves of
 // 64 lanes, all of which must be resident at once (nw <= det_sweep_capacity(k)).  Entries are

@@ -251,7 +251,7 @@ template <int KPL, int D, bool PRE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_sweep_pair_sys(
     const SysWave* __restrict__ sw, const WaveDesc* __restrict__ sys, int nw, int lbase, const u4v* __restrict__ recs,
     float* __restrict__ U, float* __restrict__ I, uint64_t u_bytes, uint64_t i_bytes, float eta,
-    int32_t* __restrict__ prog, uint32_t base, int32_t* __restrict__ err, uint64_t* __restrict__ trace, int prio,
+    int32_t* __restrict__ prog, uint32_t base, int32_t* __restrict__ err, uint64_t* __restrict__ trace,
     const int32_t* __restrict__ place) {
   const int lane = threadIdx.x;
   // blocks b and b+8 share an XCD: give each XCD a contiguous range of waves, so most hand-offs
@@ -267,11 +267,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   const SysWave w = sw[L];
   const WaveDesc* my = sys + w.cell0;
   int32_t* my_prog = prog + static_cast<int64_t>(lbase + L) * kProgStride;
-  int32_t* nb_prog = prog + static_cast<int64_t>(w.nbr & ~kSysCritical) * kProgStride;
+  int32_t* nb_prog = prog + static_cast<int64_t>(w.nbr) * kProgStride;
   const __amdgpu_buffer_rsrc_t urs = raw_rsrc(U, u_bytes), irs = raw_rsrc(I, i_bytes);
-  // issue priority on the critical path (MFHIP_HOT_PRIO): 1 = single-run cells, 2 = the superstep's
-  // busiest wave; VALU issue between two waves of a SIMD goes by priority, then age
-  if (prio == 2 && (w.nbr & kSysCritical)) __builtin_amdgcn_s_setprio(3);
   const uint32_t vlane = static_cast<uint32_t>(lane) * 64u;
   auto first_chunks = [&](const WaveDesc& c, ChunkRaw& A, ChunkRaw& B) {  // an empty cell reads nothing
     const __amdgpu_buffer_rsrc_t rr = cell_records(recs, c.base, c.steps);
@@ -303,11 +300,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     const uint64_t c_start = __builtin_amdgcn_s_memrealtime();
     uint64_t c_clk = trace ? __builtin_amdgcn_s_memtime() : 0;
     uint64_t wait_clk = 0;
-    const bool hot = prio == 1 && d.cells == kWaveSingleRun;
-    if (hot) __builtin_amdgcn_s_setprio(3);
     if (!PRE && d.steps > 0) first_chunks(d, L0, L1);
     if (d.steps > 0) pair_cell<KPL, D, kSC1>(d, L0, L1, recs, urs, irs, eta, lane, wait_clk);
-    if (hot) __builtin_amdgcn_s_setprio(0);
     if (PRE) {
       first_chunks(dn, L0, L1);
       __builtin_amdgcn_s_waitcnt(0x0F78);  // vmcnt(8): the 8 loads above may fly, every older store has landed
@@ -356,15 +350,15 @@ bool cell_preload(int kpl) {
 template <int KPL>
 void dispatch_sys(hipStream_t st, const SysWave* sw, const WaveDesc* sys, int nw, int lbase, const PairRec* recs,
                   float* U, float* I, uint64_t ub, uint64_t ib, float eta, int32_t* prog, uint32_t base, int32_t* err,
-                  uint64_t* trace, hipEvent_t ev0, hipEvent_t ev1, int prio, const int32_t* place) {
+                  uint64_t* trace, hipEvent_t ev0, hipEvent_t ev1, const int32_t* place) {
   if (cell_preload(KPL))
     hipExtLaunchKernelGGL((k_sweep_pair_sys<KPL, kPairRing, true>), dim3(static_cast<unsigned>(nw)), dim3(64), 0, st,
                           ev0, ev1, 0, sw, sys, nw, lbase, reinterpret_cast<const u4v*>(recs), U, I, ub, ib, eta, prog,
-                          base, err, trace, prio, place);
+                          base, err, trace, place);
   else
     hipExtLaunchKernelGGL((k_sweep_pair_sys<KPL, kPairRing, false>), dim3(static_cast<unsigned>(nw)), dim3(64), 0, st,
                           ev0, ev1, 0, sw, sys, nw, lbase, reinterpret_cast<const u4v*>(recs), U, I, ub, ib, eta, prog,
-                          base, err, trace, prio, place);
+                          base, err, trace, place);
 }
 
 template <int KPL>
@@ -396,9 +390,9 @@ int sweep_pair_sys_capacity(int k) {
 void launch_sweep_pair_sys(hipStream_t st, const SysWave* sw, const WaveDesc* sys, int nw, int lbase,
                            const PairRec* recs, float* U, float* I, uint64_t u_bytes, uint64_t i_bytes, int k, float eta,
                            int32_t* prog, uint32_t base, int32_t* err, uint64_t* trace, hipEvent_t ev0, hipEvent_t ev1,
-                           int prio, const int32_t* place) {
+                           const int32_t* place) {
   if (nw <= 0) return;
-#define MF_SYS(KPL) dispatch_sys<KPL>(st, sw, sys, nw, lbase, recs, U, I, u_bytes, i_bytes, eta, prog, base, err, trace, ev0, ev1, prio, place)
+#define MF_SYS(KPL) dispatch_sys<KPL>(st, sw, sys, nw, lbase, recs, U, I, u_bytes, i_bytes, eta, prog, base, err, trace, ev0, ev1, place)
   switch (k) {
     case 64: MF_SYS(1); break;
     case 128: MF_SYS(2); break;

@@ -148,7 +148,6 @@ struct mf_ctx {
   // MFHIP_ITEM_SPLIT=m sweeps an item with more than m ratings in one rating block as ceil(r / m)
   // chains averaged when the superstep ends (read at prepare; 0 / unset = off)
   int32_t item_split = 0;
-  int32_t hot_prio = 0;  // MFHIP_HOT_PRIO (experiment): raised issue priority on the critical path
   std::vector<int64_t> fast_rb_size;  // per rating block (fast mode)
   mf_stats stats{};
   bool profiling = false;
@@ -678,7 +677,7 @@ void fast_superstep(mf_ctx* ctx, Shard& s, int64_t superstep, double eta) {
                             static_cast<int>(a), s.st_recs.as<PairRec>(), s.uf.as<float>(), s.itf.as<float>(),
                             s.uf.bytes(), s.itf.bytes(), ctx->P.num_factors, static_cast<float>(eta),
                             s.fast_prog.as<int32_t>(), s.sys_base, s.fast_err.as<int32_t>(),
-                            s.st_trace.get() ? s.st_trace.as<uint64_t>() : nullptr, tm.start(), tm.stop(), ctx->hot_prio,
+                            s.st_trace.get() ? s.st_trace.as<uint64_t>() : nullptr, tm.start(), tm.stop(),
                             s.st_place.get() ? s.st_place.as<int32_t>() + w0 + a : nullptr);
       ctx->stats.kernel_launches += 1;
     };
@@ -1111,8 +1110,6 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
   PhaseClock clk;
   ctx->item_split = 0;
   if (const char* v = std::getenv("MFHIP_ITEM_SPLIT")) ctx->item_split = std::max(0, std::atoi(v));
-  ctx->hot_prio = 0;
-  if (const char* v = std::getenv("MFHIP_HOT_PRIO")) ctx->hot_prio = std::atoi(v);
   ctx->reaper.join();
   DevRatingBlocks dev_rb;  // the device copy of the rating blocks (full device schedule only)
   ctx->nb = std::max(1, ctx->P.num_blocks);
@@ -1336,15 +1333,6 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
           s.st_sys.alloc(std::max<size_t>(pp.sys.size(), 1) * sizeof(WaveDesc));
           if (!pp.sys.empty())
             MF_HIP(hipMemcpy(s.st_sys.get(), pp.sys.data(), pp.sys.size() * sizeof(WaveDesc), hipMemcpyHostToDevice));
-          for (int32_t sm = 0; sm < ctx->nb; ++sm) {  // each superstep's busiest wave (kSysCritical)
-            int64_t best = -1, most = -1;
-            for (int64_t w = pp.sys_off[sm]; w < pp.sys_off[sm + 1]; ++w) {
-              int64_t pairs = 0;
-              for (int32_t t = 0; t < pp.sys_waves[w].G; ++t) pairs += pp.sys[pp.sys_waves[w].cell0 + t].steps;
-              if (pairs > most) { most = pairs; best = w; }
-            }
-            if (best >= 0) pp.sys_waves[best].nbr |= kSysCritical;
-          }
           s.st_sysw.alloc(std::max<size_t>(pp.sys_waves.size(), 1) * sizeof(SysWave));
           if (!pp.sys_waves.empty())
             MF_HIP(hipMemcpy(s.st_sysw.get(), pp.sys_waves.data(), pp.sys_waves.size() * sizeof(SysWave),

@@ -273,9 +273,7 @@ struct PairRec {
 };
 static_assert(sizeof(PairRec) == 64, "PairRec is four 16-B words");
 // Systolic sweep wave: its G cells are PairPlan::sys[cell0 .. cell0+G), one per sub-step; it
-// waits on wave nbr (same superstep) -- item group g+1 of the same rating block.  kSysCritical in
-// nbr marks the superstep's busiest wave (its critical path), which may run at raised priority.
-constexpr int32_t kSysCritical = 1 << 30;
+// waits on wave nbr (same superstep) -- item group g+1 of the same rating block.
 struct SysWave {
   int64_t cell0;
   int32_t G;
