@@ -623,7 +623,9 @@ void det_superstep(mf_ctx* ctx, Shard& s, int64_t superstep, int32_t iteration, 
 // stay in one L2), and inside it the heaviest waves (modelled time) take the CUs that hold the
 // fewest waves, with the lightest waves as their partners.  Placement only: results are
 // identical (tests compare with the per-sub-step launches bit for bit).  MFHIP_SYS_PLACE=0: the
-// plain XCD-contiguous map.
+// plain XCD-contiguous map.  Measured and dropped: per-CU wave counts chosen against a crowding
+// factor (1 / 1.3 / 1.52 / 1.8 per waves on the CU), spare slots padded with empty blocks -- NFLX
+// 21.6 vs 21.3 ms, ML20M equal (profiles/r03_placement_NFLX.txt).
 void sys_placement(const PairPlan& pp, int64_t w0, int64_t a, int64_t z, std::vector<int32_t>& place) {
   const int64_t nw = z - a;
   if (nw <= 0) return;
