@@ -155,6 +155,11 @@ struct mf_ctx {
   bool order_dirty = true;
   int64_t init_seed = 0;      // seed of the initial factors (P.seed, or a random one when unseeded)
   std::string failed;         // non-empty: a device-side bound tripped; the fit must be prepared again
+  // deterministic sweep: the next run's first supersteps, built on worker threads when a run ends
+  // (a superstep's schedule depends only on its number and the training data): det_spec_s[slot] =
+  // the superstep built into det_buf[slot], -1 = none (det_spec_wait joins them)
+  std::future<void> det_spec[mfhip::kDetSlots];
+  int64_t det_spec_s[mfhip::kDetSlots] = {-1, -1, -1};
 };
 
 namespace mfhip {
@@ -420,7 +425,26 @@ void dump_wave_trace(mf_ctx* ctx) {
   if (f) std::fclose(f);
 }
 
+// Joins the speculative builds of det_run.  invalidate: the training data, the layouts or the
+// superstep changes, so the builds are dropped (otherwise a later run may still use them).
+void det_spec_wait(mf_ctx* ctx, bool invalidate) {
+  std::exception_ptr first;
+  for (int slot = 0; slot < kDetSlots; ++slot) {
+    if (ctx->det_spec[slot].valid()) {
+      try {
+        ctx->det_spec[slot].get();
+      } catch (...) {
+        if (!first) first = std::current_exception();
+        ctx->det_spec_s[slot] = -1;
+      }
+    }
+    if (invalidate) ctx->det_spec_s[slot] = -1;
+  }
+  if (first) std::rethrow_exception(first);
+}
+
 void sync_all(mf_ctx* ctx) {
+  det_spec_wait(ctx, false);
   for (auto& s : ctx->shards) {
     DeviceGuard g(s.device);
     MF_HIP(hipStreamSynchronize(s.stream));
@@ -946,15 +970,28 @@ void det_run(mf_ctx* ctx, int64_t count) {
       db.pending = false;
     }
   };
-  for (int slot = 0; slot < kDetSlots; ++slot) reclaim(slot);  // a previous call's last copies
   std::future<void> builds[kDetSlots];
   constexpr int kAhead = kDetSlots - 1;  // supersteps built ahead of the one launched
+  // the previous run's speculative builds of supersteps s0, s0+1 (slots 0, 1) are taken over;
+  // any other is joined and dropped
+  bool prebuilt[kDetSlots] = {false, false, false};
+  for (int slot = 0; slot < kDetSlots; ++slot) {
+    if (slot < kAhead && slot < count && ctx->det_spec_s[slot] == s0 + slot) {
+      builds[slot] = std::move(ctx->det_spec[slot]);  // invalid when sync_all already joined it
+      prebuilt[slot] = true;
+    } else if (ctx->det_spec[slot].valid()) {
+      ctx->det_spec[slot].get();
+    }
+    ctx->det_spec_s[slot] = -1;
+  }
+  for (int slot = 0; slot < kDetSlots; ++slot) reclaim(slot);  // a previous call's last copies
   for (int64_t x = 0; x < std::min<int64_t>(count, kAhead); ++x)
-    builds[x % kDetSlots] = std::async(std::launch::async, det_build, ctx, s0 + x, static_cast<int>(x % kDetSlots));
+    if (!prebuilt[x % kDetSlots])
+      builds[x % kDetSlots] = std::async(std::launch::async, det_build, ctx, s0 + x, static_cast<int>(x % kDetSlots));
   for (int64_t x = 0; x < count; ++x) {
     const int64_t s = s0 + x;
     const int slot = static_cast<int>(x % kDetSlots);
-    builds[slot].get();
+    if (builds[slot].valid()) builds[slot].get();
     const int32_t iteration = static_cast<int32_t>(s / ctx->nb);  // :476
     const double eta = learning_rate(ctx->P.lr_method, ctx->P.learning_rate, iteration + 1, ctx->P.lambda,
                                      ctx->P.lr_arg);  // :383-386
@@ -1004,6 +1041,22 @@ void det_run(mf_ctx* ctx, int64_t count) {
     }
   }
   ctx->stats.algorithmic_bytes = static_cast<double>(ctx->stats.updates) * bytes_per_update(ctx);
+  // the next run's first supersteps, built while the caller syncs, evaluates or returns: a run's
+  // start no longer waits for its first host build (~36 ms of an NFLX call before).  A builder
+  // first waits for the staging copy that last read its slot's pinned buffer.
+  for (int64_t x = 0; x < kAhead; ++x) {
+    const int slot = static_cast<int>(x);
+    const int64_t s = s0 + count + x;
+    ctx->det_spec[slot] = std::async(std::launch::async, [ctx, slot, s] {
+      for (auto& sh : ctx->shards) {
+        if (!sh.det_buf[slot].copied) continue;
+        DeviceGuard g(sh.device);
+        MF_HIP(hipEventSynchronize(sh.det_buf[slot].copied));
+      }
+      det_build(ctx, s, slot);
+    });
+    ctx->det_spec_s[slot] = s;
+  }
 }
 
 void run_supersteps(mf_ctx* ctx, int64_t count) {
@@ -1107,6 +1160,7 @@ void prepare_det_sweep(mf_ctx* ctx) {
 void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, int64_t n) {
   MF_REQUIRE(n >= 0, "negative rating count");
   MF_REQUIRE(n == 0 || (u && i && r), "null rating arrays");
+  det_spec_wait(ctx, true);
   ctx->failed.clear();
   sync_all(ctx);
   PhaseClock clk;
@@ -1966,6 +2020,10 @@ int mf_create_rank(const mf_params* p, int device_id, int nranks, int rank, cons
 int mf_destroy(mf_ctx* ctx) {
   return guarded([&] {
     if (!ctx) return;
+    try {
+      det_spec_wait(ctx, true);
+    } catch (...) {  // a failed speculative build only matters to a run that would have used it
+    }
     for (auto& s : ctx->shards) {
       DeviceGuard g(s.device);
       (void)hipStreamSynchronize(s.stream);
@@ -2003,6 +2061,7 @@ int mf_dsgd_set_superstep(mf_ctx* ctx, int64_t done) {
   return guarded([&] {
     MF_REQUIRE(ctx && done >= 0, "bad argument");
     MF_REQUIRE(ctx->prepared, "mf_dsgd_set_superstep before mf_dsgd_prepare");
+    det_spec_wait(ctx, true);
     sync_all(ctx);
     ctx->superstep_done = done;
     reset_item_loc(ctx);
@@ -2013,6 +2072,7 @@ int mf_dsgd_restart(mf_ctx* ctx) {
   return guarded([&] {
     MF_REQUIRE(ctx, "null context");
     MF_REQUIRE(ctx->prepared, "mf_dsgd_restart before mf_dsgd_prepare");
+    det_spec_wait(ctx, true);
     ctx->failed.clear();
     sync_all(ctx);
     init_factors(ctx);
@@ -2082,6 +2142,7 @@ int mf_set_factors(mf_ctx* ctx, int side, const int32_t* ids, const double* vecs
   return guarded([&] {
     MF_REQUIRE(ctx && (n == 0 || (ids && vecs)), "null argument");
     MF_REQUIRE(side == MF_SIDE_USER || side == MF_SIDE_ITEM, "bad side");
+    det_spec_wait(ctx, true);  // rows may be added: the layouts change
     if (!ctx->have_model) { ctx->U = SideLayout(); ctx->I = SideLayout(); ctx->have_model = true; }
     SideLayout& S = side_of(ctx, side);
     std::vector<int32_t> fresh;
@@ -2206,6 +2267,7 @@ int mf_online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const doub
                      int num_partitions, int64_t* touched_users, int64_t* touched_items) {
   return guarded([&] {
     MF_REQUIRE(ctx, "null context");
+    det_spec_wait(ctx, true);  // new ids change the layouts the builds read
     online_update(ctx, u, i, r, n, flavour, num_partitions, touched_users, touched_items);
   });
 }
@@ -2215,6 +2277,7 @@ int mf_online_update_out(mf_ctx* ctx, const int32_t* u, const int32_t* i, const 
                          double* item_out) {
   return guarded([&] {
     MF_REQUIRE(ctx, "null context");
+    det_spec_wait(ctx, true);  // new ids change the layouts the builds read
     online_update(ctx, u, i, r, n, flavour, num_partitions, touched_users, touched_items, user_out, item_out);
   });
 }
