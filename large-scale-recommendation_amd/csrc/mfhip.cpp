@@ -157,7 +157,8 @@ struct mf_ctx {
   std::string failed;         // non-empty: a device-side bound tripped; the fit must be prepared again
   // deterministic sweep: the next run's first supersteps, built on worker threads when a run ends
   // (a superstep's schedule depends only on its number and the training data): det_spec_s[slot] =
-  // the superstep built into det_buf[slot], -1 = none (det_spec_wait joins them)
+  // the superstep built into det_buf[slot], -1 = none (det_run takes them over; det_spec_wait
+  // joins them where the data, layouts or superstep change)
   std::future<void> det_spec[mfhip::kDetSlots];
   int64_t det_spec_s[mfhip::kDetSlots] = {-1, -1, -1};
 };
@@ -443,8 +444,9 @@ void det_spec_wait(mf_ctx* ctx, bool invalidate) {
   if (first) std::rethrow_exception(first);
 }
 
+// (does not wait for det_run's speculative builds: they touch no device state, and a caller's
+// sync must not pay for the next run's host work)
 void sync_all(mf_ctx* ctx) {
-  det_spec_wait(ctx, false);
   for (auto& s : ctx->shards) {
     DeviceGuard g(s.device);
     MF_HIP(hipStreamSynchronize(s.stream));
@@ -973,11 +975,11 @@ void det_run(mf_ctx* ctx, int64_t count) {
   std::future<void> builds[kDetSlots];
   constexpr int kAhead = kDetSlots - 1;  // supersteps built ahead of the one launched
   // the previous run's speculative builds of supersteps s0, s0+1 (slots 0, 1) are taken over;
-  // any other is joined and dropped
+  // any other is joined and dropped (a taken-over build is waited for like the run's own)
   bool prebuilt[kDetSlots] = {false, false, false};
   for (int slot = 0; slot < kDetSlots; ++slot) {
     if (slot < kAhead && slot < count && ctx->det_spec_s[slot] == s0 + slot) {
-      builds[slot] = std::move(ctx->det_spec[slot]);  // invalid when sync_all already joined it
+      builds[slot] = std::move(ctx->det_spec[slot]);
       prebuilt[slot] = true;
     } else if (ctx->det_spec[slot].valid()) {
       ctx->det_spec[slot].get();
@@ -1041,8 +1043,8 @@ void det_run(mf_ctx* ctx, int64_t count) {
     }
   }
   ctx->stats.algorithmic_bytes = static_cast<double>(ctx->stats.updates) * bytes_per_update(ctx);
-  // the next run's first supersteps, built while the caller syncs, evaluates or returns: a run's
-  // start no longer waits for its first host build (~36 ms of an NFLX call before).  A builder
+  // the next run's first supersteps, built in the background while the caller syncs, evaluates or
+  // returns: a run's start no longer waits for its first host build (~36 ms of an NFLX call).  A builder
   // first waits for the staging copy that last read its slot's pinned buffer.
   for (int64_t x = 0; x < kAhead; ++x) {
     const int slot = static_cast<int>(x);
