@@ -138,6 +138,30 @@ def test_staged_run_and_resume_equal_one_shot():
             assert np.array_equal(ctx2.factors(side)[1], m.factors(side)[1])
 
 
+def test_staged_runs_take_over_prebuilt_supersteps():
+    """A deterministic run builds the next run's first supersteps ahead (mfhip.cpp det_run): staged runs of
+    1-3 supersteps each take them over, a restart or a factor upload drops them, and every path equals the
+    oracle's one-shot fit bit for bit."""
+    d = synth.generate(300, 150, 8000, seed=2)
+    m = coracle.dsgd_fit(d.u, d.i, d.r, k=16, iterations=3, n_blocks=3, seed=4)
+    with mfhip.Context(params(16, 3, 3, 4)) as ctx:
+        ctx.prepare(d.u, d.i, d.r)
+        for n in (2, 1, 3, 3):
+            ctx.run(n)
+        assert ctx.superstep == 9
+        for side in (0, 1):
+            assert np.array_equal(ctx.factors(side)[1], m.factors(side)[1])
+        ctx.restart()  # superstep 0 again: the builds made for superstep 10 are dropped
+        ctx.run(4)
+        uids, uv = ctx.factors(0)
+        iids, iv = ctx.factors(1)
+        ctx.set_factors(0, uids, uv)  # same values back: the layouts may change, builds are dropped
+        ctx.set_factors(1, iids, iv)
+        ctx.run(5)
+        for side in (0, 1):
+            assert np.array_equal(ctx.factors(side)[1], m.factors(side)[1])
+
+
 def test_snapshot_file_resume_bit_exact(tmp_path):
     """mf_save_model / mf_load_model (TemporaryPath persistence, DSGDforMF.scala:291-296, 330-349):
     4 supersteps, snapshot to disk, a fresh context resumes and finishes == the oracle's one-shot fit;
