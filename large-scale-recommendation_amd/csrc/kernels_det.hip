@@ -183,7 +183,10 @@ __global__ __launch_bounds__(64) void k_online_sweep(const int64_t* __restrict__
     const int32_t t2 = __hip_atomic_load(ticket + (n2 ? u2 : ur), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
     for (int c = 0; c < KPL; ++c) pr[c] = pv[c] * qv[c];
-    const T e = r - seq_fold<T, KPL>(pr, k, lds, lane);
+    T dot;
+    if constexpr (FULL) dot = seq_fold_dpp<T, KPL>(pr);  // registers + DPP, no LDS round trip
+    else dot = seq_fold<T, KPL>(pr, k, lds, lane);
+    const T e = r - dot;
     // the tickets are looked at before the stores (so no wait for them lands behind the stores)
     const bool g1 = n1 && u1 != ur && (q1 == 0 || __builtin_amdgcn_readfirstlane(t1) == q1);
     const bool g2 = n2 && u2 != ur && (q2 == 0 || __builtin_amdgcn_readfirstlane(t2) == q2);

@@ -25,8 +25,6 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
-#include <cstdlib>
-#include <string>
 
 #include "kernels.hpp"
 
@@ -121,139 +119,9 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70 & ~0xF);
 }
 
-// Per wave, entry j runs as (one memory-operation sequence per entry, no branch on the common
-// path, so the compiler's vmcnt bookkeeping stays exact):
-//   (a) prefetch entry j+1's user row -- if its ticket, polled at entry j-1, was ready; else an
-//       out-of-range offset (zeros, entry j+1 then waits and loads itself) -- and its item row
-//       unless j+1 keeps j's (issued after every earlier store of this wave: a wave reads its own
-//       earlier stores), load its two lambda / omega values, and poll entry j+2's ticket;
-//   (b) compute entry j from the rows prefetched at entry j-1 (the sequential dot via LDS);
-//   (c) wait only for entry j-1's stores (vmcnt(2*KPL + 3): (a)'s operations are younger) and
-//       publish entry j-1's ticket;
-//   (d) store entry j's user row and its item row unless entry j+1 keeps it.
-// So a row load overlaps one entry's compute and a store drain the next entry's.  A wave blocks
-// on a ticket only after publishing its own pending one, so no published ticket ever waits on a
-// blocked wave.
-template <int KPL>
-__global__ __launch_bounds__(64) void k_det_sweep(const DetWave* __restrict__ waves, const uint32_t* __restrict__ eu,
-                                                  const uint32_t* __restrict__ ei, const uint32_t* __restrict__ eq,
-                                                  const double* __restrict__ er, double* U, double* I,
-                                                  uint64_t u_bytes, uint64_t i_bytes, const double* __restrict__ regU,
-                                                  const double* __restrict__ regI, int k, double eta,
-                                                  int32_t* ticket, int32_t* dummy_ticket, int32_t* err) {
-  __shared__ __attribute__((aligned(16))) double lds[64 * KPL];
-  const int lane = threadIdx.x;
-  const DetWave d = waves[blockIdx.x];
-  const int64_t cnt = d.count;
-  if (cnt == 0) return;
-  dummy_ticket += 16 * static_cast<int64_t>(blockIdx.x);  // this wave's own scratch line
-  const __amdgpu_buffer_rsrc_t urs = raw_rsrc(U, u_bytes), irs = raw_rsrc(I, i_bytes);
-  uint32_t voff[KPL];
-#pragma unroll
-  for (int c = 0; c < KPL; ++c) voff[c] = lane + 64 * c < k ? static_cast<uint32_t>(lane + 64 * c) * 8u : 0x80000000u;
-  const uint32_t rowb = static_cast<uint32_t>(k) * 8u;
-
-  DetChunk C0 = det_chunk(eu, ei, eq, er, d.begin + lane);
-  DetChunk C1 = det_chunk(eu, ei, eq, er, d.begin + 64 + lane);
-  // field of entry (chunk-relative) s + dj, dj in {0, 1, 2}
-  auto fld = [&](uint32_t a0, uint32_t a1, int s, int dj) { return s + dj < 64 ? rl(a0, s + dj) : rl(a1, s + dj - 64); };
-
-  // entry 0 read synchronously; entry 1's ticket polled ahead
-  DRow<KPL> P, Q;
-  int32_t okP;
-  double RU, RI;
-  {
-    const uint32_t u0 = rl(C0.u, 0), i0 = rl(C0.i, 0), q0 = rl(C0.q, 0);
-    okP = poll(ticket + u0) == static_cast<int32_t>(q0 & kDetUseqMask);
-    P = ldrow<KPL>(urs, voff, okP ? u0 * rowb : kOOB);
-    Q = ldrow<KPL>(irs, voff, i0 * rowb);
-    RU = ld_sc1(regU + u0);
-    RI = ld_sc1(regI + i0);
-  }
-  int32_t tk1 = poll_issue(cnt > 1 ? ticket + rl(C0.u, 1) : dummy_ticket);
-  __builtin_amdgcn_s_waitcnt(0x0F70);
-  int32_t* pend = dummy_ticket;  // entry j-1's ticket word and value, published after its drain
-  int32_t pend_val = 0;
-  double q[KPL];
-#pragma unroll
-  for (int c = 0; c < KPL; ++c) q[c] = 0.0;
-
-  for (int64_t c0 = 0; c0 < cnt; c0 += 64) {
-    if (c0 > 0) {
-      C0 = C1;
-      C1 = det_chunk(eu, ei, eq, er, d.begin + c0 + 64 + lane);
-    }
-    const int n = static_cast<int>(min<int64_t>(64, cnt - c0));
-    for (int s = 0; s < n; ++s) {
-      const int64_t j = c0 + s;
-      const uint32_t u = rl(C0.u, s), i = rl(C0.i, s), qf = rl(C0.q, s);
-      const double r = rld(C0.r, s);
-      const int32_t useq = static_cast<int32_t>(qf & kDetUseqMask);
-      // (a) prefetch entry j+1, poll entry j+2
-      const bool live1 = j + 1 < cnt;
-      const uint32_t u1 = fld(C0.u, C1.u, s, 1), i1 = fld(C0.i, C1.i, s, 1), q1 = fld(C0.q, C1.q, s, 1);
-      const int32_t okN = live1 && __builtin_amdgcn_readfirstlane(tk1) == static_cast<int32_t>(q1 & kDetUseqMask);
-      const DRow<KPL> PN = ldrow<KPL>(urs, voff, okN ? u1 * rowb : kOOB);
-      const DRow<KPL> QN = ldrow<KPL>(irs, voff, live1 && !(q1 & kDetKeepQ) ? i1 * rowb : kOOB);
-      const int32_t tk2 = poll_issue(j + 2 < cnt ? ticket + fld(C0.u, C1.u, s, 2) : dummy_ticket);
-      // entry j+1's lambda / omega as vector loads: a scalar load here would be waited for at the
-      // dot's first LDS wait (lgkmcnt also counts SMEM)
-      const double RUN = ld_sc1(regU + (live1 ? u1 : 0u)), RIN = ld_sc1(regI + (live1 ? i1 : 0u));
-      // entry j's user row: prefetched, or (rarely) wait for its ticket now
-      if (!okP) {
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): entry j-1's stores landed
-        publish(pend, pend_val, lane);
-        pend = dummy_ticket;
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // bounded wait (100 MHz clock)
-        while (poll(ticket + u) != useq) {
-          if (poll(err) != 0) return;
-          if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {  // ~1 s: a producer never ran
-            if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-        P = ldrow<KPL>(urs, voff, u * rowb);
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // waited here, so the fast path's waits stay counted
-      }
-      // (b) compute
-      if (!(qf & kDetKeepQ)) {
-#pragma unroll
-        for (int c = 0; c < KPL; ++c) q[c] = Q.v[c];
-      }
-      const double ru = uniform(RU), ri = uniform(RI);  // lambda / omega, prefetched with the rows
-      double pr[KPL], pn[KPL];
-#pragma unroll
-      for (int c = 0; c < KPL; ++c) pr[c] = P.v[c] * q[c];
-      const double e = r - seq_fold<double, KPL>(pr, k, lds, lane);  // :405
-#pragma unroll
-      for (int c = 0; c < KPL; ++c) {
-        pn[c] = P.v[c] - eta * (ru * P.v[c] - e * q[c]);  // :407-408
-        q[c] = q[c] - eta * (ri * q[c] - e * P.v[c]);     // :409-410 (old p)
-      }
-      // (c) entry j-1's stores have landed: publish its ticket
-      wait_vmcnt<2 * KPL + 3>();
-      publish(pend, pend_val, lane);
-      // (d) stores
-      strow<KPL>(urs, voff, u * rowb, pn);
-      strow<KPL>(irs, voff, (qf & kDetDeferQ) ? kOOB : i * rowb, q);
-      pend = ticket + u;
-      pend_val = useq + 1;
-      P = PN;
-      Q = QN;
-      RU = RUN;
-      RI = RIN;
-      okP = okN;
-      tk1 = tk2;
-    }
-  }
-  __builtin_amdgcn_s_waitcnt(0x0F70);
-  publish(pend, pend_val, lane);
-}
-
-// k_det_sweep2: the same schedule, entry order and arithmetic as k_det_sweep (bitwise the same
-// factors), with a deeper pipeline for the per-item chains (the hot item's wave is the superstep's
-// critical path: ~26k chained updates per NFLX superstep):
+// k_det_sweep2: per wave, the entries of its items in shuffled order, with a two-deep pipeline for
+// the per-item chains (the hot item's wave is the superstep's critical path: ~26k chained updates
+// per NFLX superstep):
 //   * entries in chunks of kDetChunk with the entry index inside a chunk a compile-time constant
 //     (unrolled), so every field is a v_readlane with a constant lane and the body is straight-line
 //     code whose wait counts the compiler tracks exactly;
@@ -264,11 +132,14 @@ __global__ __launch_bounds__(64) void k_det_sweep(const DetWave* __restrict__ wa
 //   * a ticket is published TWO entries late: entry j waits only for entry j-2's stores
 //     (vmcnt(6 KPL + 7): the operations issued after them), so a store's write-through latency
 //     overlaps two entries of compute.  A wave publishes every pending ticket before it blocks on
-//     one, so the no-deadlock argument of k_det_sweep holds unchanged.
+//     one, so no published ticket ever waits on a blocked wave and the unfinished entry with the
+//     smallest shuffle position stays runnable (no deadlock with every wave resident);
+//   * FULL (k == 64 KPL): the dot's sequential fold in registers (seq_fold_dpp: permlane swaps and
+//     DPP broadcasts, ~6.6 instead of ~11-13 cycles per f64 add), else through LDS (seq_fold).
 constexpr int kDetChunk = 16;
 
 
-template <int KPL>
+template <int KPL, bool FULL>
 __global__ __launch_bounds__(64) void k_det_sweep2(const DetWave* __restrict__ waves, const uint32_t* __restrict__ eu,
                                                    const uint32_t* __restrict__ ei, const uint32_t* __restrict__ eq,
                                                    const double* __restrict__ er, double* U, double* I,
@@ -358,7 +229,10 @@ __global__ __launch_bounds__(64) void k_det_sweep2(const DetWave* __restrict__ w
 #pragma unroll
     for (int c = 0; c < KPL; ++c) pr[c] = P[slot].v[c] * q[c];
     stamp(0);
-    const double e = r - seq_fold<double, KPL>(pr, k, lds, lane);  // :405
+    double dot;
+    if constexpr (FULL) dot = seq_fold_dpp<double, KPL>(pr);
+    else dot = seq_fold<double, KPL>(pr, k, lds, lane);
+    const double e = r - dot;  // :405
     stamp(1);
 #pragma unroll
     for (int c = 0; c < KPL; ++c) {
@@ -420,25 +294,23 @@ done:
 }
 
 template <int KPL>
-int det_capacity() {
+int det_capacity(bool full) {
   int dev = 0, cus = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-  int a = 0, b = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, k_det_sweep<KPL>, 64, 0) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_det_sweep2<KPL>, 64, 0) != hipSuccess)
-    return 0;
-  per_cu = a < b ? a : b;
-  return cus * per_cu;
+  const hipError_t st = full ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_det_sweep2<KPL, true>, 64, 0)
+                             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_det_sweep2<KPL, false>, 64, 0);
+  return st == hipSuccess ? cus * per_cu : 0;
 }
 
 }  // namespace
 
+// the co-resident wave count of the instance launch_det_sweep picks for k
 int det_sweep_capacity(int k) {
-  if (k <= 64) return det_capacity<1>();
-  if (k <= 128) return det_capacity<2>();
-  if (k <= 256) return det_capacity<4>();
-  return det_capacity<8>();
+  if (k <= 64) return det_capacity<1>(k == 64);
+  if (k <= 128) return det_capacity<2>(k == 128);
+  if (k <= 256) return det_capacity<4>(k == 256);
+  return det_capacity<8>(k == 512);
 }
 
 void launch_det_sweep(hipStream_t st, const DetWave* waves, int nw, const uint32_t* eu, const uint32_t* ei,
@@ -447,16 +319,14 @@ void launch_det_sweep(hipStream_t st, const DetWave* waves, int nw, const uint32
                       int32_t* dummy_ticket, int32_t* err, hipEvent_t ev0, hipEvent_t ev1) {
   if (nw <= 0) return;
   const dim3 g(static_cast<unsigned>(nw)), b(64);
-  // MFHIP_DET_SWEEP=1: the one-entry-deep pipeline (k_det_sweep), for A/B
-  static const bool deep = [] { const char* v = std::getenv("MFHIP_DET_SWEEP"); return !(v && std::string(v) == "1"); }();
 #define MF_DET(KPL)                                                                                                  \
   do {                                                                                                               \
-    if (deep)                                                                                                        \
-      hipExtLaunchKernelGGL((k_det_sweep2<KPL>), g, b, 0, st, ev0, ev1, 0, waves, eu, ei, eq, er, U, I, u_bytes,     \
+    if (k == 64 * (KPL))                                                                                             \
+      hipExtLaunchKernelGGL((k_det_sweep2<KPL, true>), g, b, 0, st, ev0, ev1, 0, waves, eu, ei, eq, er, U, I, u_bytes, \
                             i_bytes, regU, regI, k, eta, ticket, dummy_ticket, err);                                 \
     else                                                                                                             \
-      hipExtLaunchKernelGGL((k_det_sweep<KPL>), g, b, 0, st, ev0, ev1, 0, waves, eu, ei, eq, er, U, I, u_bytes,      \
-                            i_bytes, regU, regI, k, eta, ticket, dummy_ticket, err);                                 \
+      hipExtLaunchKernelGGL((k_det_sweep2<KPL, false>), g, b, 0, st, ev0, ev1, 0, waves, eu, ei, eq, er, U, I,       \
+                            u_bytes, i_bytes, regU, regI, k, eta, ticket, dummy_ticket, err);                        \
   } while (0)
   if (k <= 64) MF_DET(1);
   else if (k <= 128) MF_DET(2);

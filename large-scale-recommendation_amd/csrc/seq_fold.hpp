@@ -31,6 +31,83 @@ __device__ __forceinline__ T lane0_value(T v) {
   }
 }
 
+// The same fold with no LDS round trip, for k == 64 * KPL.  A single wave issues at most one LDS
+// read every ~24 cycles (profiles/r04_fold_microbench.txt: 12-13 cycles per f64 add whatever the
+// read width, window or EXEC), so the operands are brought to row 0 (lanes 0-15) in registers
+// instead: v_permlane16_swap / v_permlane32_swap copy rows 1-3 of each product register to row 0
+// of three more registers (3 swaps per dword), then every add reads its operand straight from the
+// register file through DPP row_newbcast:n (lane n of the row, the only DPP mode the f64 ALU
+// has).  f64 has no v_add_f64_dpp, so the add is v_fmac_f64_dpp acc, x, 1.0: x * 1.0 is exact, so
+// fma(x, 1.0, acc) is the single rounding of acc + x -- bitwise the add.  Element 64c + 16r + n is
+// register (c, r), lane n: the adds run f = 0, 1, ..., 64 KPL - 1 in order.  Every lane of row 0
+// ends with the sum (rows 1-3 hold garbage); returned as a wave-uniform value.
+// One dword d: rows 1, 2, 3 of d to row 0 of three registers, three swaps and no copies.  A swap
+// delivers one new row-0 value (into its second operand), so three per dword is the minimum; the
+// second operands start as don't-care registers (an empty asm defines them), since only their row
+// 0 after the swap is read.  swap16(a, b): b.row0 <- a.row1, b.row2 <- a.row3 (a keeps rows 0, 2);
+// swap32(a, b): b.rows0,1 <- a.rows2,3 (a keeps rows 0, 1).
+__device__ __forceinline__ void dword_views(unsigned d, unsigned (&v)[4]) {
+  unsigned t1, t2, t3;
+  asm volatile("" : "=v"(t1), "=v"(t2), "=v"(t3));
+  const auto s16 = __builtin_amdgcn_permlane16_swap(d, t1, false, false);   // s16[1].row0 = d.row1, .row2 = d.row3
+  const auto s32 = __builtin_amdgcn_permlane32_swap(s16[0], t2, false, false);  // s32[1].row0 = d.row2, s32[0].row0 = d.row0
+  const auto s3 = __builtin_amdgcn_permlane32_swap(s16[1], t3, false, false);   // s3[1].row0 = d.row3, s3[0].row0 = d.row1
+  v[0] = s32[0];
+  v[1] = s3[0];
+  v[2] = s32[1];
+  v[3] = s3[1];
+}
+template <typename T>
+__device__ __forceinline__ void row_views(T x, T (&v)[4]) {
+  if constexpr (sizeof(T) == 8) {
+    const unsigned long long b = static_cast<unsigned long long>(__double_as_longlong(x));
+    unsigned lo[4], hi[4];
+    dword_views(static_cast<unsigned>(b), lo);
+    dword_views(static_cast<unsigned>(b >> 32), hi);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      v[r] = __longlong_as_double(static_cast<long long>((static_cast<unsigned long long>(hi[r]) << 32) | lo[r]));
+  } else {
+    unsigned d[4];
+    dword_views(static_cast<unsigned>(__float_as_int(x)), d);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = __int_as_float(static_cast<int>(d[r]));
+  }
+}
+
+#define MFHIP_FOLD_D(R, N) "v_fmac_f64_dpp %0, %" #R ", %5 row_newbcast:" #N " row_mask:0xf bank_mask:0xf\n\t"
+#define MFHIP_FOLD_S(R, N) "v_add_f32_dpp %0, %" #R ", %0 row_newbcast:" #N " row_mask:0xf bank_mask:0xf\n\t"
+#define MFHIP_FOLD_ROW(M, R)                                                                         \
+  M(R, 0) M(R, 1) M(R, 2) M(R, 3) M(R, 4) M(R, 5) M(R, 6) M(R, 7) M(R, 8) M(R, 9) M(R, 10) M(R, 11) \
+      M(R, 12) M(R, 13) M(R, 14) M(R, 15)
+
+template <typename T, int KPL>
+__device__ __forceinline__ T seq_fold_dpp(const T (&prod)[KPL]) {
+  T acc = T(0);
+#pragma unroll
+  for (int c = 0; c < KPL; ++c) {
+    T v[4];
+    row_views<T>(prod[c], v);
+    // s_nop 1: the two wait states a DPP source needs after the VALU (swap) that wrote it
+    if constexpr (sizeof(T) == 8) {
+      const double one = 1.0;
+      asm volatile("s_nop 1\n\t" MFHIP_FOLD_ROW(MFHIP_FOLD_D, 1) MFHIP_FOLD_ROW(MFHIP_FOLD_D, 2)
+                       MFHIP_FOLD_ROW(MFHIP_FOLD_D, 3) MFHIP_FOLD_ROW(MFHIP_FOLD_D, 4)
+                   : "+v"(acc)
+                   : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(one));
+    } else {
+      asm volatile("s_nop 1\n\t" MFHIP_FOLD_ROW(MFHIP_FOLD_S, 1) MFHIP_FOLD_ROW(MFHIP_FOLD_S, 2)
+                       MFHIP_FOLD_ROW(MFHIP_FOLD_S, 3) MFHIP_FOLD_ROW(MFHIP_FOLD_S, 4)
+                   : "+v"(acc)
+                   : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));
+    }
+  }
+  return lane0_value(acc);
+}
+#undef MFHIP_FOLD_ROW
+#undef MFHIP_FOLD_S
+#undef MFHIP_FOLD_D
+
 template <typename T, int KPL, bool LANE0 = false>
 __device__ __forceinline__ T seq_fold(const T (&prod)[KPL], int k, T* lds, int lane) {
 #pragma unroll

@@ -175,7 +175,8 @@ def test_per_rating_outputs_bit_exact(flavour, name):
         ctx.online_update_out(u[:10], i[:10], r[:10], L.ONLINE_SPARK_SWEEP)
 
 
-@pytest.mark.parametrize("mode,k", [(L.MODE_FAST_F32, 128), (L.MODE_DETERMINISTIC_F64, 200), (L.MODE_FAST_F32, 40)])
+@pytest.mark.parametrize("mode,k", [(L.MODE_FAST_F32, 128), (L.MODE_DETERMINISTIC_F64, 200), (L.MODE_FAST_F32, 40),
+                                    (L.MODE_DETERMINISTIC_F64, 128), (L.MODE_DETERMINISTIC_F64, 64)])
 def test_online_sweep_equals_level_replay(monkeypatch, mode, k):
     """The one-launch online sweep (the default: per-item waves, per-user tickets, k_online_sweep,
     its wave lists and tickets built on the device by kernels_online.hip) gives the factors of the

@@ -1,0 +1,105 @@
+#!/bin/bash
+# One parameterised GPU runner for gpurun (replaces the per-experiment gpurun_*.sh scripts):
+#
+#   gpurun -- bash tools/gpu.sh <out-dir-name> <step> [<step> ...]
+#
+# Steps run in order, each under its own time limit; the first failure ends the call (nothing more
+# touches the GPU after a fault, an abort or a time limit).  Outputs go to gpurun_out/<out-dir-name>/.
+#   test:<pytest args>                     pytest -m gpu (one process), log test_<n>.log
+#   smoke                                  __graft_entry__.smoke()
+#   bench:<tag>:<bench.py args>            one bench line -> <tag>.json, summary printed
+#   ab:<tag>:<reps>:<envA>|<envB>[|...]:<bench.py args>
+#                                          alternating A/B of environment settings on the bench line
+#   prof:<tag>:<kernel>:<cfg>:<mode>:<rank>:<bench.py args>
+#                                          rocprofv3 --kernel-trace --stats, then separate --pmc FETCH_SIZE
+#                                          and --pmc WRITE_SIZE passes, summarised per launch of <kernel>
+#                                          (tools/pmc_summary.py) -> traffic_<tag>.json, stats_<tag>.csv
+#   micro:<src.hip>[:<hipcc flags>]        build a tools/micro benchmark and run it
+#   cmd:<shell command>                    anything else (300 s limit)
+set -o pipefail
+export TMPDIR=/tmp
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/${1:?out dir}
+shift
+mkdir -p "$O"
+cd "$R"
+n=0
+summ() {  # one-line summary of a bench JSON line
+  python3 - "$1" <<'EOF'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+r = d.get("roofline") or {}
+det = d.get("deterministic") or {}
+on = d.get("online") or {}
+s = f"{d['config']['workload']}: {d['value']/1e9:.3f} Gups {d['ms_per_step']} ms/step rmse {d.get('rmse')} rel {d.get('rmse_rel')}"
+if r: s += f" | launch {r.get('avg_launch_us')} us frac {r.get('frac')} traffic_frac {r.get('traffic_frac')}"
+if det: s += f" | det {det['value']/1e6:.1f} Mups {det['ms_per_step']} ms eq {det.get('rmse_equal_to_ref')} launch {det.get('avg_launch_us')} us cold {det.get('cold_fit_s')}"
+for key, v in on.items():
+    s += f" | online {key} {v['value']/1e6:.1f} M/s"
+print(s)
+EOF
+}
+for step in "$@"; do
+  n=$((n + 1))
+  kind=${step%%:*}
+  rest=${step#*:}
+  echo "== step $n: $step"
+  case $kind in
+    test)
+      timeout -k 10 1100 python -u -m pytest $rest -m gpu -v --timeout 300 --timeout-method thread > "$O/test_$n.log" 2>&1 \
+        || { echo "pytest failed"; grep -E "FAILED|Error|Timeout" "$O/test_$n.log" | head -20; tail -3 "$O/test_$n.log"; exit 1; }
+      tail -1 "$O/test_$n.log" ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$O/smoke.log" 2>&1 \
+        || { echo "smoke failed"; tail -5 "$O/smoke.log"; exit 1; }
+      tail -1 "$O/smoke.log" ;;
+    bench)
+      tag=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args=""
+      timeout -k 10 900 python bench.py $args > "$O/$tag.json" 2> "$O/$tag.err" \
+        || { echo "bench $tag failed"; tail -5 "$O/$tag.err"; exit 1; }
+      summ "$O/$tag.json" ;;
+    ab)
+      tag=${rest%%:*}; rest=${rest#*:}
+      reps=${rest%%:*}; rest=${rest#*:}
+      vars=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args=""
+      IFS='|' read -ra VARS <<< "$vars"
+      for rep in $(seq 1 "$reps"); do
+        for v in "${VARS[@]}"; do
+          t="${tag}_$(echo "$v" | tr ' =/' '_-_')_$rep"
+          env $v timeout -k 10 600 python bench.py $args > "$O/$t.json" 2> "$O/$t.err" \
+            || { echo "ab run [$v] failed"; tail -5 "$O/$t.err"; exit 1; }
+          echo "[$v] $(summ "$O/$t.json")"
+        done
+      done ;;
+    prof)
+      IFS=':' read -r tag kern cfg mode rank args <<< "$rest"
+      cd /tmp
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/kt_$tag" -o kt --output-format csv -- python3 "$R/bench.py" $args \
+        > "$O/prof_kt_$tag.log" 2>&1 || { echo "kernel trace $tag failed"; tail -5 "$O/prof_kt_$tag.log"; exit 1; }
+      timeout -s KILL 600 rocprofv3 --pmc FETCH_SIZE -d "$O/fetch_$tag" -o fetch --output-format csv -- python3 "$R/bench.py" $args \
+        > "$O/prof_fetch_$tag.log" 2>&1 || { echo "fetch $tag failed"; tail -5 "$O/prof_fetch_$tag.log"; exit 1; }
+      timeout -s KILL 600 rocprofv3 --pmc WRITE_SIZE -d "$O/write_$tag" -o write --output-format csv -- python3 "$R/bench.py" $args \
+        > "$O/prof_write_$tag.log" 2>&1 || { echo "write $tag failed"; tail -5 "$O/prof_write_$tag.log"; exit 1; }
+      cd "$R"
+      stats=$(ls "$O"/kt_$tag/*kernel_stats.csv | head -1)
+      cp "$stats" "$O/stats_$tag.csv"
+      python3 tools/pmc_summary.py --stats "$stats" --fetch $(ls "$O"/fetch_$tag/*counter_collection.csv | head -1) \
+        --write $(ls "$O"/write_$tag/*counter_collection.csv | head -1) --kernel "$kern" --config "$cfg" --mode "$mode" \
+        --rank "$rank" --out "$O/traffic_$tag.json" > /dev/null || { echo "pmc summary $tag failed"; exit 1; }
+      rm -rf "$O/fetch_$tag" "$O/write_$tag"
+      echo "traffic $tag: $(tr -d '\n ' < "$O/traffic_$tag.json" | cut -c1-260)"
+      head -6 "$O/stats_$tag.csv" | cut -c1-150 ;;
+    micro)
+      src=${rest%%:*}; flags=${rest#*:}; [ "$flags" = "$rest" ] && flags=""
+      b=$(basename "$src" .hip)
+      hipcc -O3 --offload-arch=gfx950 $flags -o "$O/$b" "$src" > "$O/$b.build.log" 2>&1 \
+        || { echo "micro build failed"; tail -5 "$O/$b.build.log"; exit 1; }
+      timeout -k 10 120 "$O/$b" > "$O/$b.txt" 2>&1 || { echo "micro $b failed"; tail -5 "$O/$b.txt"; exit 1; }
+      cat "$O/$b.txt" ;;
+    cmd)
+      timeout -k 10 300 bash -c "$rest" > "$O/cmd_$n.log" 2>&1 || { echo "cmd failed"; tail -10 "$O/cmd_$n.log"; exit 1; }
+      tail -20 "$O/cmd_$n.log" ;;
+    *)
+      echo "unknown step kind: $kind"; exit 2 ;;
+  esac
+done
