@@ -98,9 +98,14 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def pmc_traffic(a, k, groups, kernel):
+PMC_LAUNCH_TOL = 0.05  # a committed PMC summary must describe a launch this long (+-5%)
+
+
+def pmc_traffic(a, k, groups, kernel, launch_us):
     """HBM bytes per launch of the dominant kernel from a committed rocprofv3 --pmc summary
-    (tools/pmc_summary.py) of the same workload and kernel, or (None, None)."""
+    (tools/pmc_summary.py) of the same workload and kernel, or (None, None).  A summary whose
+    rocprofv3 average launch differs from this run's event-timed launch (launch_us) by more than
+    PMC_LAUNCH_TOL is stale -- it profiled another build of the kernel -- and is refused."""
     import glob
     paths = [a.traffic_json] if a.traffic_json else sorted(
         glob.glob(os.path.join(ROOT, "profiles", f"r*_traffic_{a.config}_{a.mode}.json")))
@@ -108,8 +113,15 @@ def pmc_traffic(a, k, groups, kernel):
         if not path or not os.path.exists(path):
             continue
         rec = json.load(open(path))
-        if rec.get("rank") == k and rec.get("groups") in (groups, 0) and rec.get("kernel") == kernel and a.scale == 1.0:
-            return rec["bytes_per_launch"], os.path.relpath(path, ROOT)
+        if not (rec.get("rank") == k and rec.get("groups") in (groups, 0) and rec.get("kernel") == kernel
+                and a.scale == 1.0):
+            continue
+        prof_us = rec.get("avg_ns", 0.0) / 1e3
+        if not launch_us or abs(prof_us - launch_us) > PMC_LAUNCH_TOL * launch_us:
+            print(f"[bench] {os.path.relpath(path, ROOT)}: profiled launch {prof_us:.1f} us vs this run's "
+                  f"{launch_us} us: stale, not used", file=sys.stderr)
+            return None, None
+        return rec["bytes_per_launch"], os.path.relpath(path, ROOT)
     return None, None
 
 
@@ -159,7 +171,7 @@ def rmse_reference(a, arrays):
 
 
 def det_kernel_name():
-    return "k_det_sweep" if os.environ.get("MFHIP_DET_SWEEP") == "1" else "k_det_sweep2"
+    return "k_det_sweep2"
 
 
 def det_roofline(a, k, sp):
@@ -173,7 +185,7 @@ def det_roofline(a, k, sp):
     ksec = sp["kernel_ms"] / 1e3
     alg = sp["updates"] * (32 * k + 24) / ksec / 1e9
     da = argparse.Namespace(**{**vars(a), "mode": "det"})
-    traffic, src = pmc_traffic(da, k, 0, det_kernel_name())
+    traffic, src = pmc_traffic(da, k, 0, det_kernel_name(), round(sp["kernel_ms"] * 1e3 / launches, 2))
     return {"bound": "hbm", "achieved": round(alg, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(alg / HBM_PEAK_GBS, 4), "bytes_model": "algorithmic B_f64(k) = 32k+24 per update",
             "avg_launch_us": round(sp["kernel_ms"] * 1e3 / launches, 2), "traffic": traffic, "traffic_source": src,
@@ -183,9 +195,12 @@ def det_roofline(a, k, sp):
 def det_leg(a, k, nb, train, test, ref, stream):
     """The deterministic f64 mode on the same data: DSGDforMF.scala:378-418's exact update order
     (JVM shuffle, F2J ddot fold, no FMA), one persistent sweep per superstep.  Timed epochs after
-    one warmup epoch, then a restarted 10-epoch fit whose held-out RMSE must equal the f64
-    oracle's on this data (tests/golden/rmse_ref.json) to the last bit of its printout; then the
-    ONLINE leg in f64 on that model (the precision the bit-exact online tests cover)."""
+    one warmup epoch (warm: a run takes over the first supersteps the previous run built on the
+    host in the background), then a restarted 10-epoch fit -- cold: restart drops those builds,
+    so it pays the first superstep's host build, reported as cold_fit_s -- whose held-out RMSE
+    must equal the f64 oracle's on this data (tests/golden/rmse_ref.json) to the last bit of its
+    printout; then the ONLINE leg in f64 on that model (the precision the bit-exact online tests
+    cover)."""
     import mfhip
     from mfhip import _lib as L
     p = L.default_params()
@@ -211,8 +226,13 @@ def det_leg(a, k, nb, train, test, ref, stream):
         ctx.sync()
         ctx.set_profiling(False)
         sp = ctx.stats()
+        ctx.reset_stats()
+        t0 = time.perf_counter()
         ctx.restart()
         ctx.run(10 * nb)
+        ctx.sync()
+        cold = time.perf_counter() - t0
+        cold_updates = ctx.stats()["updates"]
         rmse, _ = ctx.rmse(*test)
         online = online_leg(ctx, stream, a) if stream is not None else None
     return {"metric": "SGD rating updates/sec, deterministic f64 (the reference's exact update order)",
@@ -221,6 +241,9 @@ def det_leg(a, k, nb, train, test, ref, stream):
             "avg_launch_us": round(sp["kernel_ms"] * 1e3 / max(sp["kernel_launches"], 1), 2),
             "roofline": det_roofline(a, k, sp),
             "launches_per_epoch": sp["kernel_launches"], "prepare_s": round(t_prep, 2),
+            "cold_fit_s": round(cold, 4), "cold_fit_epochs": 10,
+            "cold_value": round(cold_updates / cold, 1) if cold > 0 else None,
+            "cold_note": "restart + 10 epochs + sync from a cold host pipeline (no superstep built ahead)",
             "rmse": round(rmse, 9), "rmse_ref": round(ref["oracle_rmse"], 9) if ref else None,
             "rmse_equal_to_ref": (abs(rmse - ref["oracle_rmse"]) <= 1e-12 * ref["oracle_rmse"]) if ref else None,
             "online": online}  # moved to the top-level "online" block by main()
@@ -360,8 +383,9 @@ def main():
         ksec = st_p["kernel_ms"] / 1e3
         achieved = st_p["moved_bytes"] / ksec / 1e9  # GB/s, this rank's sweep kernel
         kname = L.lib().mf_fast_kernel_name(k).decode() if a.mode == "fast" else det_kernel_name()
+        launch_us = round(st_p["kernel_ms"] * 1e3 / max(launches, 1), 2)
         # the committed PMC summaries are one-GPU runs: a rank of an N-GPU ring runs other launches
-        traffic, traffic_src = pmc_traffic(a, k, st["groups"], kname) if D.world == 1 else (None, None)
+        traffic, traffic_src = pmc_traffic(a, k, st["groups"], kname, launch_us) if D.world == 1 else (None, None)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kname,
                 "bytes_per_launch": round(st_p["moved_bytes"] / max(launches, 1)),

@@ -19,7 +19,7 @@ extern "C" {
    mf_debug_fast_schedule: for every input rating, the rating block (ub*n+ib), rotation
    sub-step, item group and position inside its cell of the fast-mode plan with `groups`
    groups per rating block (groups < 0: the systolic sweep's per-block choice for a budget of
-   -groups waves per superstep, as mf_dsgd_prepare makes it with MFHIP_SYS_WAVES=-groups),
+   -groups waves per superstep, as mf_dsgd_prepare makes it with MFHIP_TEST=sys_waves=-groups),
    MF_BLOCKING_* `blocking` and hazard window `window` (0: 8). */
 int mf_debug_levels(const uint32_t* urow, const uint32_t* irow, const int32_t* order, int64_t n,
                     int32_t* level_out);
@@ -42,13 +42,19 @@ int mf_debug_ring_schedule(int32_t rank, int32_t world, int32_t n_blocks, int64_
 /* mf_debug_plan_digest: after mf_dsgd_prepare of a fast-mode fit on one shard, an FNV-1a digest
    of the device schedule -- the pair records, the wave table and (systolic) the per-wave cell
    tables -- and the pair-record count: out[0] = digest, out[1] = records.  Compares the device-
-   built plan (kernels_plan.hip) with the host-built one (MFHIP_DEVICE_PLAN=0). */
+   built plan (kernels_plan.hip) with the host-built one (MFHIP_TEST=device_plan=0). */
 int mf_debug_plan_digest(mf_ctx* ctx, uint64_t out[2]);
 /* The plan window (records between two uses of a row inside a cell unless adjacent) the fast
    sweep uses at rank k: the prefetch distance of the kernel selected for k. */
 int mf_fast_plan_window(int32_t k, int32_t* window_out);
 /* Name of the fast-mode sweep kernel used at rank k (for profiles and bench reports). */
 const char* mf_fast_kernel_name(int32_t k);
+/* Build flags: bit 0 = built with -DMFHIP_EXPERIMENTS (hot-item replicas, wave traces and the
+   other experiment switches exist; the default build has none of them). */
+int32_t mf_debug_build_flags(void);
+/* Device memory this process holds through the library: out[0] = live bytes, out[1] = the
+   high-water mark since the library was loaded (rank rehearsals report it per rank). */
+int mf_debug_device_bytes(int64_t out[2]);
 
 #ifdef __cplusplus
 }

@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstring>
 #include <cstdlib>
 #include <atomic>
 #include <functional>
@@ -60,6 +61,10 @@ int guarded(F&& f) {
   } while (0)
 
 // Owning device allocation on the current device.
+// Device bytes this process holds in DevBufs (live, high-water mark): mf_debug_device_bytes.
+inline std::atomic<int64_t>& dev_bytes_live() { static std::atomic<int64_t> v{0}; return v; }
+inline std::atomic<int64_t>& dev_bytes_peak() { static std::atomic<int64_t> v{0}; return v; }
+
 class DevBuf {
  public:
   DevBuf() = default;
@@ -77,9 +82,15 @@ class DevBuf {
     if (bytes == 0) return;
     MF_HIP(hipMalloc(&p_, bytes));
     bytes_ = bytes;
+    const int64_t now = dev_bytes_live() += static_cast<int64_t>(bytes);
+    int64_t pk = dev_bytes_peak().load();
+    while (now > pk && !dev_bytes_peak().compare_exchange_weak(pk, now)) {}
   }
   void release() {
-    if (p_) (void)hipFree(p_);
+    if (p_) {
+      (void)hipFree(p_);
+      dev_bytes_live() -= static_cast<int64_t>(bytes_);
+    }
     p_ = nullptr;
     bytes_ = 0;
   }
@@ -127,6 +138,35 @@ class PinnedBuf {
   void* p_ = nullptr;
   size_t bytes_ = 0;
 };
+
+// Runtime switches.  The library reads five environment variables:
+//   MFHIP_THREADS / OMP_NUM_THREADS  host workers (below);
+//   MFHIP_TIMING                     prepare's phase timings on stderr;
+//   MFHIP_DEBUG_PLAN                 planner diagnostics and the sweeps' error words on stderr;
+//   MFHIP_DEVICE_SHARERS             rank mode: ranks sharing one device (the one-GPU ring rehearsal);
+//   MFHIP_TEST                       "key=value,..." overrides the test suite uses to force the
+//                                    alternative paths it compares bit for bit (test_knob).
+// Experiment switches (hot-item replicas, group-model constants, wave traces, ...) exist only in a
+// build with -DMFHIP_EXPERIMENTS (make EXPERIMENTS=1); the default build never reads them.
+inline std::string test_knob(const char* key) {
+  const char* s = std::getenv("MFHIP_TEST");  // read where it is used (never cached): one process may switch
+  if (!s) return "";
+  const size_t kl = std::strlen(key);
+  for (const char* p = s;;) {
+    const char* e = std::strchr(p, ',');
+    const size_t len = e ? static_cast<size_t>(e - p) : std::strlen(p);
+    if (len > kl && std::strncmp(p, key, kl) == 0 && p[kl] == '=') return std::string(p + kl + 1, len - kl - 1);
+    if (!e) return "";
+    p = e + 1;
+  }
+}
+#ifdef MFHIP_EXPERIMENTS
+inline const char* exp_knob(const char* name) { return std::getenv(name); }
+constexpr bool kExperiments = true;
+#else
+inline const char* exp_knob(const char*) { return nullptr; }
+constexpr bool kExperiments = false;
+#endif
 
 // Host worker count: OMP_NUM_THREADS / MFHIP_THREADS if set (the GPU box exports 16),
 // else hardware_concurrency, capped at 32.

@@ -195,7 +195,7 @@ __global__ __launch_bounds__(64) void k_det_sweep2(const DetWave* __restrict__ w
   for (int c = 0; c < KPL; ++c) q[c] = 0.0;
 
   // one entry (chunk-relative s, a compile-time constant once unrolled)
-#ifdef MFHIP_DET_PROBE
+#if defined(MFHIP_EXPERIMENTS) && defined(MFHIP_DET_PROBE)
   uint64_t pc[4] = {0, 0, 0, 0};  // experiment build: shader cycles per phase, printed by wave 0
   uint64_t pt = __builtin_amdgcn_s_memtime();
   auto stamp = [&](int x) { const uint64_t n = __builtin_amdgcn_s_memtime(); pc[x] += n - pt; pt = n; };
@@ -286,7 +286,7 @@ done:
   __builtin_amdgcn_s_waitcnt(0x0F70);
   publish(pend0, pv0, lane);
   publish(pend1, pv1, lane);
-#ifdef MFHIP_DET_PROBE
+#if defined(MFHIP_EXPERIMENTS) && defined(MFHIP_DET_PROBE)
   if (blockIdx.x == 0 && lane == 0)
     printf("[det probe] wave 0: %lld entries, cycles per entry: pre-fold %.0f fold %.0f post-fold %.0f prefetch %.0f\n",
            (long long)cnt, double(pc[0]) / cnt, double(pc[1]) / cnt, double(pc[2]) / cnt, double(pc[3]) / cnt);

@@ -30,15 +30,97 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
-#include <cstdlib>
-#include <string>
-
 #include "kernels.hpp"
 
 namespace mfhip {
 namespace {
 
 #include "pair_device.hpp"
+
+// A cell that is one item run (build_pair_plan): the item row stays in registers from the first
+// pair to the last, so a pair moves no item row, only user rows (4 VMEM operations).  B's user row
+// is stored where it was loaded from (its offset rides an SGPR ring).  FWD = false: so is A's (no
+// user repeats at the next record: kWaveSingleRun); FWD = true (kWaveSingleRunFwd): A's row may be
+// the previous pair's result (a user rating the item twice in a row), forwarded in registers.
+template <int KPL, int UP, bool FWD>
+__device__ __forceinline__ void single_run_cell(Chunk C0, ChunkRaw C1, __amdgpu_buffer_rsrc_t RR,
+                                                __amdgpu_buffer_rsrc_t urs, __amdgpu_buffer_rsrc_t irs, float eta,
+                                                uint32_t vlane, uint32_t voff, int npairs, uint64_t& wait_clk) {
+  (void)wait_clk;
+  constexpr int NV = Row<KPL>::NV;
+  constexpr int CH = kPairChunk;
+  constexpr int DS = kPairRingSingle;
+  const uint32_t item_off = rl(C0.ia, 0);
+  Row<KPL> q = ld<KPL>(irs, voff, item_off);
+  Row<KPL> RA[DS], RB[DS], plA, plB;
+#pragma unroll
+  for (int e = 0; e < NV; ++e) plA.v[e] = plB.v[e] = f2{0.f, 0.f};
+  uint32_t oa[DS], ob[DS];
+#pragma unroll
+  for (int s = 0; s < DS; ++s) {
+    oa[s] = rl(C0.ua, s);
+    ob[s] = rl(C0.ub, s);
+    RA[s] = ld<KPL, UP>(urs, voff, oa[s]);
+    RB[s] = ld<KPL, UP>(urs, voff, ob[s]);
+  }
+  drain_vmem();
+  const float neta = vgpr_of(-eta);
+  for (int c = 0;; ++c) {
+#pragma unroll
+    for (int s = 0; s < CH; ++s) {
+      if (c * CH + s >= npairs) goto run_done;
+      const int slot = s % DS;
+#if defined(MFHIP_EXPERIMENTS) && defined(MFHIP_WAITPROBE)
+      {  // experiment build: shader cycles spent waiting for this pair's prefetched user rows
+        const uint64_t a = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_s_waitcnt((4 * (DS - 1)) & 15 | (((4 * (DS - 1)) >> 4) << 14) | 0x0F70 & ~0xF);
+        wait_clk += __builtin_amdgcn_s_memtime() - a;
+      }
+#endif
+      // the ring's next offsets (pair s + DS), named up front
+      const uint32_t noa = s + DS < CH ? rl(C0.ua, s + DS) : rl(C1.w0[0], s + DS - CH);
+      const uint32_t nob = s + DS < CH ? rl(C0.ub, s + DS) : rl(C1.w0[1], s + DS - CH);
+      Row<KPL> pa;
+      uint32_t osa;
+      if constexpr (FWD) {
+        const uint32_t fl = rl(C0.flags, s);
+        osa = rl(C0.sa, s);
+        const float kfa = static_cast<float>(fl & 0xFFu), kfb = static_cast<float>((fl >> 8) & 0xFFu);
+#pragma unroll
+        for (int e = 0; e < NV; ++e) pa.v[e] = kfb * plB.v[e] + (kfa * plA.v[e] + RA[slot].v[e]);
+      } else {
+        osa = oa[slot];
+        pa = RA[slot];
+      }
+      const Row<KPL> pb = RB[slot];
+      float c1 = dot_part<KPL>(pa, q), c2 = dot_part<KPL>(pb, q), g = dot_part<KPL>(pb, pa);
+      wave_sum3(c1, c2, g);
+      // wa = eta eA, wb = eta eB for every pair of the chunk at once (lane s holds pair s)
+      const float wav = fmaf(c1, neta, C0.era);
+      const float wbv = fmaf(fmaf(wav, g, C0.aa * c2), neta, C0.erb);
+      const float wa = rlf(wav, s), wb = rlf(wbv, s);
+      const float aa = rlf(C0.aa, s), ab = rlf(C0.ab, s), ba = rlf(C0.ba, s), bb = rlf(C0.bb, s);
+#pragma unroll
+      for (int e = 0; e < NV; ++e) {
+        const f2 q0 = q.v[e], a0 = pa.v[e], b0 = pb.v[e];
+        const f2 q1 = aa * q0 + wa * a0;
+        plA.v[e] = ba * a0 + wa * q0;
+        plB.v[e] = bb * b0 + wb * q1;
+        q.v[e] = ab * q1 + wb * b0;
+      }
+      st<KPL, UP>(urs, voff, osa, plA);
+      st<KPL, UP>(urs, voff, ob[slot], plB);
+      oa[slot] = noa;
+      ob[slot] = nob;
+      RA[slot] = ld<KPL, UP>(urs, voff, noa);
+      RB[slot] = ld<KPL, UP>(urs, voff, nob);
+    }
+    C0 = chunk_convert(C1, eta);
+    C1 = chunk_load(RR, c + 2, vlane);
+  }
+run_done:
+  st<KPL>(irs, voff, item_off, q);
+}
 
 // One cell (WaveDesc d) of the pair schedule, swept by the calling wave.  UP = cache policy of
 // the user-row loads and stores.  L0 / L1: the cell's first two record chunks, loaded by the
@@ -58,75 +140,17 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const ChunkRaw& L0, 
 
   Chunk C0 = chunk_convert(L0, eta);  // current chunk
   ChunkRaw C1 = L1;                   // next chunk, as loaded
+  if (d.cells == kWaveSingleRun) {
+    single_run_cell<KPL, UP, false>(C0, C1, RR, urs, irs, eta, vlane, voff, npairs, wait_clk);
+    return;
+  }
+  if (d.cells == kWaveSingleRunFwd) {
+    single_run_cell<KPL, UP, true>(C0, C1, RR, urs, irs, eta, vlane, voff, npairs, wait_clk);
+    return;
+  }
   Row<KPL> plA, plB;  // the previous pair's updated user rows (forwarding)
 #pragma unroll
   for (int e = 0; e < NV; ++e) plA.v[e] = plB.v[e] = f2{0.f, 0.f};
-
-  if (d.cells == kWaveSingleRun) {
-    // The cell is one item run (build_pair_plan): the item row stays in registers from the
-    // first pair to the last, so a pair moves no item row; B's user row is stored where it
-    // was loaded from (offset kept in an SGPR ring), A's may be forwarded from the previous
-    // pair (a user rating the item twice in a row).
-    const uint32_t item_off = rl(C0.ia, 0);
-    Row<KPL> q = ld<KPL>(irs, voff, item_off);
-    constexpr int DS = kPairRingSingle;  // 4 VMEM ops per pair: a deeper ring than the generic path
-    Row<KPL> RA[DS], RB[DS];
-    uint32_t ob[DS];
-#pragma unroll
-    for (int s = 0; s < DS; ++s) {
-      ob[s] = rl(C0.ub, s);
-      RA[s] = ld<KPL, UP>(urs, voff, rl(C0.ua, s));
-      RB[s] = ld<KPL, UP>(urs, voff, ob[s]);
-    }
-    drain_vmem();
-    for (int c = 0;; ++c) {
-#pragma unroll
-      for (int s = 0; s < CH; ++s) {
-        if (c * CH + s >= npairs) goto run_done;
-        const int slot = s % DS;
-#ifdef MFHIP_WAITPROBE
-        {  // experiment build: shader cycles spent waiting for this pair's prefetched user rows
-          const uint64_t a = __builtin_amdgcn_s_memtime();
-          __builtin_amdgcn_s_waitcnt((4 * (DS - 1)) & 15 | (((4 * (DS - 1)) >> 4) << 14) | 0x0F70 & ~0xF);
-          wait_clk += __builtin_amdgcn_s_memtime() - a;
-        }
-#endif
-        const uint32_t fl = rl(C0.flags, s), osa = rl(C0.sa, s);
-        // the ring's next offsets (pair s + DS), also named up front
-        const uint32_t noa = s + DS < CH ? rl(C0.ua, s + DS) : rl(C1.w0[0], s + DS - CH);
-        const uint32_t nob = s + DS < CH ? rl(C0.ub, s + DS) : rl(C1.w0[1], s + DS - CH);
-        const float kfa = static_cast<float>(fl & 0xFFu), kfb = static_cast<float>((fl >> 8) & 0xFFu);
-        Row<KPL> pa;
-        const Row<KPL> pb = RB[slot];
-#pragma unroll
-        for (int e = 0; e < NV; ++e) pa.v[e] = kfb * plB.v[e] + (kfa * plA.v[e] + RA[slot].v[e]);
-        float c1 = dot_part<KPL>(pa, q), c2 = dot_part<KPL>(pb, q), g = dot_part<KPL>(pb, pa);
-        wave_sum3(c1, c2, g);
-        const float era = rlf(C0.era, s), erb = rlf(C0.erb, s);
-        const float aa = rlf(C0.aa, s), ab = rlf(C0.ab, s), ba = rlf(C0.ba, s), bb = rlf(C0.bb, s);
-        const float wa = fmaf(-eta, c1, era);
-        const float wb = fmaf(-eta, fmaf(wa, g, aa * c2), erb);
-#pragma unroll
-        for (int e = 0; e < NV; ++e) {
-          const f2 q0 = q.v[e], a0 = pa.v[e], b0 = pb.v[e];
-          const f2 q1 = aa * q0 + wa * a0;
-          plA.v[e] = ba * a0 + wa * q0;
-          plB.v[e] = bb * b0 + wb * q1;
-          q.v[e] = ab * q1 + wb * b0;
-        }
-        st<KPL, UP>(urs, voff, osa, plA);
-        st<KPL, UP>(urs, voff, ob[slot], plB);
-        ob[slot] = nob;
-        RA[slot] = ld<KPL, UP>(urs, voff, noa);
-        RB[slot] = ld<KPL, UP>(urs, voff, ob[slot]);
-      }
-      C0 = chunk_convert(C1, eta);
-      C1 = chunk_load(RR, c + 2, vlane);
-    }
-  run_done:
-    st<KPL>(irs, voff, item_off, q);
-    return;
-  }
 
   {
     Row<KPL> PA[D], PB[D], QA[D], QB[D];
@@ -140,6 +164,7 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const ChunkRaw& L0, 
 #pragma unroll
     for (int s = 0; s < D; ++s) MF_PREFETCH(s, C0.ua, C0.ub, C0.ia, C0.ib, s);
     drain_vmem();
+    const float neta = vgpr_of(-eta);
     Row<KPL> q;
 #pragma unroll
     for (int e = 0; e < NV; ++e) q.v[e] = f2{0.f, 0.f};
@@ -149,7 +174,7 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const ChunkRaw& L0, 
       for (int s = 0; s < CH; ++s) {
         if (c * CH + s >= npairs) return;
         const int slot = s % D;
-#ifdef MFHIP_WAITPROBE
+#if defined(MFHIP_EXPERIMENTS) && defined(MFHIP_WAITPROBE)
         {  // experiment build: shader cycles spent waiting for this pair's prefetched rows
           const uint64_t a = __builtin_amdgcn_s_memtime();
           __builtin_amdgcn_s_waitcnt((8 * (D - 1)) & 15 | (((8 * (D - 1)) >> 4) << 14) | 0x0F70 & ~0xF);
@@ -179,11 +204,12 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const ChunkRaw& L0, 
         }
         float c1 = dot_part<KPL>(pa, qa), c2 = dot_part<KPL>(pb, qbd), g = dot_part<KPL>(pb, pa);
         wave_sum3(c1, c2, g);
-        const float era = rlf(C0.era, s), erb = rlf(C0.erb, s);
+        // wa = eta eA, wb = eta eB in the chunk layout (lane s = pair s); a split pair has no
+        // coupling to A's update (sr = 0, m = 1)
+        const float wav = fmaf(c1, neta, C0.era);
+        const float wbv = fmaf(fmaf(C0.sr * wav, g, C0.m * c2), neta, C0.erb);
+        const float wa = rlf(wav, s), wb = rlf(wbv, s);
         const float aa = rlf(C0.aa, s), ab = rlf(C0.ab, s), ba = rlf(C0.ba, s), bb = rlf(C0.bb, s);
-        const float wa = fmaf(-eta, c1, era);
-        const float m = fmaf(sr, aa - 1.f, 1.f), gw = sr * wa;  // split: no coupling to A's update
-        const float wb = fmaf(-eta, fmaf(gw, g, m * c2), erb);
         Row<KPL> q1;
 #pragma unroll
         for (int e = 0; e < NV; ++e) {
@@ -315,7 +341,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
       uint64_t* tr = trace + 4 * (w.cell0 + t);
       tr[0] = c_start;
       tr[1] = __builtin_amdgcn_s_memrealtime();
-#ifdef MFHIP_WAITPROBE
+#if defined(MFHIP_EXPERIMENTS) && defined(MFHIP_WAITPROBE)
       tr[2] = wait_clk;  // experiment build: the trace's clock column carries the wait cycles
 #else
       tr[2] = __builtin_amdgcn_s_memtime() - c_clk;
@@ -338,27 +364,17 @@ void dispatch(hipStream_t st, const WaveDesc* waves, int nwaves, const PairRec* 
 
 // Record preload across the cell boundary (PRE): on for k >= 128 (NFLX 22.49-22.67 vs 22.56-22.81 ms
 // per epoch, A/B/A/B), off for k = 64 (ML20M 5.86-5.98 vs 5.59-5.60 ms: its cells are short and its
-// waves tightly coupled).  MFHIP_CELL_PRELOAD=0/1 overrides (A/B).
-bool cell_preload(int kpl) {
-  static const int env = [] {
-    const char* v = std::getenv("MFHIP_CELL_PRELOAD");
-    return v ? std::atoi(v) : -1;
-  }();
-  return env >= 0 ? env != 0 : kpl >= 2;
-}
+// waves tightly coupled).  One instance per k.
+template <int KPL>
+constexpr bool kCellPreload = KPL >= 2;
 
 template <int KPL>
 void dispatch_sys(hipStream_t st, const SysWave* sw, const WaveDesc* sys, int nw, int lbase, const PairRec* recs,
                   float* U, float* I, uint64_t ub, uint64_t ib, float eta, int32_t* prog, uint32_t base, int32_t* err,
                   uint64_t* trace, hipEvent_t ev0, hipEvent_t ev1, const int32_t* place) {
-  if (cell_preload(KPL))
-    hipExtLaunchKernelGGL((k_sweep_pair_sys<KPL, kPairRing, true>), dim3(static_cast<unsigned>(nw)), dim3(64), 0, st,
-                          ev0, ev1, 0, sw, sys, nw, lbase, reinterpret_cast<const u4v*>(recs), U, I, ub, ib, eta, prog,
-                          base, err, trace, place);
-  else
-    hipExtLaunchKernelGGL((k_sweep_pair_sys<KPL, kPairRing, false>), dim3(static_cast<unsigned>(nw)), dim3(64), 0, st,
-                          ev0, ev1, 0, sw, sys, nw, lbase, reinterpret_cast<const u4v*>(recs), U, I, ub, ib, eta, prog,
-                          base, err, trace, place);
+  hipExtLaunchKernelGGL((k_sweep_pair_sys<KPL, kPairRing, kCellPreload<KPL>>), dim3(static_cast<unsigned>(nw)),
+                        dim3(64), 0, st, ev0, ev1, 0, sw, sys, nw, lbase, reinterpret_cast<const u4v*>(recs), U, I, ub,
+                        ib, eta, prog, base, err, trace, place);
 }
 
 template <int KPL>
@@ -366,11 +382,9 @@ int sys_capacity() {
   int dev = 0, cus = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-  int a = 0, b = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, k_sweep_pair_sys<KPL, kPairRing, true>, 64, 0) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_sweep_pair_sys<KPL, kPairRing, false>, 64, 0) != hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sweep_pair_sys<KPL, kPairRing, kCellPreload<KPL>>, 64,
+                                                   0) != hipSuccess)
     return 0;
-  per_cu = std::min(a, b);
   return cus * per_cu;
 }
 
@@ -414,6 +428,7 @@ void launch_sweep_pair(hipStream_t st, const WaveDesc* waves, int nwaves, const 
   }
 }
 
+#ifdef MFHIP_EXPERIMENTS
 // Hot-item replicas (plan.hpp SplitItem), one workgroup per split item, any k.  fork: the item's
 // row to its R-1 replica rows; join: q = (q + sum_r q_r) / R, replicas in order (deterministic).
 __global__ __launch_bounds__(64) void k_split_fork(const SplitItem* __restrict__ sp, float* __restrict__ I, int k) {
@@ -438,12 +453,23 @@ __global__ __launch_bounds__(64) void k_split_join(const SplitItem* __restrict__
   }
 }
 
+#endif
+
+// Hot-item replicas exist only in a -DMFHIP_EXPERIMENTS build (the default build never plans any).
 void launch_split_fork(hipStream_t st, const SplitItem* sp, int n, float* I, int k) {
+#ifdef MFHIP_EXPERIMENTS
   if (n > 0) hipLaunchKernelGGL(k_split_fork, dim3(n), dim3(64), 0, st, sp, I, k);
+#else
+  (void)st; (void)sp; (void)n; (void)I; (void)k;
+#endif
 }
 
 void launch_split_join(hipStream_t st, const SplitItem* sp, int n, float* I, int k) {
+#ifdef MFHIP_EXPERIMENTS
   if (n > 0) hipLaunchKernelGGL(k_split_join, dim3(n), dim3(64), 0, st, sp, I, k);
+#else
+  (void)st; (void)sp; (void)n; (void)I; (void)k;
+#endif
 }
 
 }  // namespace mfhip

@@ -252,7 +252,7 @@ struct PairArgs {
   const int64_t* wave_cell;  // per wave
   const int64_t* wave_base;  // per wave: first pair record
   PairRec* out;
-  int32_t* kind;             // per wave: kWaveGeneric / kWaveSingleRun
+  int32_t* kind;             // per wave: kWaveGeneric / kWaveSingleRun / kWaveSingleRunFwd
   int32_t* noops;            // per wave: no-op halves
   double* bytes;             // per wave: requested bytes
   int64_t nwaves;
@@ -353,7 +353,9 @@ __global__ __launch_bounds__(kPlanThreads) void k_pair_waves(PairArgs A) {
       }
     }
     if (single && out > first) rows += 2;
-    A.kind[w] = single ? kWaveSingleRun : kWaveGeneric;
+    bool fwd = false;  // A rows forwarded from the previous pair: the lean path's FWD instance
+    for (const PairRec* r = first; single && r < out; ++r) fwd = fwd || (r->flags & (kPairFwdA | kPairFwdB));
+    A.kind[w] = single ? (fwd ? kWaveSingleRunFwd : kWaveSingleRun) : kWaveGeneric;
     A.noops[w] = noop;
     A.bytes[w] = 64.0 * static_cast<double>(out - first) + A.row_bytes * static_cast<double>(rows);
   }

@@ -139,7 +139,7 @@ struct mf_ctx {
   int32_t G_fast = 0;
   uint32_t fast_dummy_u = 0, fast_dummy_i = 0;  // zeroed rows past the real ones (padding / idle prefetch)
   int32_t fast_prio_len = 1 << 30;  // cells at least this long run at raised priority
-  bool fast_persistent = false;  // MFHIP_FAST_KERNEL=persistent selects the systolic single launch
+  bool fast_persistent = false;  // MFHIP_TEST fast_kernel=persistent selects the systolic single launch
   bool fast_pair = false;         // two updates per step (kernels_pair.hip), k in {64, 128, 256}
   bool fast_sys = false;          // pair cells as one systolic launch per superstep (k_sweep_pair_sys)
   bool det_sweep = false;         // deterministic mode: one persistent k_det_sweep launch per superstep
@@ -172,17 +172,13 @@ enum class FastKernel { kPair, kCell, kPersistent };
 
 // Fast sweep kernel: pair (default where k is 64, 128 or 256; kernels_pair.hip) | cell (one
 // update per step, any k; kernels_fast.hip) | persistent (kernels_fast.hip, one launch per
-// superstep); MFHIP_FAST_KERNEL overrides.
-// Pair cells as one systolic launch per superstep (default; MFHIP_PAIR_SYS=0: one launch per
+// superstep); MFHIP_TEST fast_kernel= overrides.
+// Pair cells as one systolic launch per superstep (default; MFHIP_TEST pair_sys=0: one launch per
 // sub-step).  Falls back to per-sub-step launches when a superstep's waves cannot all be resident.
-bool want_pair_sys() {
-  const char* v = std::getenv("MFHIP_PAIR_SYS");
-  return v ? std::string(v) != "0" : true;
-}
+bool want_pair_sys() { return test_knob("pair_sys") != "0"; }
 
 FastKernel choose_fast_kernel(int k) {
-  const char* v = std::getenv("MFHIP_FAST_KERNEL");
-  const std::string want = v ? v : "";
+  const std::string want = test_knob("fast_kernel");
   if (want == "persistent") return FastKernel::kPersistent;
   if (want == "cell") return FastKernel::kCell;
   if (pair_kernel_supports(k)) return FastKernel::kPair;
@@ -387,7 +383,7 @@ void collect_profile(mf_ctx* ctx) {
 // the wave actually ran at is cycles / ((end - start) x 10 ns), and a 10th: where the wave ran,
 // XCC_ID << 32 | HW_ID (SIMD bits 5:4, CU 11:8, SH 12, SE 15:13).
 void dump_wave_trace(mf_ctx* ctx) {
-  const char* path = std::getenv("MFHIP_WAVE_TRACE");
+  const char* path = exp_knob("MFHIP_WAVE_TRACE");
   if (!path) return;
   FILE* f = nullptr;
   for (auto& s : ctx->shards) {
@@ -472,9 +468,9 @@ void sync_all(mf_ctx* ctx) {
         // the context refuses further supersteps and reads until the fit is prepared again
         ctx->failed = eb == &s.fast_err
                           ? "fast sweep: a wave waited > 1 s for its neighbour (workgroups not co-resident?); "
-                            "set MFHIP_PAIR_SYS=0 (or MFHIP_FAST_KERNEL=cell)"
+                            "set MFHIP_TEST=pair_sys=0 (or fast_kernel=cell)"
                           : "deterministic sweep: a wave waited > 1 s for a user ticket (waves not co-resident?); "
-                            "set MFHIP_DET_KERNEL=level";
+                            "set MFHIP_TEST=det_kernel=level";
         fail(MF_ERR_TIMEOUT, ctx->failed);
       }
     }
@@ -660,7 +656,7 @@ void sys_placement(const PairPlan& pp, int64_t w0, int64_t a, int64_t z, std::ve
     const SysWave& sw = pp.sys_waves[w0 + a + L];
     for (int32_t t = 0; t < sw.G; ++t) {
       const WaveDesc& d = pp.sys[sw.cell0 + t];
-      if (d.steps > 0) load[L] += 2000.0 + d.steps * (d.cells == kWaveSingleRun ? 171.0 : 218.0);
+      if (d.steps > 0) load[L] += 2000.0 + d.steps * (d.cells == kWaveSingleRun || d.cells == kWaveSingleRunFwd ? 171.0 : 218.0);
     }
   }
   const int64_t per = nw / 8, extra = nw % 8;
@@ -756,7 +752,7 @@ void fast_superstep(mf_ctx* ctx, Shard& s, int64_t superstep, double eta) {
     }
     ctx->stats.kernel_launches += ctx->G_fast;
   }
-  static const bool keep_join = [] { const char* v = std::getenv("MFHIP_SPLIT_JOIN"); return v && std::string(v) == "keep"; }();
+  static const bool keep_join = [] { const char* v = exp_knob("MFHIP_SPLIT_JOIN"); return v && std::string(v) == "keep"; }();
   if (!keep_join)  // MFHIP_SPLIT_JOIN=keep: the item keeps replica 0's chain (the others are dropped)
     launch_split_join(s.stream, s.st_split.as<SplitItem>() + sp0, nsplit, s.itf.as<float>(), ctx->P.num_factors);
   MF_HIP(hipGetLastError());
@@ -1108,12 +1104,11 @@ struct PhaseClock {
 };
 
 // Deterministic mode: the persistent sweep's item -> wave layout and staging buffers, unless
-// MFHIP_DET_KERNEL=level (one launch per dependency level, det_superstep) or the device cannot
-// hold a superstep's waves.  Waves per superstep and shard: half the device's resident capacity
-// (shared by the shards on that device; MFHIP_DET_WAVES overrides).
+// MFHIP_TEST det_kernel=level (one launch per dependency level, det_superstep) or the device
+// cannot hold a superstep's waves.  Waves per superstep and shard: half the device's resident
+// capacity (shared by the shards on that device; MFHIP_TEST det_waves= overrides).
 void prepare_det_sweep(mf_ctx* ctx) {
-  const char* kv = std::getenv("MFHIP_DET_KERNEL");
-  if (kv && std::string(kv) == "level") return;
+  if (test_knob("det_kernel") == "level") return;
   int cap = 1 << 30;
   for (auto& s : ctx->shards) {
     DeviceGuard g(s.device);
@@ -1128,7 +1123,7 @@ void prepare_det_sweep(mf_ctx* ctx) {
   if (static_cast<uint64_t>(ctx->U.rows()) * k8 >= 0xFFFFF000ull || static_cast<uint64_t>(ctx->I.rows()) * k8 >= 0xFFFFF000ull)
     return;  // the sweep addresses each f64 slab with 32-bit offsets
   int32_t waves = std::max(1, cap / 2);
-  if (const char* v = std::getenv("MFHIP_DET_WAVES")) waves = std::clamp(std::atoi(v), 1, cap);
+  if (const std::string v = test_knob("det_waves"); !v.empty()) waves = std::clamp(std::atoi(v.c_str()), 1, cap);
   const int32_t n = ctx->nb;
   for (auto& s : ctx->shards) {
     build_det_layout(s.det_layout, ctx->rb, ctx->U, ctx->I, ctx->c, s.index, waves);
@@ -1167,7 +1162,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
   sync_all(ctx);
   PhaseClock clk;
   ctx->item_split = 0;
-  if (const char* v = std::getenv("MFHIP_ITEM_SPLIT")) ctx->item_split = std::max(0, std::atoi(v));
+  if (const char* v = exp_knob("MFHIP_ITEM_SPLIT")) ctx->item_split = std::max(0, std::atoi(v));  // replicas
   ctx->reaper.join();
   DevRatingBlocks dev_rb;  // the device copy of the rating blocks (full device schedule only)
   ctx->nb = std::max(1, ctx->P.num_blocks);
@@ -1175,17 +1170,16 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
   ctx->c = ctx->nb / ctx->G;
   int32_t lo = 0, hi = ctx->nb;
   if (ctx->rank_mode) { lo = ctx->shards[0].index * ctx->c; hi = lo + ctx->c; }
-  // the reference's seeded blocking runs on the device (MFHIP_HOST_BLOCKING=1: on the host)
-  const char* hb = std::getenv("MFHIP_HOST_BLOCKING");
+  // the reference's seeded blocking runs on the device (MFHIP_TEST host_blocking=1: on the host)
+  const std::string hb = test_knob("host_blocking");
   const bool on_device = ctx->P.has_seed && (ctx->f64 || ctx->P.fast_blocking == MF_BLOCKING_REFERENCE) &&
-                         !(hb && std::string(hb) != "0") && n < (int64_t{1} << 31);
+                         !(!hb.empty() && hb != "0") && n < (int64_t{1} << 31);
   if (on_device) {
     Shard& s0 = ctx->shards[0];
     DeviceGuard g(s0.device);
-    const char* dpv0 = std::getenv("MFHIP_DEVICE_PLAN");
+    const std::string dpv0 = test_knob("device_plan");
     const bool keep = !ctx->f64 && ctx->shards.size() == 1 && ctx->item_split == 0 &&
-                      choose_fast_kernel(ctx->P.num_factors) == FastKernel::kPair &&
-                      !(dpv0 && (std::string(dpv0) == "0" || std::string(dpv0) == "1"));
+                      choose_fast_kernel(ctx->P.num_factors) == FastKernel::kPair && dpv0 != "0" && dpv0 != "1";
     device_blocking(s0.stream, u, i, r, n, ctx->nb, ctx->P.seed, lo, hi, ctx->f64, ctx->U, ctx->I, ctx->rb,
                     keep ? &dev_rb : nullptr, !keep);
     clk.lap("blocking + rating blocks (device)");
@@ -1225,9 +1219,8 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
         cap = std::min(cap, sweep_pair_sys_capacity(k));
         simds = std::min(simds, 4 * cus);
       }
-      if (const char* v = std::getenv("MFHIP_SYS_WAVES")) simds = std::max(8, std::atoi(v));  // tests pin it
-      const char* bg = std::getenv("MFHIP_BLOCK_GROUPS");
-      if (ctx->P.fast_waves == 0 && !(bg && std::string(bg) == "0")) {
+      if (const std::string v = test_knob("sys_waves"); !v.empty()) simds = std::max(8, std::atoi(v.c_str()));
+      if (ctx->P.fast_waves == 0 && test_knob("block_groups") != "0") {
         block_groups.assign(nb2, 0);
         for (auto& s : ctx->shards) {
           std::vector<int32_t> gb;
@@ -1270,16 +1263,16 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
     }
     clk.lap("schedule model (groups)");
     // the per-cell emission and the pair records on the device (kernels_plan.hip) for the default
-    // systolic pair sweep of one shard; MFHIP_DEVICE_PLAN=0 keeps them on the host
-    const char* dpv = std::getenv("MFHIP_DEVICE_PLAN");
+    // systolic pair sweep of one shard; MFHIP_TEST device_plan=0 keeps them on the host
+    const std::string dpv = test_knob("device_plan");
     // (a rank whose user blocks hold no rating -- the reference's blocking can leave a block
     // empty -- plans on the host: its schedule is empty)
     const bool dev_plan = ctx->fast_pair && ctx->fast_sys && ctx->item_split == 0 &&
-                          ctx->shards.size() == 1 && ctx->rb.start[nb2] > 0 && !(dpv && std::string(dpv) == "0");
+                          ctx->shards.size() == 1 && ctx->rb.start[nb2] > 0 && dpv != "0";
     std::vector<FastBlockWork> entries;
     PairPlan dev_pp;
     DevBuf dev_pairs;
-    // MFHIP_DEVICE_PLAN: unset / 2 = the whole schedule on the device, 1 = host phase 1 + device
+    // MFHIP_TEST device_plan: unset / 2 = the whole schedule on the device, 1 = host phase 1 + device
     // emission, 0 = host
     const bool dev_full = dev_plan && dev_rb.total == ctx->rb.start[nb2] && dev_rb.urow.get();
     if (dev_full) {
@@ -1326,7 +1319,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
           recs += o[gg];
         }
       ctx->fast_prio_len = cells ? static_cast<int32_t>(std::max<int64_t>(16, 3 * recs / cells)) : (1 << 30);
-      if (const char* v = std::getenv("MFHIP_PRIO_LEN")) ctx->fast_prio_len = std::atoi(v);
+      if (const char* v = exp_knob("MFHIP_PRIO_LEN")) ctx->fast_prio_len = std::atoi(v);
     }
     ctx->fast_rb_size.assign(nb2, 0);
     for (int64_t b = 0; b < nb2; ++b) ctx->fast_rb_size[b] = ctx->rb.size(b);
@@ -1340,9 +1333,8 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
     ctx->fast_dummy_u = dummy;
     ctx->fast_dummy_i = static_cast<uint32_t>(ctx->I.rows());
     {
-      const char* ov = std::getenv("MFHIP_RING_OVERLAP");
       ctx->ring_overlap = ctx->fast_pair && ctx->fast_sys && ctx->G > 1 && ctx->c >= 2 &&
-                          ctx->item_split == 0 && !(ov && std::string(ov) == "0");
+                          ctx->item_split == 0 && test_knob("ring_overlap") != "0";
     }
     for (auto& s : ctx->shards) {
       ensure_rows(ctx, s, kSideU, ctx->U.rows() + 2);
@@ -1398,8 +1390,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
           s.st_sys_off = pp.sys_off;
           s.st_sys_block_off = pp.sys_block_off;
           s.st_place.release();
-          if (!(std::getenv("MFHIP_SYS_PLACE") && std::string(std::getenv("MFHIP_SYS_PLACE")) == "0") &&
-              !pp.sys_waves.empty()) {
+          if (test_knob("sys_place") != "0" && !pp.sys_waves.empty()) {
             std::vector<int32_t> place(pp.sys_waves.size(), 0);
             for (int32_t sm = 0; sm < ctx->nb; ++sm) {
               const int64_t w0 = pp.sys_off[sm], nw = pp.sys_off[sm + 1] - w0;
@@ -1424,7 +1415,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
         }
         clk.lap("pair plan + H2D");
         ctx->reaper.drop(pp.recs);
-        if (std::getenv("MFHIP_WAVE_TRACE")) {
+        if (exp_knob("MFHIP_WAVE_TRACE")) {
           const size_t n = ctx->fast_sys ? pp.sys.size() : pp.waves.size();
           const size_t per = ctx->fast_sys ? 32 : 16;  // systolic: realtime and shader-clock stamps
           s.st_trace.alloc(std::max<size_t>(n, 1) * per);
@@ -1661,13 +1652,12 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
   const int k = ctx->P.num_factors;
   PhaseClock clk;
   std::vector<int32_t> fu, fi;
-  // one persistent launch (the default; MFHIP_ONLINE_KERNEL=level forces the level-by-level
+  // one persistent launch (the default; MFHIP_TEST online_kernel=level forces the level-by-level
   // replay, which is also the path with per-rating outputs): NFLX 1M-rating batches 1.1e8 vs
   // 0.5e8 ratings/s end to end
   const bool outs = uout || iout;
-  const char* okv = std::getenv("MFHIP_ONLINE_KERNEL");
   int cap = 0;
-  if (n > 0 && !outs && !(okv && std::string(okv) == "level")) {
+  if (n > 0 && !outs && test_knob("online_kernel") != "level") {
     DeviceGuard g(s.device);
     cap = online_sweep_capacity(k, ctx->f64);  // 0 (occupancy query failed): the level replay
   }
@@ -1785,7 +1775,7 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
     // sequence order, and per update the number of earlier updates of its user (its ticket value)
     DeviceGuard g(s.device);
     int64_t wmax = 4096;
-    if (const char* v = std::getenv("MFHIP_ONLINE_WAVES")) wmax = std::max(1, std::atoi(v));  // experiments
+    if (const char* v = exp_knob("MFHIP_ONLINE_WAVES")) wmax = std::max(1, std::atoi(v));
     const int64_t W = std::max<int64_t>(1, std::min<int64_t>({static_cast<int64_t>(cap / 2), wmax, n}));
     const uint32_t W32 = static_cast<uint32_t>(W);
     // the batch in sequence order goes up as is (16 bytes an update); the per-wave lists and the
@@ -1841,7 +1831,7 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
       // in the index: the model is partly updated, so the context refuses further work (as the
       // DSGD sweeps do, sync_all) until a fit is prepared again
       ctx->failed = "online sweep: a wave waited > 1 s for a user ticket (waves not co-resident?); "
-                    "set MFHIP_ONLINE_KERNEL=level";
+                    "set MFHIP_TEST=online_kernel=level";
       fail(MF_ERR_TIMEOUT, ctx->failed);
     }
     if (tu) *tu = touched[0];
@@ -2456,6 +2446,15 @@ const char* mf_fast_kernel_name(int32_t k) {
     case FastKernel::kPersistent: return "k_fast_superstep";
     default: return "k_fast_substep";
   }
+}
+
+int32_t mf_debug_build_flags(void) { return mfhip::kExperiments ? 1 : 0; }
+
+int mf_debug_device_bytes(int64_t out[2]) {
+  if (!out) return MF_ERR_INVALID;
+  out[0] = mfhip::dev_bytes_live().load();
+  out[1] = mfhip::dev_bytes_peak().load();
+  return MF_OK;
 }
 
 int mf_debug_plan_digest(mf_ctx* ctx, uint64_t out[2]) {

@@ -106,6 +106,7 @@ struct Chunk {
   uint32_t flags;
   float era, erb;           // eta * r
   float aa, ab, ba, bb;     // 1 - eta * ri, 1 - eta * ru (1 for no-op records)
+  float sr, m;              // 1 - split; split ? 1 : aa (B's coupling to A's update)
 };
 
 // A chunk's records as loaded (raw words, one pair per lane).  The next chunk is loaded a whole
@@ -151,5 +152,17 @@ __device__ __forceinline__ Chunk chunk_convert(const ChunkRaw& r, float eta) {
   ch.bb = fmaf(-eta, __uint_as_float(r.w3[0]), 1.f);
   ch.aa = fmaf(-eta, __uint_as_float(r.w3[1]), 1.f);
   ch.ab = fmaf(-eta, __uint_as_float(r.w3[2]), 1.f);
+  const bool split = (r.w2[0] & kPairSplit) != 0;
+  ch.sr = split ? 0.f : 1.f;
+  ch.m = split ? 1.f : ch.aa;  // == fmaf(sr, aa - 1, 1) exactly: aa - 1 and its sum with 1 are exact
   return ch;
+}
+
+// -eta in a VGPR: the per-pair scalar recurrence runs in the chunk layout (lane s = pair s), where
+// each step reads one SGPR (a wave sum) and takes -eta from a register, so no SGPR is copied to a
+// VGPR first (one SGPR per VALU instruction on gfx9).
+__device__ __forceinline__ float vgpr_of(float x) {
+  float v;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "s"(x));
+  return v;
 }

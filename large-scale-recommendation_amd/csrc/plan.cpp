@@ -1163,7 +1163,9 @@ void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, in
           }
         }
       }
-      if (single) pp.waves[w_this].cells = kWaveSingleRun;
+      bool fwd = false;  // A rows forwarded from the previous pair: the lean path's FWD instance
+      for (const PairRec* r = first; single && r < out; ++r) fwd = fwd || (r->flags & (kPairFwdA | kPairFwdB));
+      if (single) pp.waves[w_this].cells = fwd ? kWaveSingleRunFwd : kWaveSingleRun;
       else if (g_plan_debug) g_not_single[why]++;
       // what the kernel requests: the 64-B record of every pair and every row access with an
       // in-range offset (the lean path: the item row once in, once out, B's row stored where
@@ -1254,7 +1256,7 @@ std::vector<int32_t> choose_block_groups(const std::vector<int64_t>& size, const
   const int64_t nb2 = static_cast<int64_t>(nb) * nb;
   std::vector<int32_t> Gb(nb2, 0);
   double cell_ns = kSysCellNs, pair_ns = kSysPairNs, run_ns = kSysRunPairNs;
-  if (const char* v = std::getenv("MFHIP_SYS_MODEL"))  // tuning knob: "cell_ns,pair_ns,run_pair_ns"
+  if (const char* v = exp_knob("MFHIP_SYS_MODEL"))  // tuning knob: "cell_ns,pair_ns,run_pair_ns"
     std::sscanf(v, "%lf,%lf,%lf", &cell_ns, &pair_ns, &run_ns);
   auto wave_ns = [&](int64_t b, int32_t G) {
     const double per_group = static_cast<double>(size[b]) / G;

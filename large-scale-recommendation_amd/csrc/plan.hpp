@@ -263,7 +263,8 @@ constexpr uint32_t kPairFwdB = 1u << 8;    // A's user row = previous pair's B r
 constexpr uint32_t kPairKeepQ = 1u << 16;  // A continues the item row held in registers
 constexpr uint32_t kPairSplit = 1u << 24;  // B's item differs from A's (B starts a run)
 constexpr int32_t kWaveGeneric = 1;    // WaveDesc.cells: generic pair steps
-constexpr int32_t kWaveSingleRun = 2;  // the cell is one item run: no item traffic per pair
+constexpr int32_t kWaveSingleRun = 2;  // the cell is one item run with no forwarded user row: no item traffic per pair
+constexpr int32_t kWaveSingleRunFwd = 3;  // one item run, some A rows forwarded from the previous pair
 struct PairRec {
   uint32_t ua, ub, ia, ib;   // loads: users A and B; items of A (run start) and B (split)
   uint32_t sa, sb, sia, si;  // stores: users A and B; A's item (split), the item after B (run end)

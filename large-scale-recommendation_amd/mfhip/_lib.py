@@ -99,7 +99,8 @@ EXPORTS = [
 # The test hooks include/mfhip_testing.h declares (not product surface; same library).
 TESTING_EXPORTS = [
     "mf_debug_levels", "mf_debug_fast_schedule", "mf_debug_fast_split", "mf_debug_ring_schedule",
-    "mf_debug_plan_digest", "mf_fast_plan_window", "mf_fast_kernel_name",
+    "mf_debug_plan_digest", "mf_fast_plan_window", "mf_fast_kernel_name", "mf_debug_build_flags",
+    "mf_debug_device_bytes",
 ]
 
 _i32p = C.POINTER(C.c_int32)
@@ -170,8 +171,12 @@ def lib() -> C.CDLL:
                                            _f64p, _f64p]),
         "mf_debug_ring_schedule": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int64, _i32p, _i32p, _i32p, _i32p]),
         "mf_debug_plan_digest": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
+        "mf_debug_build_flags": (C.c_int32, []),
+        "mf_debug_device_bytes": (C.c_int, [_i64p]),
     }
     for name, (res, args) in sig.items():
+        if name in TESTING_EXPORTS and not hasattr(L, name):
+            continue  # an older build (A/B runs): its test hooks may predate this binding
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args

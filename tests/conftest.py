@@ -26,6 +26,20 @@ def _built():
     yield
 
 
+def set_knob(monkeypatch, key, value):
+    """One of the library's test overrides, MFHIP_TEST="key=value,..." (csrc/common.hpp test_knob;
+    restored by monkeypatch at teardown)."""
+    cur = dict(x.split("=", 1) for x in os.environ.get("MFHIP_TEST", "").split(",") if "=" in x)
+    cur[key] = str(value)
+    monkeypatch.setenv("MFHIP_TEST", ",".join(f"{a}={b}" for a, b in cur.items()))
+
+
+def experiments_built():
+    """True when libmfhip was built with -DMFHIP_EXPERIMENTS (make EXPERIMENTS=1)."""
+    from mfhip import _lib as L
+    return bool(L.lib().mf_debug_build_flags() & 1)
+
+
 def golden(name):
     import numpy as np
     return dict(np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False))

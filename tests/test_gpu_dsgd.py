@@ -5,11 +5,18 @@ import pytest
 import coracle
 import mf_oracle as O
 import mfhip
-from conftest import golden
+from conftest import experiments_built, golden, set_knob
 from mfhip import _lib as L
 from mfhip import synth
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def needs_experiments():
+    """Hot-item replicas (MFHIP_ITEM_SPLIT) exist only in an EXPERIMENTS=1 build of libmfhip."""
+    if not experiments_built():
+        pytest.skip("libmfhip built without MFHIP_EXPERIMENTS (make EXPERIMENTS=1)")
 
 
 def params(k, iterations, nb, seed, mode=L.MODE_DETERMINISTIC_F64, lam=1.0, lr=0.001, fast_waves=0, has_seed=1,
@@ -307,6 +314,7 @@ def test_fast_kernel_equals_its_schedule(k, nb, G, hot):
 
 
 @pytest.mark.parametrize("k,nb,G,split", [(128, 1, 4, 60), (64, 2, 8, 40), (256, 1, 8, 100), (40, 2, 4, 50)])
+@pytest.mark.usefixtures("needs_experiments")
 def test_hot_item_replicas_equal_their_schedule(monkeypatch, k, nb, G, split):
     """MFHIP_ITEM_SPLIT (experiment): fork (replica rows), the sweep over replica rows, and the averaging join
     == a sequential f64 replay of the same plan with the same fork/join."""
@@ -323,14 +331,15 @@ def test_hot_item_replicas_equal_their_schedule(monkeypatch, k, nb, G, split):
     np.testing.assert_allclose(a_i, I, rtol=2e-4, atol=2e-5)
 
 
+@pytest.mark.usefixtures("needs_experiments")
 def test_hot_item_replicas_systolic_equals_substep(monkeypatch):
     """Replicas under the systolic sweep (automatic per-block groups) == per-sub-step launches, bitwise."""
     d = synth.generate(20000, 3000, 400_000, seed=4)
     outs = []
-    monkeypatch.setenv("MFHIP_BLOCK_GROUPS", "0")  # the same uniform G for both drivers
+    set_knob(monkeypatch, "block_groups", "0")  # the same uniform G for both drivers
     monkeypatch.setenv("MFHIP_ITEM_SPLIT", "300")
     for sys_on in ("1", "0"):
-        monkeypatch.setenv("MFHIP_PAIR_SYS", sys_on)
+        set_knob(monkeypatch, "pair_sys", sys_on)
         with mfhip.Context(params(128, 2, 4, 1, mode=L.MODE_FAST_F32)) as ctx:
             ctx.fit(d.u, d.i, d.r)
             outs.append((ctx.factors(0)[1], ctx.factors(1)[1], ctx.stats()["kernel_launches"]))
@@ -338,6 +347,7 @@ def test_hot_item_replicas_systolic_equals_substep(monkeypatch):
     assert outs[0][2] < outs[1][2]
 
 
+@pytest.mark.usefixtures("needs_experiments")
 def test_hot_item_replicas_multi_shard_matches_single(monkeypatch):
     """Replica rows are per-shard scratch outside the rotated item blocks: virtual shards agree."""
     d = synth.generate(3000, 600, 100_000, seed=12)
@@ -350,6 +360,7 @@ def test_hot_item_replicas_multi_shard_matches_single(monkeypatch):
     assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
 
 
+@pytest.mark.usefixtures("needs_experiments")
 def test_hot_item_replicas_rmse_within_one_percent_of_reference(monkeypatch):
     """Replicas relax the hot items' sequential chains, so they change the trajectory (averaged
     chains): an opt-in with a looser bar than the default fast mode -- held-out RMSE after 10
@@ -422,9 +433,9 @@ def test_systolic_sweep_equals_substep_launches(monkeypatch, k, nb, G, hot, n):
     else:
         d = synth.generate(max(400, n // 50), max(120, n // 300), n, seed=k)
     outs = []
-    monkeypatch.setenv("MFHIP_BLOCK_GROUPS", "0")  # the same uniform G for both drivers
+    set_knob(monkeypatch, "block_groups", "0")  # the same uniform G for both drivers
     for sys_on in ("0", "1"):
-        monkeypatch.setenv("MFHIP_PAIR_SYS", sys_on)
+        set_knob(monkeypatch, "pair_sys", sys_on)
         with mfhip.Context(params(k, 2, nb, 3, mode=L.MODE_FAST_F32, fast_waves=-G if G else 0,
                                   blocking=L.BLOCKING_REFERENCE)) as ctx:
             ctx.fit(d.u, d.i, d.r)
@@ -434,7 +445,7 @@ def test_systolic_sweep_equals_substep_launches(monkeypatch, k, nb, G, hot, n):
 
 
 def test_systolic_multi_shard_matches_single(monkeypatch):
-    monkeypatch.setenv("MFHIP_PAIR_SYS", "1")
+    set_knob(monkeypatch, "pair_sys", "1")
     d = synth.generate(2000, 500, 60000, seed=9)
     outs = []
     for devs in ([0], [0, 0]):
@@ -448,7 +459,7 @@ def test_systolic_multi_shard_matches_single(monkeypatch):
 def test_systolic_per_block_groups_equal_their_schedule(monkeypatch, k, nb, waves, hot):
     """Automatic G: every rating block of a superstep gets its own G_j x G_j rotation
     (choose_block_groups, budget `waves` per superstep); the kernel == sequential replay of that plan."""
-    monkeypatch.setenv("MFHIP_SYS_WAVES", str(waves))
+    set_knob(monkeypatch, "sys_waves", str(waves))
     d = hot_item_data(k) if hot else synth.generate(3000, 600, 60000, seed=k)
     seed, lam, lr, iters = 3, 1.0, 0.002, 2
     uids, U, iids, I = fast_replay_reference(d, k, nb, seed, -waves, iters, lam, lr)
@@ -490,8 +501,8 @@ def test_ring_overlap_split_launches_bitwise(monkeypatch, shards, nb):
     while the leaving block moves on a third stream as soon as A is done (the north star's ring
     exchange overlapped with compute).  Scheduling only: factors bitwise equal to the same plan
     without the overlap and to one shard."""
-    monkeypatch.setenv("MFHIP_PAIR_SYS", "1")
-    monkeypatch.setenv("MFHIP_BLOCK_GROUPS", "0")  # the same uniform G on every path
+    set_knob(monkeypatch, "pair_sys", "1")
+    set_knob(monkeypatch, "block_groups", "0")  # the same uniform G on every path
     d = hot_item_data(64)
     big = synth.generate(4000, 900, 120000, seed=31)
     d.u = np.concatenate([d.u, big.u + 500])
@@ -499,7 +510,7 @@ def test_ring_overlap_split_launches_bitwise(monkeypatch, shards, nb):
     d.r = np.concatenate([d.r, big.r])
     outs = []
     for devs, ov in (([0], "1"), ([0] * shards, "0"), ([0] * shards, "1")):
-        monkeypatch.setenv("MFHIP_RING_OVERLAP", ov)
+        set_knob(monkeypatch, "ring_overlap", ov)
         with mfhip.Context(params(64, 2, nb, 5, mode=L.MODE_FAST_F32, fast_waves=-8), devices=devs) as ctx:
             ctx.fit(d.u, d.i, d.r)
             outs.append((ctx.factors(0)[1], ctx.factors(1)[1], ctx.stats()["kernel_launches"]))
@@ -527,7 +538,7 @@ def test_device_blocking_equals_host_blocking(monkeypatch, mode, k, nb, seed):
     r = np.concatenate([d.r, d.r[:3000][::-1]])
     outs = []
     for host in ("1", "0"):
-        monkeypatch.setenv("MFHIP_HOST_BLOCKING", host)
+        set_knob(monkeypatch, "host_blocking", host)
         with mfhip.Context(params(k, 2, nb, seed, mode=mode)) as ctx:
             ctx.fit(u, i, r)
             outs.append([ctx.factors(s) for s in (0, 1)])
@@ -540,7 +551,7 @@ def test_device_blocking_equals_host_blocking(monkeypatch, mode, k, nb, seed):
                                        (64, 8, "tiny")])
 def test_device_plan_equals_host_plan(monkeypatch, k, nb, kind):
     """The fast schedule built on the device (kernels_plan.hip: the per-cell emission and pair
-    records, and with MFHIP_DEVICE_PLAN=2 the cell-major order and spreading too) is bitwise the host's (plan.cpp build_fast_plan + build_pair_plan):
+    records, and with MFHIP_TEST device_plan=2 the cell-major order and spreading too) is bitwise the host's (plan.cpp build_fast_plan + build_pair_plan):
     same pair records, wave and systolic tables (digest), same padding and requested bytes, and
     so the same factors after a fit."""
     if kind == "hot":
@@ -551,7 +562,7 @@ def test_device_plan_equals_host_plan(monkeypatch, k, nb, kind):
         d = synth.generate(6000, 1500, 400000, seed=17)
     res = {}
     for flag in ("0", "1", "2"):  # host / device emission / whole schedule on the device
-        monkeypatch.setenv("MFHIP_DEVICE_PLAN", flag)
+        set_knob(monkeypatch, "device_plan", flag)
         with mfhip.Context(params(k, 2, nb, 5, mode=L.MODE_FAST_F32)) as ctx:
             ctx.prepare(d.u, d.i, d.r)
             dig = ctx.plan_digest()

@@ -7,7 +7,7 @@ import pytest
 import coracle
 import mf_oracle as O
 import mfhip
-from conftest import golden
+from conftest import set_knob, golden
 from mfhip import _lib as L
 
 pytestmark = pytest.mark.gpu
@@ -180,7 +180,7 @@ def test_per_rating_outputs_bit_exact(flavour, name):
 def test_online_sweep_equals_level_replay(monkeypatch, mode, k):
     """The one-launch online sweep (the default: per-item waves, per-user tickets, k_online_sweep,
     its wave lists and tickets built on the device by kernels_online.hip) gives the factors of the
-    level-by-level replay (MFHIP_ONLINE_KERNEL=level) bit for bit, including a hot item, repeated
+    level-by-level replay (MFHIP_TEST online_kernel=level) bit for bit, including a hot item, repeated
     (user, item) pairs and ids first seen in a later batch."""
     rng = np.random.default_rng(7)
     n = 120000
@@ -190,7 +190,7 @@ def test_online_sweep_equals_level_replay(monkeypatch, mode, k):
     r = rng.integers(1, 6, n).astype(np.float64)
     res = {}
     for kern in ("level", "sweep"):
-        monkeypatch.setenv("MFHIP_ONLINE_KERNEL", kern)
+        set_knob(monkeypatch, "online_kernel", kern)
         p = L.default_params()
         p.num_factors, p.mode, p.online_learning_rate = k, mode, 0.01
         with mfhip.Context(p) as ctx:
@@ -221,7 +221,7 @@ def test_online_sweep_edge_batches(monkeypatch, shape, k):
     flav = L.ONLINE_SPARK_SWEEP if shape == "spark" else L.ONLINE_NEXT_FACTORS
     res = {}
     for kern in ("level", "sweep"):
-        monkeypatch.setenv("MFHIP_ONLINE_KERNEL", kern)
+        set_knob(monkeypatch, "online_kernel", kern)
         p = L.default_params()
         p.num_factors, p.mode, p.online_learning_rate = k, L.MODE_FAST_F32, 0.01
         with mfhip.Context(p) as ctx:

@@ -25,7 +25,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     ("det", ["--users", "30000"])])
 def test_rank_mode_staged_eval_matches_single_context(mode, extra):
     env = dict(os.environ, MFHIP_FAKE_HOSTS="1", MFHIP_DEVICE_SHARERS="2", NCCL_DEBUG="WARN",
-               MFHIP_RING_OVERLAP="1")
+               MFHIP_TEST="ring_overlap=1")
     port = 29611 + len(extra) + (10 if mode == "det" else 0)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "tools", "rank_check.py"),

@@ -23,7 +23,7 @@ only = sys.argv[3] if len(sys.argv) > 3 else ""  # run only cases whose label st
 def run(u, i, groups, label, kern):
     if only and not label.startswith(only):
         return
-    os.environ["MFHIP_FAST_KERNEL"] = kern
+    os.environ["MFHIP_TEST"] = f"fast_kernel={kern}"
     p = L.default_params()
     p.num_factors, p.num_blocks, p.mode, p.fast_waves, p.iterations = k, 1, L.MODE_FAST_F32, -groups, 1
     ctx = mfhip.Context(p)

@@ -5,7 +5,8 @@
 #
 # Steps run in order, each under its own time limit; the first failure ends the call (nothing more
 # touches the GPU after a fault, an abort or a time limit).  Outputs go to gpurun_out/<out-dir-name>/.
-#   test:<pytest args>                     pytest -m gpu (one process), log test_<n>.log
+#   test:<pytest args>                     pytest -m gpu (one process), log test_<n>.log (args are
+#                                          shell-parsed: quote a -k expression)
 #   smoke                                  __graft_entry__.smoke()
 #   bench:<tag>:<bench.py args>            one bench line -> <tag>.json, summary printed
 #   ab:<tag>:<reps>:<envA>|<envB>[|...]:<bench.py args>
@@ -14,6 +15,11 @@
 #                                          rocprofv3 --kernel-trace --stats, then separate --pmc FETCH_SIZE
 #                                          and --pmc WRITE_SIZE passes, summarised per launch of <kernel>
 #                                          (tools/pmc_summary.py) -> traffic_<tag>.json, stats_<tag>.csv
+#   pmc:<tag>:<counters>:<bench.py args>   one rocprofv3 --pmc pass (counters space-separated, within one
+#                                          pass's block budget) -> pmc_<tag>/ (tools/pmc_breakdown.py)
+#   rank:<world>:<rank_check.py args>      rank mode (RCCL ring) rehearsal on one GPU: <world> ranks share
+#                                          device 0 with distinct RCCL host ids (MFHIP_FAKE_HOSTS), checked
+#                                          against a single-process context (tools/rank_check.py)
 #   micro:<src.hip>[:<hipcc flags>]        build a tools/micro benchmark and run it
 #   cmd:<shell command>                    anything else (300 s limit)
 set -o pipefail
@@ -46,7 +52,7 @@ for step in "$@"; do
   echo "== step $n: $step"
   case $kind in
     test)
-      timeout -k 10 1100 python -u -m pytest $rest -m gpu -v --timeout 300 --timeout-method thread > "$O/test_$n.log" 2>&1 \
+      eval "timeout -k 10 1100 python -u -m pytest $rest -m gpu -v --timeout 300 --timeout-method thread" > "$O/test_$n.log" 2>&1 \
         || { echo "pytest failed"; grep -E "FAILED|Error|Timeout" "$O/test_$n.log" | head -20; tail -3 "$O/test_$n.log"; exit 1; }
       tail -1 "$O/test_$n.log" ;;
     smoke)
@@ -89,6 +95,19 @@ for step in "$@"; do
       rm -rf "$O/fetch_$tag" "$O/write_$tag"
       echo "traffic $tag: $(tr -d '\n ' < "$O/traffic_$tag.json" | cut -c1-260)"
       head -6 "$O/stats_$tag.csv" | cut -c1-150 ;;
+    pmc)
+      IFS=':' read -r tag ctrs args <<< "$rest"
+      cd /tmp
+      timeout -s KILL 400 rocprofv3 --pmc $ctrs -d "$O/pmc_$tag" -o pmc --output-format csv -- python3 "$R/bench.py" $args \
+        > "$O/pmc_$tag.log" 2>&1 || { echo "pmc $tag failed"; tail -5 "$O/pmc_$tag.log"; exit 1; }
+      cd "$R"
+      echo "pmc $tag: $(ls "$O"/pmc_$tag/*counter_collection.csv | head -1)" ;;
+    rank)
+      w=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args=""
+      MFHIP_FAKE_HOSTS=1 MFHIP_DEVICE_SHARERS=$w NCCL_DEBUG=WARN timeout -k 10 1100 python -m torch.distributed.run \
+        --nnodes=1 --nproc-per-node "$w" --master-addr 127.0.0.1 --master-port $((29500 + n)) tools/rank_check.py $args \
+        > "$O/rank_$n.log" 2>&1 || { echo "rank check failed"; tail -20 "$O/rank_$n.log"; exit 1; }
+      grep -E "world=|RANK_CHECK|rank [0-9]+:" "$O/rank_$n.log" | head -40 ;;
     micro)
       src=${rest%%:*}; flags=${rest#*:}; [ "$flags" = "$rest" ] && flags=""
       b=$(basename "$src" .hip)

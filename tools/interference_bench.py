@@ -14,7 +14,7 @@ k = 128
 
 
 def run(H, B, groups, kern, nb=1):
-    os.environ["MFHIP_FAST_KERNEL"] = kern
+    os.environ["MFHIP_TEST"] = f"fast_kernel={kern}"
     rng = np.random.default_rng(1)
     nu = max(H, B // 4 + 1)
     u = np.concatenate([rng.permutation(nu)[:H], rng.integers(0, nu, B)]).astype(np.int32)

@@ -78,7 +78,7 @@ int main(int argc, char** argv) {
               const WaveDesc& d = pp.sys[sw.cell0 + t];
               if (d.steps == 0) continue;
               ++cells;
-              (d.cells == kWaveSingleRun ? runp : mixp) += d.steps;
+              ((d.cells == kWaveSingleRun || d.cells == kWaveSingleRunFwd) ? runp : mixp) += d.steps;
             }
             std::printf("SCALE G %d rank %d sm %d wave %lld cells %lld run %lld mix %lld\n", G, g, sm,
                         (long long)(w - pp.sys_off[sm]), (long long)cells, (long long)runp, (long long)mixp);
@@ -104,7 +104,7 @@ int main(int argc, char** argv) {
     for (const WaveDesc& w : pp.waves)
       for (int64_t x = w.base; x < w.base + w.steps; ++x) {
         const PairRec& r = pp.recs[x];
-        if (w.cells == kWaveSingleRun) {
+        if (w.cells == kWaveSingleRun || w.cells == kWaveSingleRunFwd) {
           ++run_pairs;
           run_oob += (r.ua == kOffOOB) + (r.ub == kOffOOB) + (r.sa == kOffOOB) + (r.sb == kOffOOB);
         } else {
@@ -121,7 +121,7 @@ int main(int argc, char** argv) {
                 run_oob / double(std::max<int64_t>(run_pairs, 1)));
     int64_t fwd_pairs = 0, fwd_cells = 0, run_cells = 0, pad_b = 0;
     for (const WaveDesc& w : pp.waves) {
-      if (w.cells != kWaveSingleRun) continue;
+      if (w.cells != kWaveSingleRun && w.cells != kWaveSingleRunFwd) continue;
       ++run_cells;
       bool any = false;
       for (int64_t x = w.base; x < w.base + w.steps; ++x) {
@@ -138,7 +138,7 @@ int main(int argc, char** argv) {
     for (int BP : {4, 7, 8}) {
       int64_t blocks = 0, fwd_in = 0, fwd_first = 0, shared_prev = 0, shared_rows = 0, clean = 0;
       for (const WaveDesc& w : pp.waves) {
-        if (w.cells != kWaveSingleRun) continue;
+        if (w.cells != kWaveSingleRun && w.cells != kWaveSingleRunFwd) continue;
         std::vector<uint32_t> prev;
         for (int64_t x0 = w.base; x0 < w.base + w.steps; x0 += BP) {
           ++blocks;
@@ -184,12 +184,12 @@ int main(int argc, char** argv) {
     for (int64_t w = pp.sys_off[sm]; w < pp.sys_off[sm + 1]; ++w) {
       const SysWave& sw = pp.sys_waves[w];
       int64_t pairs = 0;
-      for (int t = 0; t < sw.G; ++t) { pairs += pp.sys[sw.cell0 + t].steps; singles += pp.sys[sw.cell0 + t].cells == kWaveSingleRun; }
+      for (int t = 0; t < sw.G; ++t) { pairs += pp.sys[sw.cell0 + t].steps; singles += pp.sys[sw.cell0 + t].cells >= kWaveSingleRun; }
       if (pairs > maxp) { maxp = pairs; maxw = w; }
     }
     int64_t ms = 0;
     const SysWave& sw = pp.sys_waves[maxw];
-    for (int t = 0; t < sw.G; ++t) ms += pp.sys[sw.cell0 + t].cells == kWaveSingleRun;
+    for (int t = 0; t < sw.G; ++t) ms += pp.sys[sw.cell0 + t].cells >= kWaveSingleRun;
     std::printf("sm %d waves %lld single cells %lld busiest wave %lld: G %d pairs %lld single cells %lld\n", sm,
                 (long long)waves_sm, (long long)singles, (long long)(maxw - pp.sys_off[sm]), sw.G, (long long)maxp,
                 (long long)ms);
