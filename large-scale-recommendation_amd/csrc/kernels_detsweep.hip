@@ -139,22 +139,25 @@ __device__ __forceinline__ void wait_vmcnt() {
 constexpr int kDetChunk = 16;
 
 
-template <int KPL, bool FULL>
-__global__ __launch_bounds__(64) void k_det_sweep2(const DetWave* __restrict__ waves, const uint32_t* __restrict__ eu,
-                                                   const uint32_t* __restrict__ ei, const uint32_t* __restrict__ eq,
-                                                   const double* __restrict__ er, double* U, double* I,
-                                                   uint64_t u_bytes, uint64_t i_bytes, const double* __restrict__ regU,
-                                                   const double* __restrict__ regI, int k, double eta,
-                                                   int32_t* ticket, int32_t* dummy_ticket, int32_t* err) {
+// One wave's entries.  SINGLE (DetWave::flags & kDetWaveSingleItem): every entry updates the same
+// item, so its row and lambda / omega are loaded once and stored once at the end, and an entry moves
+// only its user row.  Vector-memory operations per entry, in issue order (the wait before a
+// ticket is published counts on them -- change the entry, change NW):
+//   generic: publish 1 | user store KPL, item store KPL | user load KPL, item load KPL, ru 1, ri 1, poll 1
+//   SINGLE:  publish 1 | user store KPL                 | user load KPL,                ru 1,       poll 1
+// NW = the operations issued after entry j-2's stores up to entry j's publish: entry j-2's loads plus
+// all of entry j-1's: generic (2 KPL + 3) + (4 KPL + 4) = 6 KPL + 7, SINGLE (KPL + 2) + (2 KPL + 3) = 3 KPL + 5.
+template <int KPL, bool FULL, bool SINGLE>
+__device__ __forceinline__ void det_wave(const DetWave d, const uint32_t* __restrict__ eu, const uint32_t* __restrict__ ei,
+                                         const uint32_t* __restrict__ eq, const double* __restrict__ er, double* U,
+                                         double* I, uint64_t u_bytes, uint64_t i_bytes, const double* __restrict__ regU,
+                                         const double* __restrict__ regI, int k, double eta, int32_t* ticket,
+                                         int32_t* dummy_ticket, int32_t* err, double* lds) {
   constexpr int CH = kDetChunk;
-  constexpr int NW = 6 * KPL + 7;  // operations issued after an entry's stores until its ticket is published
+  constexpr int NW = SINGLE ? 3 * KPL + 5 : 6 * KPL + 7;
   static_assert(NW < 64, "vmcnt range");
-  __shared__ __attribute__((aligned(16))) double lds[64 * KPL];
   const int lane = threadIdx.x;
-  const DetWave d = waves[blockIdx.x];
   const int64_t cnt = d.count;
-  if (cnt == 0) return;
-  dummy_ticket += 16 * static_cast<int64_t>(blockIdx.x);  // this wave's own scratch line
   const __amdgpu_buffer_rsrc_t urs = raw_rsrc(U, u_bytes), irs = raw_rsrc(I, i_bytes);
   uint32_t voff[KPL];
 #pragma unroll
@@ -173,15 +176,18 @@ __global__ __launch_bounds__(64) void k_det_sweep2(const DetWave* __restrict__ w
   int32_t okP[2];  // the slot's user row was prefetched (its ticket was ready)
   int32_t tk[2];   // ticket polls, two entries ahead of the prefetch that reads them
   // prologue: entries 0 and 1 now (their tickets polled and read here), polls of entries 2 and 3
+  const uint32_t item0 = fi(0);  // SINGLE: the wave's one item
 #pragma unroll
   for (int x = 0; x < 2; ++x) {
     const bool live = x < cnt;
     const uint32_t u = fu(x), i = fi(x), q = fq(x);
     okP[x] = !live || poll(ticket + u) == static_cast<int32_t>(q & kDetUseqMask);
     P[x] = ldrow<KPL>(urs, voff, live && okP[x] ? u * rowb : kOOB);
-    Q[x] = ldrow<KPL>(irs, voff, live && !(x > 0 && (q & kDetKeepQ)) ? i * rowb : kOOB);
     RU[x] = ld_sc1(regU + (live ? u : 0u));
-    RI[x] = ld_sc1(regI + (live ? i : 0u));
+    if (!SINGLE || x == 0) {
+      Q[x] = ldrow<KPL>(irs, voff, live && !(x > 0 && (q & kDetKeepQ)) ? i * rowb : kOOB);
+      RI[x] = ld_sc1(regI + (live ? i : 0u));
+    }
   }
 #pragma unroll
   for (int x = 0; x < 2; ++x) tk[x] = poll_issue(x + 2 < cnt ? ticket + fu(x + 2) : dummy_ticket);
@@ -192,7 +198,8 @@ __global__ __launch_bounds__(64) void k_det_sweep2(const DetWave* __restrict__ w
   int32_t pv1 = 0;
   double q[KPL];
 #pragma unroll
-  for (int c = 0; c < KPL; ++c) q[c] = 0.0;
+  for (int c = 0; c < KPL; ++c) q[c] = SINGLE ? Q[0].v[c] : 0.0;
+  const double ri_single = SINGLE ? uniform(RI[0]) : 0.0;
 
   // one entry (chunk-relative s, a compile-time constant once unrolled)
 #if defined(MFHIP_EXPERIMENTS) && defined(MFHIP_DET_PROBE)
@@ -204,10 +211,12 @@ __global__ __launch_bounds__(64) void k_det_sweep2(const DetWave* __restrict__ w
 #endif
   auto entry = [&](const int s, const int64_t j) {
     const int slot = s & 1;
-    const uint32_t u = fu(s), i = fi(s), qf = fq(s);
+    const uint32_t u = fu(s), qf = fq(s);
+    const uint32_t i = SINGLE ? item0 : fi(s);
     const double r = rld(s < CH ? C0.r : C1.r, s);
     const int32_t useq = static_cast<int32_t>(qf & kDetUseqMask);
-    const uint32_t u2 = fu(s + 2), i2 = fi(s + 2), q2 = fq(s + 2), u4 = fu(s + 4);
+    const uint32_t u2 = fu(s + 2), q2 = fq(s + 2), u4 = fu(s + 4);
+    const uint32_t i2 = SINGLE ? item0 : fi(s + 2);
     // 1. the user row, when its ticket was not ready at prefetch time (rare): publish every
     //    pending ticket (after its stores), wait for ours, load now
     if (!okP[slot]) {
@@ -220,11 +229,11 @@ __global__ __launch_bounds__(64) void k_det_sweep2(const DetWave* __restrict__ w
       __builtin_amdgcn_s_waitcnt(0x0F70);
     }
     // 2. compute entry j (DSGDforMF.scala:405-410, the reference's rounding, no FMA)
-    if (!(qf & kDetKeepQ)) {
+    if (!SINGLE && !(qf & kDetKeepQ)) {
 #pragma unroll
       for (int c = 0; c < KPL; ++c) q[c] = Q[slot].v[c];
     }
-    const double ru = uniform(RU[slot]), ri = uniform(RI[slot]);
+    const double ru = uniform(RU[slot]), ri = SINGLE ? ri_single : uniform(RI[slot]);
     double pr[KPL], pn[KPL];
 #pragma unroll
     for (int c = 0; c < KPL; ++c) pr[c] = P[slot].v[c] * q[c];
@@ -248,16 +257,18 @@ __global__ __launch_bounds__(64) void k_det_sweep2(const DetWave* __restrict__ w
     pv1 = useq + 1;
     // 4. entry j's stores
     strow<KPL>(urs, voff, u * rowb, pn);
-    strow<KPL>(irs, voff, (qf & kDetDeferQ) ? kOOB : i * rowb, q);
+    if (!SINGLE) strow<KPL>(irs, voff, (qf & kDetDeferQ) ? kOOB : i * rowb, q);
     stamp(2);
     // 5. prefetch entry j+2 into this slot (after the stores: a reload of an item row this wave
     //    just stored sees it); its user row only if its ticket (polled at entry j-2) was ready
     const bool live2 = j + 2 < cnt;
     const int32_t okN = !live2 || __builtin_amdgcn_readfirstlane(tk[slot]) == static_cast<int32_t>(q2 & kDetUseqMask);
     P[slot] = ldrow<KPL>(urs, voff, live2 && okN ? u2 * rowb : kOOB);
-    Q[slot] = ldrow<KPL>(irs, voff, live2 && !(q2 & kDetKeepQ) ? i2 * rowb : kOOB);
     RU[slot] = ld_sc1(regU + (live2 ? u2 : 0u));
-    RI[slot] = ld_sc1(regI + (live2 ? i2 : 0u));
+    if (!SINGLE) {
+      Q[slot] = ldrow<KPL>(irs, voff, live2 && !(q2 & kDetKeepQ) ? i2 * rowb : kOOB);
+      RI[slot] = ld_sc1(regI + (live2 ? i2 : 0u));
+    }
     okP[slot] = okN;
     // 6. poll entry j+4's ticket (read at entry j+2)
     tk[slot] = poll_issue(j + 4 < cnt ? ticket + u4 : dummy_ticket);
@@ -283,6 +294,7 @@ __global__ __launch_bounds__(64) void k_det_sweep2(const DetWave* __restrict__ w
     C1 = chunk(c0 / CH + 2);
   }
 done:
+  if (SINGLE) strow<KPL>(irs, voff, item0 * rowb, q);  // the item row, once
   __builtin_amdgcn_s_waitcnt(0x0F70);
   publish(pend0, pv0, lane);
   publish(pend1, pv1, lane);
@@ -291,6 +303,24 @@ done:
     printf("[det probe] wave 0: %lld entries, cycles per entry: pre-fold %.0f fold %.0f post-fold %.0f prefetch %.0f\n",
            (long long)cnt, double(pc[0]) / cnt, double(pc[1]) / cnt, double(pc[2]) / cnt, double(pc[3]) / cnt);
 #endif
+}
+
+template <int KPL, bool FULL>
+__global__ __launch_bounds__(64) void k_det_sweep2(const DetWave* __restrict__ waves, const uint32_t* __restrict__ eu,
+                                                   const uint32_t* __restrict__ ei, const uint32_t* __restrict__ eq,
+                                                   const double* __restrict__ er, double* U, double* I,
+                                                   uint64_t u_bytes, uint64_t i_bytes, const double* __restrict__ regU,
+                                                   const double* __restrict__ regI, int k, double eta,
+                                                   int32_t* ticket, int32_t* dummy_ticket, int32_t* err) {
+  __shared__ __attribute__((aligned(16))) double lds[64 * KPL];
+  const DetWave d = waves[blockIdx.x];
+  if (d.count == 0) return;
+  dummy_ticket += 16 * static_cast<int64_t>(blockIdx.x);  // this wave's own scratch line
+  if (d.flags & kDetWaveSingleItem)
+    det_wave<KPL, FULL, true>(d, eu, ei, eq, er, U, I, u_bytes, i_bytes, regU, regI, k, eta, ticket, dummy_ticket, err, lds);
+  else
+    det_wave<KPL, FULL, false>(d, eu, ei, eq, er, U, I, u_bytes, i_bytes, regU, regI, k, eta, ticket, dummy_ticket, err,
+                               lds);
 }
 
 template <int KPL>

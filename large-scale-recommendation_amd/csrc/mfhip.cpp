@@ -424,15 +424,25 @@ void dump_wave_trace(mf_ctx* ctx) {
 
 // Joins the speculative builds of det_run.  invalidate: the training data, the layouts or the
 // superstep changes, so the builds are dropped (otherwise a later run may still use them).
+// A failed build is never used: its slot is marked empty before the error can surface, and when the
+// builds are being dropped (invalidate) their errors are dropped with them (MFHIP_DEBUG_PLAN logs
+// them) -- only a run that would take a build over reports its failure (det_run).
 void det_spec_wait(mf_ctx* ctx, bool invalidate) {
   std::exception_ptr first;
   for (int slot = 0; slot < kDetSlots; ++slot) {
     if (ctx->det_spec[slot].valid()) {
       try {
         ctx->det_spec[slot].get();
-      } catch (...) {
-        if (!first) first = std::current_exception();
+      } catch (const std::exception& e) {
         ctx->det_spec_s[slot] = -1;
+        if (invalidate) {
+          if (std::getenv("MFHIP_DEBUG_PLAN")) std::fprintf(stderr, "[mfhip] dropped speculative build: %s\n", e.what());
+        } else if (!first) {
+          first = std::current_exception();
+        }
+      } catch (...) {
+        ctx->det_spec_s[slot] = -1;
+        if (!invalidate && !first) first = std::current_exception();
       }
     }
     if (invalidate) ctx->det_spec_s[slot] = -1;
@@ -974,13 +984,17 @@ void det_run(mf_ctx* ctx, int64_t count) {
   // any other is joined and dropped (a taken-over build is waited for like the run's own)
   bool prebuilt[kDetSlots] = {false, false, false};
   for (int slot = 0; slot < kDetSlots; ++slot) {
-    if (slot < kAhead && slot < count && ctx->det_spec_s[slot] == s0 + slot) {
-      builds[slot] = std::move(ctx->det_spec[slot]);
+    const int64_t built = ctx->det_spec_s[slot];
+    ctx->det_spec_s[slot] = -1;  // before anything can throw: a slot is never taken over twice
+    if (slot < kAhead && slot < count && built == s0 + slot && ctx->det_spec[slot].valid()) {
+      builds[slot] = std::move(ctx->det_spec[slot]);  // joined (and its error raised) below, like a fresh build
       prebuilt[slot] = true;
     } else if (ctx->det_spec[slot].valid()) {
-      ctx->det_spec[slot].get();
+      try {
+        ctx->det_spec[slot].get();  // a build this run does not use: its failure does not matter
+      } catch (...) {
+      }
     }
-    ctx->det_spec_s[slot] = -1;
   }
   for (int slot = 0; slot < kDetSlots; ++slot) reclaim(slot);  // a previous call's last copies
   for (int64_t x = 0; x < std::min<int64_t>(count, kAhead); ++x)
@@ -989,7 +1003,7 @@ void det_run(mf_ctx* ctx, int64_t count) {
   for (int64_t x = 0; x < count; ++x) {
     const int64_t s = s0 + x;
     const int slot = static_cast<int>(x % kDetSlots);
-    if (builds[slot].valid()) builds[slot].get();
+    builds[slot].get();  // every superstep of the run has a build (taken over or started here)
     const int32_t iteration = static_cast<int32_t>(s / ctx->nb);  // :476
     const double eta = learning_rate(ctx->P.lr_method, ctx->P.learning_rate, iteration + 1, ctx->P.lambda,
                                      ctx->P.lr_arg);  // :383-386

@@ -471,12 +471,15 @@ void build_det_step(const RatingBlocks& rb, const SideLayout& U, const SideLayou
   parallel_tasks(nbk, [&](int64_t x) {
     const int32_t W = L.block_waves[blocks[x]];
     for (int32_t w = 0; w < W; ++w) {
-      const DetWave dw = out.waves[w0[x] + w];
+      DetWave& dw = out.waves[w0[x] + w];
       const int64_t a = dw.begin, z = dw.begin + dw.count;
+      bool single = z > a;
       for (int64_t y = a; y < z; ++y) {
         if (y > a && out.i[y - 1] == out.i[y]) out.qf[y] |= kDetKeepQ;
         if (y + 1 < z && out.i[y + 1] == out.i[y]) out.qf[y] |= kDetDeferQ;
+        single = single && out.i[y] == out.i[a];
       }
+      dw.flags = single ? kDetWaveSingleItem : 0;  // the sweep's lean path (one item row, loaded and stored once)
     }
   });
 }

@@ -129,8 +129,9 @@ constexpr uint32_t kDetDeferQ = 1u << 31;  // same item as the wave's next entry
 struct DetWave {
   int64_t begin;  // first entry
   int32_t count;
-  int32_t pad_;
+  int32_t flags;  // kDetWaveSingleItem
 };
+constexpr int32_t kDetWaveSingleItem = 1;  // every entry of the wave updates one item
 static_assert(sizeof(DetWave) == 16, "DetWave is one 16-B word");
 
 struct DetSweepLayout {

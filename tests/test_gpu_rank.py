@@ -18,6 +18,21 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def run_ranks(cmd, env, timeout):
+    """The launcher and its ranks in a process group of their own: on a timeout the whole group is
+    killed, so no rank is left holding the device."""
+    import signal
+    p = subprocess.Popen(cmd, env=env, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                         start_new_session=True)
+    try:
+        out, _ = p.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        out, _ = p.communicate()
+        return -9, (out or "") + "\n[timeout]"
+    return p.returncode, out
+
+
 @pytest.mark.parametrize("mode,extra", [
     ("fast", ["--fast-waves", "-8", "--k", "64"]),                       # rank 0 holds no rating
     ("fast", ["--fast-waves", "-8", "--k", "128", "--users", "30000"]),  # both ranks sweep, ring overlap
@@ -30,6 +45,22 @@ def test_rank_mode_staged_eval_matches_single_context(mode, extra):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "tools", "rank_check.py"),
            "--mode", mode, "--blocks", "4", "--staged"] + extra
-    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
-    out = r.stdout + r.stderr
-    assert r.returncode == 0 and "RANK_CHECK_OK" in out, out[-3000:]
+    rc, out = run_ranks(cmd, env, 240)
+    assert rc == 0 and "RANK_CHECK_OK" in out, out[-3000:]
+
+
+@pytest.mark.parametrize("mode,extra", [
+    ("det", []),                            # bitwise against one context: the reference order is plan-free
+    ("fast", ["--fast-waves", "-16"])])     # uniform G: bitwise against 8 in-process virtual shards
+def test_rank_mode_yahoo_shaped_world8(mode, extra):
+    """BASELINE config 4 (Yahoo-Music-shaped, k = 256, numBlocks = 8, "on 8 x MI355X") through the
+    rank path at 0.05 scale (91k users x 6.8k items x 36M ratings): 8 ranks share device 0, each
+    owning one user block, the item blocks rotating over the RCCL ring (DSGDforMF.scala:262-357,
+    611-619).  One epoch; factors compared bit for bit (tools/rank_check.py)."""
+    env = dict(os.environ, MFHIP_FAKE_HOSTS="1", MFHIP_DEVICE_SHARERS="8", NCCL_DEBUG="WARN")
+    port = 29661 + (10 if mode == "det" else 0)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "tools", "rank_check.py"),
+           "--mode", mode, "--config", "YAHOO", "--scale", "0.05", "--iterations", "1"] + extra
+    rc, out = run_ranks(cmd, env, 280)
+    assert rc == 0 and "RANK_CHECK_OK" in out, out[-3000:]

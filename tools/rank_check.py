@@ -89,9 +89,11 @@ def main():
     st = ctx.stats()
     mem2 = np.zeros(2, np.int64)
     L.lib().mf_debug_device_bytes(mem2.ctypes.data_as(L.C.POINTER(L.C.c_int64)))
+    import resource
+    rss = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20  # KiB -> GiB
     print(f"rank {rank}: updates {st['updates']} groups {st['groups']} pads {st['pads']} plan records {int(plan[1])} "
-          f"device bytes after prepare {mem[0] / 2**30:.2f} GiB, peak {mem2[1] / 2**30:.2f} GiB; "
-          f"prepare {t_prep:.1f} s, {p.iterations} epoch(s) {t_run:.1f} s", flush=True)
+          f"device bytes after prepare {mem[0] / 2**30:.2f} GiB, peak {mem2[1] / 2**30:.2f} GiB; host max RSS "
+          f"{rss:.1f} GiB; prepare {t_prep:.1f} s, {p.iterations} epoch(s) {t_run:.1f} s", flush=True)
     uids, uf = ctx.factors(L.SIDE_USER)
     iids, itf = ctx.factors(L.SIDE_ITEM)
     ctx.close()
