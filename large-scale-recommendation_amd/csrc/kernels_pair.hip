@@ -37,12 +37,19 @@ namespace {
 
 #include "pair_device.hpp"
 
+#ifdef MFHIP_EXP_ITEM_SC1
+constexpr int kItemPolicy = kSC1;
+#else
+constexpr int kItemPolicy = 0;
+#endif
+
 // A cell that is one item run (build_pair_plan): the item row stays in registers from the first
 // pair to the last, so a pair moves no item row, only user rows (4 VMEM operations).  B's user row
 // is stored where it was loaded from (its offset rides an SGPR ring).  FWD = false: so is A's (no
 // user repeats at the next record: kWaveSingleRun); FWD = true (kWaveSingleRunFwd): A's row may be
 // the previous pair's result (a user rating the item twice in a row), forwarded in registers.
-template <int KPL, int UP, bool FWD>
+// IP = cache policy of the item-row accesses (kItemPolicy)
+template <int KPL, int UP, bool FWD, int IP = kItemPolicy>
 __device__ __forceinline__ void single_run_cell(Chunk C0, ChunkRaw C1, __amdgpu_buffer_rsrc_t RR,
                                                 __amdgpu_buffer_rsrc_t urs, __amdgpu_buffer_rsrc_t irs, float eta,
                                                 uint32_t vlane, uint32_t voff, int npairs, uint64_t& wait_clk) {
@@ -51,7 +58,7 @@ __device__ __forceinline__ void single_run_cell(Chunk C0, ChunkRaw C1, __amdgpu_
   constexpr int CH = kPairChunk;
   constexpr int DS = kPairRingSingle;
   const uint32_t item_off = rl(C0.ia, 0);
-  Row<KPL> q = ld<KPL>(irs, voff, item_off);
+  Row<KPL> q = ld<KPL, IP>(irs, voff, item_off);
   Row<KPL> RA[DS], RB[DS], plA, plB;
 #pragma unroll
   for (int e = 0; e < NV; ++e) plA.v[e] = plB.v[e] = f2{0.f, 0.f};
@@ -119,13 +126,13 @@ __device__ __forceinline__ void single_run_cell(Chunk C0, ChunkRaw C1, __amdgpu_
     C1 = chunk_load(RR, c + 2, vlane);
   }
 run_done:
-  st<KPL>(irs, voff, item_off, q);
+  st<KPL, IP>(irs, voff, item_off, q);
 }
 
 // One cell (WaveDesc d) of the pair schedule, swept by the calling wave.  UP = cache policy of
 // the user-row loads and stores.  L0 / L1: the cell's first two record chunks, loaded by the
 // caller (the systolic sweep loads them while the previous cell's stores drain).
-template <int KPL, int D, int UP>
+template <int KPL, int D, int UP, int IP = kItemPolicy>
 __device__ __forceinline__ void pair_cell(const WaveDesc d, const ChunkRaw& L0, const ChunkRaw& L1,
                                           const u4v* __restrict__ recs, __amdgpu_buffer_rsrc_t urs,
                                           __amdgpu_buffer_rsrc_t irs, float eta, int lane, uint64_t& wait_clk) {
@@ -158,8 +165,8 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const ChunkRaw& L0, 
     do {                                                                        \
       PA[slot] = ld<KPL, UP>(urs, voff, rl(UA, (YY)));                              \
       PB[slot] = ld<KPL, UP>(urs, voff, rl(UB, (YY)));                              \
-      QA[slot] = ld<KPL>(irs, voff, rl(IA, (YY)));                              \
-      QB[slot] = ld<KPL>(irs, voff, rl(IB, (YY)));                              \
+      QA[slot] = ld<KPL, IP>(irs, voff, rl(IA, (YY)));                              \
+      QB[slot] = ld<KPL, IP>(irs, voff, rl(IB, (YY)));                              \
     } while (0)
 #pragma unroll
     for (int s = 0; s < D; ++s) MF_PREFETCH(s, C0.ua, C0.ub, C0.ia, C0.ib, s);
@@ -222,13 +229,13 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const ChunkRaw& L0, 
         }
         st<KPL, UP>(urs, voff, osa, plA);
         st<KPL, UP>(urs, voff, osb, plB);
-        st<KPL>(irs, voff, osia, q1);
-        st<KPL>(irs, voff, osi, q);
+        st<KPL, IP>(irs, voff, osia, q1);
+        st<KPL, IP>(irs, voff, osi, q);
         // rows of pair j+D (after this pair's stores)
         PA[slot] = ld<KPL, UP>(urs, voff, nua);
         PB[slot] = ld<KPL, UP>(urs, voff, nub);
-        QA[slot] = ld<KPL>(irs, voff, nia);
-        QB[slot] = ld<KPL>(irs, voff, nib);
+        QA[slot] = ld<KPL, IP>(irs, voff, nia);
+        QB[slot] = ld<KPL, IP>(irs, voff, nib);
       }
       C0 = chunk_convert(C1, eta);
       C1 = chunk_load(RR, c + 2, vlane);

@@ -464,7 +464,8 @@ void sync_all(mf_ctx* ctx) {
       MF_HIP(hipMemcpy(err4, eb->get(), std::min<size_t>(sizeof(err4), eb->bytes()), hipMemcpyDeviceToHost));
       const int32_t err = err4[0];
       if (err) {
-        MF_HIP(hipMemset(eb->get(), 0, std::min<size_t>(sizeof(err4), eb->bytes())));
+        MF_HIP(hipMemsetAsync(eb->get(), 0, std::min<size_t>(sizeof(err4), eb->bytes()), s.stream));
+        MF_HIP(hipStreamSynchronize(s.stream));
         if (std::getenv("MFHIP_DEBUG_PLAN") && eb->bytes() > 16) {
           std::vector<uint32_t> dg(eb->bytes() / 4);
           MF_HIP(hipMemcpy(dg.data(), eb->get(), eb->bytes(), hipMemcpyDeviceToHost));
@@ -472,7 +473,8 @@ void sync_all(mf_ctx* ctx) {
             if (dg[4 + 4 * w + 3])
               std::fprintf(stderr, "[mfhip] sweep timeout: wave slot %zu seen %u want %u published %u\n", w,
                            dg[4 + 4 * w], dg[4 + 4 * w + 1], dg[4 + 4 * w + 2]);
-          MF_HIP(hipMemset(eb->get(), 0, eb->bytes()));
+          MF_HIP(hipMemsetAsync(eb->get(), 0, eb->bytes(), s.stream));
+          MF_HIP(hipStreamSynchronize(s.stream));
         }
         // waves that gave up skipped the rest of their work: the model is partly updated, so
         // the context refuses further supersteps and reads until the fit is prepared again
@@ -1163,7 +1165,7 @@ void prepare_det_sweep(mf_ctx* ctx) {
     s.det_ticket.alloc(static_cast<size_t>(std::max<int64_t>(ctx->U.rows(), 1)) * 4);
     s.det_scratch.alloc(static_cast<size_t>(s.det_nw_max) * 64);  // one scratch line per wave
     s.det_err.alloc(16);
-    MF_HIP(hipMemset(s.det_err.get(), 0, 16));
+    MF_HIP(hipMemsetAsync(s.det_err.get(), 0, 16, s.stream));
   }
   ctx->det_sweep = true;
 }
@@ -1370,8 +1372,9 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
           MF_HIP(hipMemcpy(s.st_split.get(), tab.data(), tab.size() * sizeof(SplitItem), hipMemcpyHostToDevice));
       }
       const size_t row_bytes = static_cast<size_t>(ctx->P.num_factors) * ctx->es;
-      MF_HIP(hipMemset(s.uf.as<char>() + static_cast<size_t>(dummy) * row_bytes, 0, 2 * row_bytes));
-      MF_HIP(hipMemset(s.itf.as<char>() + static_cast<size_t>(ctx->fast_dummy_i) * row_bytes, 0, row_bytes));
+      MF_HIP(hipMemsetAsync(s.uf.as<char>() + static_cast<size_t>(dummy) * row_bytes, 0, 2 * row_bytes, s.stream));
+      MF_HIP(hipMemsetAsync(s.itf.as<char>() + static_cast<size_t>(ctx->fast_dummy_i) * row_bytes, 0, row_bytes,
+                            s.stream));
       if (ctx->fast_pair) {
         PairPlan pp;
         if (dev_plan) {
@@ -1423,9 +1426,9 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
           int64_t max_waves = 1;
           for (int32_t sm = 0; sm < ctx->nb; ++sm) max_waves = std::max(max_waves, pp.sys_off[sm + 1] - pp.sys_off[sm]);
           s.fast_prog.alloc(static_cast<size_t>(max_waves) * kProgStride * sizeof(int32_t));
-          MF_HIP(hipMemset(s.fast_prog.get(), 0, s.fast_prog.bytes()));
+          MF_HIP(hipMemsetAsync(s.fast_prog.get(), 0, s.fast_prog.bytes(), s.stream));
           s.fast_err.alloc(16);
-          MF_HIP(hipMemset(s.fast_err.get(), 0, 16));
+          MF_HIP(hipMemsetAsync(s.fast_err.get(), 0, 16, s.stream));
         }
         clk.lap("pair plan + H2D");
         ctx->reaper.drop(pp.recs);
@@ -1433,7 +1436,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
           const size_t n = ctx->fast_sys ? pp.sys.size() : pp.waves.size();
           const size_t per = ctx->fast_sys ? 32 : 16;  // systolic: realtime and shader-clock stamps
           s.st_trace.alloc(std::max<size_t>(n, 1) * per);
-          MF_HIP(hipMemset(s.st_trace.get(), 0, std::max<size_t>(n, 1) * per));
+          MF_HIP(hipMemsetAsync(s.st_trace.get(), 0, std::max<size_t>(n, 1) * per, s.stream));
           if (ctx->fast_sys) {
             s.st_sys_host = pp.sys;
             s.st_sysw_host = pp.sys_waves;
@@ -1477,7 +1480,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
         }
       s.fast_prog.alloc(static_cast<size_t>(ctx->c) * ctx->G_fast * kProgStride * sizeof(int32_t));
       s.fast_err.alloc(16);
-      MF_HIP(hipMemset(s.fast_err.get(), 0, 16));
+      MF_HIP(hipMemsetAsync(s.fast_err.get(), 0, 16, s.stream));
       s.fast_blks.alloc(blks.size() * sizeof(FastBlk));
       MF_HIP(hipMemcpy(s.fast_blks.get(), blks.data(), blks.size() * sizeof(FastBlk), hipMemcpyHostToDevice));
     }
@@ -1492,6 +1495,16 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
     ctx->reaper.release();
   }
   clk.lap("release host blocks");
+  // hipMemset on device memory returns before the fill is done and the legacy stream does not
+  // order the non-blocking sweep streams (tools/micro/memset_order.hip: a 4-GiB memset returns
+  // in 3 us and a kernel on another stream still reads the old bytes), so the zeroing above is
+  // issued on the shard streams, and the device drains here: the first superstep's launches
+  // (aux included, which waits on no event yet) see every table, zeroed row and progress word.
+  // A run of 8 ranks sharing one GPU raced here (stale progress words let waves skip a hand-off).
+  for (auto& s : ctx->shards) {
+    DeviceGuard g(s.device);
+    MF_HIP(hipDeviceSynchronize());
+  }
   ctx->superstep_done = 0;
   reset_item_loc(ctx);
   ctx->prepared = true;

@@ -106,8 +106,13 @@ for step in "$@"; do
       w=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args=""
       MFHIP_FAKE_HOSTS=1 MFHIP_DEVICE_SHARERS=$w NCCL_DEBUG=WARN timeout -k 10 1100 python -m torch.distributed.run \
         --nnodes=1 --nproc-per-node "$w" --master-addr 127.0.0.1 --master-port $((29500 + n)) tools/rank_check.py $args \
-        > "$O/rank_$n.log" 2>&1 || { echo "rank check failed"; tail -20 "$O/rank_$n.log"; exit 1; }
-      grep -E "world=|RANK_CHECK|rank [0-9]+:" "$O/rank_$n.log" | head -40 ;;
+        > "$O/rank_$n.log" 2>&1
+      rc=$?
+      grep -E "world=|RANK_CHECK|rank [0-9]+:|differing|superstep|STEPWISE|repeats" "$O/rank_$n.log" | head -60
+      # a failed bitwise comparison lets the next step run; anything else (a fault, an abort, a
+      # time limit) ends the call
+      [ $rc -eq 0 ] || { echo "rank check failed ($rc)"; tail -5 "$O/rank_$n.log";
+                         grep -q "AssertionError: rank mode is not bit-exact" "$O/rank_$n.log" || exit 1; } ;;
     micro)
       src=${rest%%:*}; flags=${rest#*:}; [ "$flags" = "$rest" ] && flags=""
       b=$(basename "$src" .hip)

@@ -18,6 +18,57 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "large-scale-recommendation_amd"))
 
 
+def row_hash(f):
+    """One 64-bit hash per factor row (bitwise: any differing bit changes it)."""
+    import numpy as np
+    b = np.ascontiguousarray(f).view(np.uint64)
+    mult = (np.arange(1, b.shape[1] + 1, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)) | np.uint64(1)
+    with np.errstate(over="ignore"):
+        return (b * mult).sum(axis=1, dtype=np.uint64)
+
+
+def stepwise(a, ctx, p, tu, ti, tr, rank, world, dist):
+    from mfhip import _lib as L
+    import mfhip
+    steps = p.iterations * p.num_blocks
+    trace = []
+    for s in range(steps):
+        ctx.run(1)
+        ctx.sync()
+        uids, uf = ctx.factors(L.SIDE_USER)
+        iids, itf = ctx.factors(L.SIDE_ITEM)  # (an all-gather of the item blocks: every rank calls it)
+        trace.append((uids, row_hash(uf), iids, row_hash(itf)))
+    ctx.close()
+    parts = [None] * world if rank == 0 else None
+    dist.gather_object(trace, parts, dst=0)
+    if rank == 0:
+        ref = mfhip.Context(p, devices=[0] * world) if a.fast_waves < 0 else mfhip.Context(p)
+        ref.prepare(tu, ti, tr)
+        first = None
+        for s in range(steps):
+            ref.run(1)
+            ref.sync()
+            ruids, ruf = ref.factors(L.SIDE_USER)
+            riids, ritf = ref.factors(L.SIDE_ITEM)
+            rhu, rhi = dict(zip(ruids.tolist(), row_hash(ruf).tolist())), row_hash(ritf)
+            du = {}
+            for r in range(world):
+                uids, hu, iids, hi = parts[r][s]
+                du[r] = int(sum(1 for x, h in zip(uids.tolist(), hu.tolist()) if rhu[x] != h))
+            iids, hi = parts[0][s][2], parts[0][s][3]
+            assert np.array_equal(iids, riids)
+            di = int(np.sum(hi != rhi))
+            dv = [int(np.sum(parts[r][s][3] != hi)) for r in range(world)]
+            print(f"superstep {s + 1}: differing user rows per rank {du}; differing item rows {di} "
+                  f"(rank views differing from rank 0's: {dv})", flush=True)
+            if first is None and (di or any(du.values())):
+                first = s + 1
+        ref.close()
+        print(f"STEPWISE first differing superstep: {first}", flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mode", default="det")
@@ -39,7 +90,19 @@ def main():
     ap.add_argument("--staged", action="store_true",
                     help="prepare + run + evaluate with no sync in between (the JNI dsgdPrepare / dsgdRun path): "
                          "evaluation must wait for the last superstep's overlapped launch and ring step itself")
+    ap.add_argument("--stepwise", action="store_true",
+                    help="run one superstep at a time (synced) and compare every rank's rows with the "
+                         "single context after each: names the first superstep and rank that differ")
+    ap.add_argument("--twice", action="store_true",
+                    help="fit each side twice and report which side (rank ring / single context) repeats itself")
+    ap.add_argument("--sync-each", action="store_true", help="host-sync after every superstep of the rank fits")
+    ap.add_argument("--knobs", default=None, help="MFHIP_TEST for this run (e.g. device_plan=0)")
+    ap.add_argument("--setenv", action="append", default=[], help="K=V set before the communicator exists")
     a = ap.parse_args()
+    if a.knobs:
+        os.environ["MFHIP_TEST"] = a.knobs
+    for kv in a.setenv:
+        os.environ[kv.split("=", 1)[0]] = kv.split("=", 1)[1]
     import torch.distributed as dist
     import mfhip
     from mfhip import _lib as L
@@ -79,16 +142,27 @@ def main():
     if a.mode == "fast" and L.lib().mf_debug_plan_digest(ctx._h, plan.ctypes.data_as(L.C.POINTER(L.C.c_uint64))) != 0:
         plan[:] = 0  # (a rank without ratings, or a host-planned schedule, has no device plan digest)
     mem = np.zeros(2, np.int64)
-    L.lib().mf_debug_device_bytes(mem.ctypes.data_as(L.C.POINTER(L.C.c_int64)))
+    has_mem = hasattr(L.lib(), "mf_debug_device_bytes")  # (an older build, A/B runs)
+    if has_mem:
+        L.lib().mf_debug_device_bytes(mem.ctypes.data_as(L.C.POINTER(L.C.c_int64)))
+    if a.stepwise:
+        stepwise(a, ctx, p, tu, ti, tr, rank, world, dist)
+        return
     t0 = time.time()
-    ctx.run(p.iterations * p.num_blocks)  # asynchronous: rmse / factors right behind it (staged)
+    if a.sync_each:
+        for _ in range(p.iterations * p.num_blocks):
+            ctx.run(1)
+            ctx.sync()
+    else:
+        ctx.run(p.iterations * p.num_blocks)  # asynchronous: rmse / factors right behind it (staged)
     if not a.staged:
         ctx.sync()
     t_run = time.time() - t0
     rm, cnt = ctx.rmse(eu, ei, er)
     st = ctx.stats()
     mem2 = np.zeros(2, np.int64)
-    L.lib().mf_debug_device_bytes(mem2.ctypes.data_as(L.C.POINTER(L.C.c_int64)))
+    if has_mem:
+        L.lib().mf_debug_device_bytes(mem2.ctypes.data_as(L.C.POINTER(L.C.c_int64)))
     import resource
     rss = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20  # KiB -> GiB
     print(f"rank {rank}: updates {st['updates']} groups {st['groups']} pads {st['pads']} plan records {int(plan[1])} "
@@ -97,15 +171,37 @@ def main():
     uids, uf = ctx.factors(L.SIDE_USER)
     iids, itf = ctx.factors(L.SIDE_ITEM)
     ctx.close()
+    if a.twice:  # a second rank-mode fit on a fresh communicator: does the ring repeat itself?
+        obj = [mfhip.Context.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        with mfhip.Context(p, rank=(dev, world, rank, obj[0])) as c2:
+            if a.sync_each:
+                c2.prepare(tu, ti, tr)
+                for _ in range(p.iterations * p.num_blocks):
+                    c2.run(1)
+                    c2.sync()
+            else:
+                c2.fit(tu, ti, tr)
+            plan2 = np.zeros(2, np.uint64)
+            if a.mode == "fast" and L.lib().mf_debug_plan_digest(c2._h, plan2.ctypes.data_as(L.C.POINTER(L.C.c_uint64))):
+                plan2[:] = 0
+            same = (np.array_equal(row_hash(c2.factors(L.SIDE_USER)[1]), row_hash(uf)),
+                    np.array_equal(row_hash(c2.factors(L.SIDE_ITEM)[1]), row_hash(itf)),
+                    f"plan {int(plan[0]):016x}" + ("" if plan2[0] == plan[0] else f" -> {int(plan2[0]):016x}"))
+        flags = [None] * world if rank == 0 else None
+        dist.gather_object(same, flags, dst=0)
+        if rank == 0:
+            print(f"rank-mode fit repeats itself (users, items, plan digest) per rank: {flags}", flush=True)
     parts = [None] * world if rank == 0 else None
     dist.gather_object((uids, uf), parts, dst=0)
     del uf
     if rank == 0:
+        owner = np.concatenate([np.full(len(x[0]), r, np.int32) for r, x in enumerate(parts)])
         uids = np.concatenate([x[0] for x in parts])
         uf = np.concatenate([x[1] for x in parts])
         del parts
         o = np.argsort(uids)
-        uids, uf = uids[o], uf[o]
+        uids, uf, owner = uids[o], uf[o], owner[o]
         ref = mfhip.Context(p, devices=[0] * world) if a.fast_waves < 0 else mfhip.Context(p)
         t0 = time.time()
         ref.fit(tu, ti, tr)
@@ -115,10 +211,22 @@ def main():
         ruids, ruf = ref.factors(L.SIDE_USER)
         riids, ritf = ref.factors(L.SIDE_ITEM)
         ref.close()
+        if a.twice:
+            with (mfhip.Context(p, devices=[0] * world) if a.fast_waves < 0 else mfhip.Context(p)) as r2:
+                r2.fit(tu, ti, tr)
+                print(f"single-context fit repeats itself: users "
+                      f"{np.array_equal(row_hash(r2.factors(L.SIDE_USER)[1]), row_hash(ruf))} items "
+                      f"{np.array_equal(row_hash(r2.factors(L.SIDE_ITEM)[1]), row_hash(ritf))}", flush=True)
         print(f"single context: prepare + {p.iterations} epoch(s) {t_ref:.1f} s", flush=True)
         assert np.array_equal(uids, ruids) and np.array_equal(iids, riids), "id sets differ"
         du = float(np.max(np.abs(uf - ruf)))
         di = float(np.max(np.abs(itf - ritf)))
+        if du != 0.0:  # which ranks' users differ, and how many rows
+            bad = np.any(uf != ruf, axis=1)
+            per = {int(r): int(np.sum(bad & (owner == r))) for r in range(world)}
+            print(f"differing user rows per rank: {per} of {len(uids)}", flush=True)
+        if di != 0.0:
+            print(f"differing item rows: {int(np.sum(np.any(itf != ritf, axis=1)))} of {len(iids)}", flush=True)
         print(f"world={world} mode={a.mode} config={a.config or 'small'}@{a.scale:g} k={k} n={nb} "
               f"rmse rank={rm:.6f} single={rrm:.6f} matched {cnt}/{rcnt} "
               f"max|dU|={du:.3g} max|dI|={di:.3g}", flush=True)
