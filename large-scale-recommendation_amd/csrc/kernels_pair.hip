@@ -37,6 +37,15 @@ namespace {
 
 #include "pair_device.hpp"
 
+// experiment: explicit agent-scope acquire / release around a launch (L2 invalidate / write-back)
+#ifdef MFHIP_EXP_FENCES
+#define MF_LAUNCH_ACQUIRE() __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent")
+#define MF_LAUNCH_RELEASE() __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent")
+#else
+#define MF_LAUNCH_ACQUIRE() ((void)0)
+#define MF_LAUNCH_RELEASE() ((void)0)
+#endif
+
 #ifdef MFHIP_EXP_ITEM_SC1
 constexpr int kItemPolicy = kSC1;
 #else
@@ -249,6 +258,7 @@ template <int KPL, int D>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_sweep_pair(
     const WaveDesc* __restrict__ waves, const u4v* __restrict__ recs, float* __restrict__ U, float* __restrict__ I,
     uint64_t u_bytes, uint64_t i_bytes, float eta, uint64_t* __restrict__ trace) {
+  MF_LAUNCH_ACQUIRE();
   const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
   const WaveDesc d = waves[blockIdx.x];
   const __amdgpu_buffer_rsrc_t rr = cell_records(recs, d.base, d.steps);
@@ -256,6 +266,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   uint64_t wait_clk = 0;
   pair_cell<KPL, D, 0>(d, chunk_load(rr, 0, vlane), chunk_load(rr, 1, vlane), recs, raw_rsrc(U, u_bytes),
                        raw_rsrc(I, i_bytes), eta, threadIdx.x, wait_clk);
+  MF_LAUNCH_RELEASE();
   if (trace && threadIdx.x == 0) {
     trace[2 * blockIdx.x] = t_start;
     trace[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
@@ -286,6 +297,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     float* __restrict__ U, float* __restrict__ I, uint64_t u_bytes, uint64_t i_bytes, float eta,
     int32_t* __restrict__ prog, uint32_t base, int32_t* __restrict__ err, uint64_t* __restrict__ trace,
     const int32_t* __restrict__ place) {
+  MF_LAUNCH_ACQUIRE();
   const int lane = threadIdx.x;
   // blocks b and b+8 share an XCD: give each XCD a contiguous range of waves, so most hand-offs
   // (g+1 -> g) stay inside one L2 (speed only; correctness does not depend on it).  XCD x holds
@@ -359,6 +371,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     }
     d = dn;
   }
+  MF_LAUNCH_RELEASE();
 }
 
 // ev0 / ev1 (may be null): timed by the dispatch packet itself (no extra stream commands).

@@ -108,7 +108,7 @@ for step in "$@"; do
         --nnodes=1 --nproc-per-node "$w" --master-addr 127.0.0.1 --master-port $((29500 + n)) tools/rank_check.py $args \
         > "$O/rank_$n.log" 2>&1
       rc=$?
-      grep -E "world=|RANK_CHECK|rank [0-9]+:|differing|superstep|STEPWISE|repeats" "$O/rank_$n.log" | head -60
+      grep -E "world=|RANK_CHECK|rank [0-9]+:|differing|superstep|STEPWISE|repeats|DIGEST|single context" "$O/rank_$n.log" | head -60
       # a failed bitwise comparison lets the next step run; anything else (a fault, an abort, a
       # time limit) ends the call
       [ $rc -eq 0 ] || { echo "rank check failed ($rc)"; tail -5 "$O/rank_$n.log";

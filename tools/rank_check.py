@@ -27,6 +27,13 @@ def row_hash(f):
         return (b * mult).sum(axis=1, dtype=np.uint64)
 
 
+def digest(ids, hashes):
+    """Order-free 64-bit digest of (id, row) pairs: equal digests <=> (almost surely) equal rows per id."""
+    with np.errstate(over="ignore"):
+        h = hashes ^ (np.asarray(ids).astype(np.uint64) * np.uint64(0xC2B2AE3D27D4EB4F))
+        return int(h.sum(dtype=np.uint64))
+
+
 def stepwise(a, ctx, p, tu, ti, tr, rank, world, dist):
     from mfhip import _lib as L
     import mfhip
@@ -96,6 +103,16 @@ def main():
     ap.add_argument("--twice", action="store_true",
                     help="fit each side twice and report which side (rank ring / single context) repeats itself")
     ap.add_argument("--sync-each", action="store_true", help="host-sync after every superstep of the rank fits")
+    ap.add_argument("--shared-data", default=None,
+                    help="directory: rank 0 writes the split once (unless a previous step did), every rank "
+                         "memory-maps it (large scales); the caller removes it")
+    ap.add_argument("--no-ref", action="store_true",
+                    help="rank fits only: print a DIGEST line (factors and RMSE) to compare with a --ref-only run")
+    ap.add_argument("--ref-only", action="store_true",
+                    help="one process: the single context only, same DIGEST line (full-size runs keep the two "
+                         "sides in separate jobs so their host memory never adds up)")
+    ap.add_argument("--ref-world", type=int, default=8, help="--ref-only with fast-waves < 0: virtual shards")
+    ap.add_argument("--serial-prepare", action="store_true", help="ranks prepare one after another")
     ap.add_argument("--knobs", default=None, help="MFHIP_TEST for this run (e.g. device_plan=0)")
     ap.add_argument("--setenv", action="append", default=[], help="K=V set before the communicator exists")
     a = ap.parse_args()
@@ -118,25 +135,60 @@ def main():
     import time
     k, nb = a.k, a.blocks
     if a.config:
-        data = mfhip.synth.config(a.config, a.scale)
         _, _, _, k, nb = mfhip.synth.CONFIGS[a.config]
         k = a.k if a.k != 32 else k
         nb = a.blocks if a.blocks != 4 else nb
+    names = ("tu", "ti", "tr", "eu", "ei", "er")
+    if a.shared_data:
+        # rank 0 generates and splits once; every rank maps the same files (one copy in the page
+        # cache instead of one per rank: the full-size rehearsal's host memory)
+        if rank == 0 and not os.path.exists(os.path.join(a.shared_data, "er.npy")):  # (another step's split)
+            os.makedirs(a.shared_data, exist_ok=True)
+            data = mfhip.synth.config(a.config, a.scale) if a.config else mfhip.synth.generate(a.users, 800, 60000)
+            for nm, arr in zip(names, [x for part in data.split() for x in part]):
+                np.save(os.path.join(a.shared_data, nm + ".npy"), arr)
+            del data
+        dist.barrier()
+        tu, ti, tr, eu, ei, er = [np.load(os.path.join(a.shared_data, nm + ".npy"), mmap_mode="r") for nm in names]
     else:
-        data = mfhip.synth.generate(a.users, 800, 60000)
-    (tu, ti, tr), (eu, ei, er) = data.split()
-    del data
+        data = mfhip.synth.config(a.config, a.scale) if a.config else mfhip.synth.generate(a.users, 800, 60000)
+        (tu, ti, tr), (eu, ei, er) = data.split()
+        del data
     p = L.default_params()
     p.num_factors, p.num_blocks, p.iterations, p.seed, p.has_seed = k, nb, a.iterations, 5, 1
     p.mode = L.MODE_DETERMINISTIC_F64 if a.mode == "det" else L.MODE_FAST_F32
     p.fast_waves = a.fast_waves
+    if a.ref_only:
+        ref = mfhip.Context(p, devices=[0] * a.ref_world) if a.fast_waves < 0 else mfhip.Context(p)
+        t0 = time.time()
+        ref.fit(tu, ti, tr)
+        ref.sync()
+        t_ref = time.time() - t0
+        rrm, rcnt = ref.rmse(eu, ei, er)
+        ruids, ruf = ref.factors(L.SIDE_USER)
+        riids, ritf = ref.factors(L.SIDE_ITEM)
+        ref.close()
+        print(f"single context ({a.mode}, {a.config}@{a.scale:g}): prepare + {p.iterations} epoch(s) {t_ref:.1f} s",
+              flush=True)
+        print(f"DIGEST users {digest(ruids, row_hash(ruf)):016x} items {digest(riids, row_hash(ritf)):016x} "
+              f"rmse {rrm:.12f} matched {rcnt}", flush=True)
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     obj = [mfhip.Context.unique_id() if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0)
     dev = local % max(1, mfhip.device_count())
     ctx = mfhip.Context(p, rank=(dev, world, rank, obj[0]))
     t0 = time.time()
-    ctx.prepare(tu, ti, tr)
-    ctx.sync()
+    if a.serial_prepare:  # one rank at a time: the transient device blocking of every rank's copy of
+        for r in range(world):  # all ratings does not add up on the one shared card
+            if r == rank:
+                ctx.prepare(tu, ti, tr)
+                ctx.sync()
+            dist.barrier()
+    else:
+        ctx.prepare(tu, ti, tr)
+        ctx.sync()
     t_prep = time.time() - t0
     plan = np.zeros(2, np.uint64)
     if a.mode == "fast" and L.lib().mf_debug_plan_digest(ctx._h, plan.ctypes.data_as(L.C.POINTER(L.C.c_uint64))) != 0:
@@ -192,16 +244,32 @@ def main():
         dist.gather_object(same, flags, dst=0)
         if rank == 0:
             print(f"rank-mode fit repeats itself (users, items, plan digest) per rank: {flags}", flush=True)
+    if a.no_ref:
+        du_ = [None] * world if rank == 0 else None
+        dist.gather_object(digest(uids, row_hash(uf)), du_, dst=0)
+        if rank == 0:
+            tot = 0
+            for x in du_:
+                tot = (tot + x) % (1 << 64)
+            print(f"DIGEST users {tot:016x} items {digest(iids, row_hash(itf)):016x} rmse {rm:.12f} matched {cnt}",
+                  flush=True)
+            print("RANK_CHECK_OK", flush=True)
+        dist.barrier()
+        dist.destroy_process_group()
+        return
+    # users travel to rank 0 as one 64-bit hash per row (bitwise comparison) plus the row's
+    # largest magnitude-free summary: the full slab would be 3.7 GB at YAHOO's full size
     parts = [None] * world if rank == 0 else None
-    dist.gather_object((uids, uf), parts, dst=0)
+    dist.gather_object((uids, row_hash(uf), uf.astype(np.float32)), parts, dst=0)
     del uf
     if rank == 0:
         owner = np.concatenate([np.full(len(x[0]), r, np.int32) for r, x in enumerate(parts)])
         uids = np.concatenate([x[0] for x in parts])
-        uf = np.concatenate([x[1] for x in parts])
+        uh = np.concatenate([x[1] for x in parts])
+        uf32 = np.concatenate([x[2] for x in parts])
         del parts
         o = np.argsort(uids)
-        uids, uf, owner = uids[o], uf[o], owner[o]
+        uids, uh, uf32, owner = uids[o], uh[o], uf32[o], owner[o]
         ref = mfhip.Context(p, devices=[0] * world) if a.fast_waves < 0 else mfhip.Context(p)
         t0 = time.time()
         ref.fit(tu, ti, tr)
@@ -219,10 +287,10 @@ def main():
                       f"{np.array_equal(row_hash(r2.factors(L.SIDE_ITEM)[1]), row_hash(ritf))}", flush=True)
         print(f"single context: prepare + {p.iterations} epoch(s) {t_ref:.1f} s", flush=True)
         assert np.array_equal(uids, ruids) and np.array_equal(iids, riids), "id sets differ"
-        du = float(np.max(np.abs(uf - ruf)))
+        bad = uh != row_hash(ruf)
+        du = float(np.max(np.abs(uf32[bad] - ruf[bad].astype(np.float32)))) if bad.any() else 0.0
         di = float(np.max(np.abs(itf - ritf)))
-        if du != 0.0:  # which ranks' users differ, and how many rows
-            bad = np.any(uf != ruf, axis=1)
+        if bad.any():  # which ranks' users differ, and how many rows
             per = {int(r): int(np.sum(bad & (owner == r))) for r in range(world)}
             print(f"differing user rows per rank: {per} of {len(uids)}", flush=True)
         if di != 0.0:
