@@ -138,6 +138,151 @@ run_done:
   st<KPL, IP>(irs, voff, item_off, q);
 }
 
+// k = 64 (KPL = 1): one float of each row per lane.  Row<1> carries a row as a float pair with
+// a zero high half, so every update of the generic code is a packed op on a half-empty register
+// (and re-zeroing moves).  Here rows are plain floats, and the two updates that share a pattern
+// run as one packed op: {plA, q1} = {ba, aa} * {pa, qa} + wa * {qa, pa} (v_pk_mul_f32, then
+// v_pk_fma_f32 with the halves swapped), likewise {plB, q} from {pb, qb0}.  Same arithmetic per
+// element as the generic step (one product, one fused multiply-add).
+template <int POL = 0>
+__device__ __forceinline__ float ld1(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, voff, off, POL));
+}
+template <int POL = 0>
+__device__ __forceinline__ void st1(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, voff, off, POL);
+}
+// {s0 * x + w * y, s1 * y + w * x}
+__device__ __forceinline__ f2 pair_update(float s0, float s1, float w, float x, float y) {
+  const f2 v = f2{x, y};
+  return __builtin_elementwise_fma(f2{w, w}, v.yx, f2{s0, s1} * v);
+}
+
+template <int UP, bool FWD, int IP = kItemPolicy>
+__device__ __forceinline__ void single_run_cell_k1(Chunk C0, ChunkRaw C1, __amdgpu_buffer_rsrc_t RR,
+                                                   __amdgpu_buffer_rsrc_t urs, __amdgpu_buffer_rsrc_t irs, float eta,
+                                                   uint32_t vlane, uint32_t voff, int npairs) {
+  constexpr int CH = kPairChunk;
+  constexpr int DS = kPairRingSingle;
+  const uint32_t item_off = rl(C0.ia, 0);
+  float q = ld1<IP>(irs, voff, item_off);
+  float RA[DS], RB[DS], plA = 0.f, plB = 0.f;
+  uint32_t oa[DS], ob[DS];
+#pragma unroll
+  for (int s = 0; s < DS; ++s) {
+    oa[s] = rl(C0.ua, s);
+    ob[s] = rl(C0.ub, s);
+    RA[s] = ld1<UP>(urs, voff, oa[s]);
+    RB[s] = ld1<UP>(urs, voff, ob[s]);
+  }
+  drain_vmem();
+  const float neta = vgpr_of(-eta);
+  for (int c = 0;; ++c) {
+#pragma unroll
+    for (int s = 0; s < CH; ++s) {
+      if (c * CH + s >= npairs) goto run_done;
+      const int slot = s % DS;
+      const uint32_t noa = s + DS < CH ? rl(C0.ua, s + DS) : rl(C1.w0[0], s + DS - CH);
+      const uint32_t nob = s + DS < CH ? rl(C0.ub, s + DS) : rl(C1.w0[1], s + DS - CH);
+      float pa;
+      uint32_t osa;
+      if constexpr (FWD) {
+        const uint32_t fl = rl(C0.flags, s);
+        osa = rl(C0.sa, s);
+        const float kfa = static_cast<float>(fl & 0xFFu), kfb = static_cast<float>((fl >> 8) & 0xFFu);
+        pa = kfb * plB + (kfa * plA + RA[slot]);
+      } else {
+        osa = oa[slot];
+        pa = RA[slot];
+      }
+      const float pb = RB[slot];
+      float c1 = pa * q, c2 = pb * q, g = pb * pa;
+      wave_sum3(c1, c2, g);
+      const float wav = fmaf(c1, neta, C0.era);
+      const float wbv = fmaf(fmaf(wav, g, C0.aa * c2), neta, C0.erb);
+      const float wa = rlf(wav, s), wb = rlf(wbv, s);
+      const float aa = rlf(C0.aa, s), ab = rlf(C0.ab, s), ba = rlf(C0.ba, s), bb = rlf(C0.bb, s);
+      const f2 A = pair_update(ba, aa, wa, pa, q);    // {plA, q1}
+      const f2 B = pair_update(bb, ab, wb, pb, A.y);  // {plB, q}
+      plA = A.x;
+      plB = B.x;
+      q = B.y;
+      st1<UP>(urs, voff, osa, plA);
+      st1<UP>(urs, voff, ob[slot], plB);
+      oa[slot] = noa;
+      ob[slot] = nob;
+      RA[slot] = ld1<UP>(urs, voff, noa);
+      RB[slot] = ld1<UP>(urs, voff, nob);
+    }
+    C0 = chunk_convert(C1, eta);
+    C1 = chunk_load(RR, c + 2, vlane);
+  }
+run_done:
+  st1<IP>(irs, voff, item_off, q);
+}
+
+template <int D, int UP, int IP = kItemPolicy>
+__device__ __forceinline__ void generic_cell_k1(Chunk C0, ChunkRaw C1, __amdgpu_buffer_rsrc_t RR,
+                                                __amdgpu_buffer_rsrc_t urs, __amdgpu_buffer_rsrc_t irs, float eta,
+                                                uint32_t vlane, uint32_t voff, int npairs) {
+  constexpr int CH = kPairChunk;
+  float plA = 0.f, plB = 0.f;
+  float PA[D], PB[D], QA[D], QB[D];
+#pragma unroll
+  for (int s = 0; s < D; ++s) {
+    PA[s] = ld1<UP>(urs, voff, rl(C0.ua, s));
+    PB[s] = ld1<UP>(urs, voff, rl(C0.ub, s));
+    QA[s] = ld1<IP>(irs, voff, rl(C0.ia, s));
+    QB[s] = ld1<IP>(irs, voff, rl(C0.ib, s));
+  }
+  drain_vmem();
+  const float neta = vgpr_of(-eta);
+  float q = 0.f;
+  for (int c = 0;; ++c) {
+#pragma unroll
+    for (int s = 0; s < CH; ++s) {
+      if (c * CH + s >= npairs) return;
+      const int slot = s % D;
+      const uint32_t fl = rl(C0.flags, s);
+      const uint32_t osa = rl(C0.sa, s), osb = rl(C0.sb, s), osia = rl(C0.sia, s), osi = rl(C0.si, s);
+      const bool nin = s + D < CH;
+      const uint32_t nua = nin ? rl(C0.ua, s + D) : rl(C1.w0[0], s + D - CH);
+      const uint32_t nub = nin ? rl(C0.ub, s + D) : rl(C1.w0[1], s + D - CH);
+      const uint32_t nia = nin ? rl(C0.ia, s + D) : rl(C1.w0[2], s + D - CH);
+      const uint32_t nib = nin ? rl(C0.ib, s + D) : rl(C1.w0[3], s + D - CH);
+      const float kfa = static_cast<float>(fl & 0xFFu), kfb = static_cast<float>((fl >> 8) & 0xFFu);
+      const float kq = static_cast<float>((fl >> 16) & 0xFFu);
+      const float sr = rlf(C0.sr, s);
+      const float pa = kfb * plB + (kfa * plA + PA[slot]);  // loads of forwarded rows return 0
+      const float pb = PB[slot];
+      const float qa = kq * q + QA[slot];
+      const float qbd = sr * qa + QB[slot];  // B's item before A's update: q (run) or qB (split)
+      float c1 = pa * qa, c2 = pb * qbd, g = pb * pa;
+      wave_sum3(c1, c2, g);
+      const float wav = fmaf(c1, neta, C0.era);
+      const float wbv = fmaf(fmaf(C0.sr * wav, g, C0.m * c2), neta, C0.erb);
+      const float wa = rlf(wav, s), wb = rlf(wbv, s);
+      const float aa = rlf(C0.aa, s), ab = rlf(C0.ab, s), ba = rlf(C0.ba, s), bb = rlf(C0.bb, s);
+      const f2 A = pair_update(ba, aa, wa, pa, qa);  // {plA, q1}
+      const float qb0 = sr * A.y + QB[slot];
+      const f2 B = pair_update(bb, ab, wb, pb, qb0);  // {plB, q}
+      plA = A.x;
+      plB = B.x;
+      q = B.y;
+      st1<UP>(urs, voff, osa, plA);
+      st1<UP>(urs, voff, osb, plB);
+      st1<IP>(irs, voff, osia, A.y);
+      st1<IP>(irs, voff, osi, q);
+      PA[slot] = ld1<UP>(urs, voff, nua);
+      PB[slot] = ld1<UP>(urs, voff, nub);
+      QA[slot] = ld1<IP>(irs, voff, nia);
+      QB[slot] = ld1<IP>(irs, voff, nib);
+    }
+    C0 = chunk_convert(C1, eta);
+    C1 = chunk_load(RR, c + 2, vlane);
+  }
+}
+
 // One cell (WaveDesc d) of the pair schedule, swept by the calling wave.  UP = cache policy of
 // the user-row loads and stores.  L0 / L1: the cell's first two record chunks, loaded by the
 // caller (the systolic sweep loads them while the previous cell's stores drain).
@@ -156,6 +301,15 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const ChunkRaw& L0, 
 
   Chunk C0 = chunk_convert(L0, eta);  // current chunk
   ChunkRaw C1 = L1;                   // next chunk, as loaded
+  if constexpr (KPL == 1) {
+    if (d.cells == kWaveSingleRun)
+      single_run_cell_k1<UP, false>(C0, C1, RR, urs, irs, eta, vlane, voff, npairs);
+    else if (d.cells == kWaveSingleRunFwd)
+      single_run_cell_k1<UP, true>(C0, C1, RR, urs, irs, eta, vlane, voff, npairs);
+    else
+      generic_cell_k1<D, UP>(C0, C1, RR, urs, irs, eta, vlane, voff, npairs);
+    return;
+  }
   if (d.cells == kWaveSingleRun) {
     single_run_cell<KPL, UP, false>(C0, C1, RR, urs, irs, eta, vlane, voff, npairs, wait_clk);
     return;
