@@ -310,11 +310,18 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const ChunkRaw& L0, 
       generic_cell_k1<D, UP>(C0, C1, RR, urs, irs, eta, vlane, voff, npairs);
     return;
   }
-  if (d.cells == kWaveSingleRun) {
+  // k = 256 sweeps single-run cells with the generic step: with its 16-B rows the lean path did
+  // not repeat itself (a restart of the same fit gave other factors, every run, both kernels)
+  // and its RMSE sat 0.27% off the repeatable runs', which the generic step and the lean path
+  // with 8-B row halves agree on; the halves cost 30% at YAHOO, the generic step 3%
+  // (profiles/r04_k256_repeatability.txt)
+  if constexpr (KPL >= 4) {
+  } else if (d.cells == kWaveSingleRun) {
     single_run_cell<KPL, UP, false>(C0, C1, RR, urs, irs, eta, vlane, voff, npairs, wait_clk);
     return;
   }
-  if (d.cells == kWaveSingleRunFwd) {
+  if constexpr (KPL >= 4) {
+  } else if (d.cells == kWaveSingleRunFwd) {
     single_run_cell<KPL, UP, true>(C0, C1, RR, urs, irs, eta, vlane, voff, npairs, wait_clk);
     return;
   }

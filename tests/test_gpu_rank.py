@@ -56,12 +56,9 @@ def test_rank_mode_yahoo_shaped_world8(mode, extra):
     """BASELINE config 4 (Yahoo-Music-shaped, k = 256, numBlocks = 8, "on 8 x MI355X") through the
     rank path at 0.05 scale (91k users x 6.8k items x 36M ratings): 8 ranks share device 0, each
     owning one user block, the item blocks rotating over the RCCL ring (DSGDforMF.scala:262-357,
-    611-619).  One epoch; factors compared bit for bit (tools/rank_check.py).
-
-    One hardware queue per rank process: eight processes with HIP's default four queues each
-    oversubscribe the one card, and fast-mode fits then differed from run to run on some boxes
-    (det never did; DESIGN.md §5 has the evidence).  The driver's 8-GPU node has a card per rank."""
-    env = dict(os.environ, MFHIP_FAKE_HOSTS="1", MFHIP_DEVICE_SHARERS="8", NCCL_DEBUG="WARN", GPU_MAX_HW_QUEUES="1")
+    611-619).  One epoch; factors compared bit for bit (tools/rank_check.py).  The fast case is
+    the one that caught the k = 256 lean-path defect (profiles/r04_k256_repeatability.txt)."""
+    env = dict(os.environ, MFHIP_FAKE_HOSTS="1", MFHIP_DEVICE_SHARERS="8", NCCL_DEBUG="WARN")
     port = 29661 + (10 if mode == "det" else 0)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "tools", "rank_check.py"),
