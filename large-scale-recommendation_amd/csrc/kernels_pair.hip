@@ -369,8 +369,8 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const ChunkRaw& L0, 
         const uint32_t nib = nin ? rl(C0.ib, s + D) : rl(C1.w0[3], s + D - CH);
         // byte flags -> float coefficients (v_cvt_f32_ubyteN): forwarding, keep q, split
         const float kfa = static_cast<float>(fl & 0xFFu), kfb = static_cast<float>((fl >> 8) & 0xFFu);
-        const float kq = static_cast<float>((fl >> 16) & 0xFFu), sp = static_cast<float>(fl >> 24);
-        const float sr = 1.f - sp;
+        const float kq = static_cast<float>((fl >> 16) & 0xFFu);
+        const float sr = rlf(C0.sr, s);  // 1 - split, from the chunk (one readlane, no convert + subtract)
         Row<KPL> pa, pb, qa, qbd;
 #pragma unroll
         for (int e = 0; e < NV; ++e) {
