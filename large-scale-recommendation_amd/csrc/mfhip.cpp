@@ -940,9 +940,27 @@ void det_blocks(const mf_ctx* ctx, const Shard& s, int64_t superstep, std::vecto
   }
 }
 
+// MFHIP_TIMING=1: where a det_run call's host time goes (build time, waits for builds and for
+// staging copies), on stderr at the end of the call
+struct DetRunClock {
+  std::atomic<int64_t> build_ns{0}, builds{0};
+};
+DetRunClock g_det_clock;
+const bool g_det_timing = std::getenv("MFHIP_TIMING") != nullptr;
+
 // Host side of one superstep for every local shard, into det_buf[slot] (runs on a worker thread
 // while the device runs the previous superstep).
 void det_build(mf_ctx* ctx, int64_t superstep, int slot) {
+  const auto t_build = std::chrono::steady_clock::now();
+  struct Done {
+    std::chrono::steady_clock::time_point t;
+    ~Done() {
+      if (g_det_timing) {
+        g_det_clock.build_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t).count();
+        g_det_clock.builds += 1;
+      }
+    }
+  } done{t_build};
   std::vector<int64_t> blocks, seeds;
   for (auto& s : ctx->shards) {
     DetBuf& db = s.det_buf[slot];
@@ -971,7 +989,13 @@ void det_build(mf_ctx* ctx, int64_t superstep, int slot) {
 void det_run(mf_ctx* ctx, int64_t count) {
   const int k = ctx->P.num_factors;
   const int64_t s0 = ctx->superstep_done + 1;
+  using clk = std::chrono::steady_clock;
+  const auto t_run = clk::now();
+  const int64_t b_ns0 = g_det_clock.build_ns, b_n0 = g_det_clock.builds;
+  int64_t wait_build_ns = 0, wait_copy_ns = 0;
+  auto since = [](clk::time_point t) { return std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now() - t).count(); };
   auto reclaim = [&](int slot) {  // the staging copy out of this slot's pinned buffer has finished
+    const auto t = clk::now();
     for (auto& sh : ctx->shards) {
       DetBuf& db = sh.det_buf[slot];
       if (!db.pending) continue;
@@ -979,6 +1003,7 @@ void det_run(mf_ctx* ctx, int64_t count) {
       MF_HIP(hipEventSynchronize(db.copied));
       db.pending = false;
     }
+    wait_copy_ns += since(t);
   };
   std::future<void> builds[kDetSlots];
   constexpr int kAhead = kDetSlots - 1;  // supersteps built ahead of the one launched
@@ -1005,7 +1030,11 @@ void det_run(mf_ctx* ctx, int64_t count) {
   for (int64_t x = 0; x < count; ++x) {
     const int64_t s = s0 + x;
     const int slot = static_cast<int>(x % kDetSlots);
-    builds[slot].get();  // every superstep of the run has a build (taken over or started here)
+    {
+      const auto t = clk::now();
+      builds[slot].get();  // every superstep of the run has a build (taken over or started here)
+      wait_build_ns += since(t);
+    }
     const int32_t iteration = static_cast<int32_t>(s / ctx->nb);  // :476
     const double eta = learning_rate(ctx->P.lr_method, ctx->P.learning_rate, iteration + 1, ctx->P.lambda,
                                      ctx->P.lr_arg);  // :383-386
@@ -1055,6 +1084,18 @@ void det_run(mf_ctx* ctx, int64_t count) {
     }
   }
   ctx->stats.algorithmic_bytes = static_cast<double>(ctx->stats.updates) * bytes_per_update(ctx);
+  if (g_det_timing)
+    std::fprintf(stderr,
+                 "[mfhip] det_run: %lld supersteps enqueued in %.1f ms; waited %.1f ms for host builds, %.1f ms for "
+                 "staging copies; %lld builds finished meanwhile, %.2f ms each\n",
+                 static_cast<long long>(count), since(t_run) / 1e6, wait_build_ns / 1e6, wait_copy_ns / 1e6,
+                 static_cast<long long>(g_det_clock.builds - b_n0),
+                 g_det_clock.builds > b_n0 ? (g_det_clock.build_ns - b_ns0) / 1e6 / (g_det_clock.builds - b_n0) : 0.0);
+  if (g_det_timing && g_det_clock.builds > 0)
+    std::fprintf(stderr, "[mfhip] det builds so far, ms each: shuffle %.2f gather %.2f prefix %.2f scatter %.2f flags %.2f\n",
+                 det_build_phase_ns(0) / 1e6 / g_det_clock.builds, det_build_phase_ns(1) / 1e6 / g_det_clock.builds,
+                 det_build_phase_ns(2) / 1e6 / g_det_clock.builds, det_build_phase_ns(3) / 1e6 / g_det_clock.builds,
+                 det_build_phase_ns(4) / 1e6 / g_det_clock.builds);
   // the next run's first supersteps, built in the background while the caller syncs, evaluates or
   // returns: a run's start no longer waits for its first host build (~36 ms of an NFLX call).  A builder
   // first waits for the staging copy that last read its slot's pinned buffer.
@@ -1141,6 +1182,14 @@ void prepare_det_sweep(mf_ctx* ctx) {
   int32_t waves = std::max(1, cap / 2);
   if (const std::string v = test_knob("det_waves"); !v.empty()) waves = std::clamp(std::atoi(v.c_str()), 1, cap);
   const int32_t n = ctx->nb;
+  {  // the build's shuffle-order gather reads one 16-B record per rating
+    const int64_t total = ctx->rb.start.empty() ? 0 : ctx->rb.start.back();
+    ctx->rb.det_aos.resize(static_cast<size_t>(total));
+    DetEntry* a = ctx->rb.det_aos.data();
+    parallel_for(total, [&](int64_t b, int64_t e, int) {
+      for (int64_t x = b; x < e; ++x) a[x] = DetEntry{ctx->rb.urow[x], ctx->rb.irow[x], ctx->rb.r[x]};
+    });
+  }
   for (auto& s : ctx->shards) {
     build_det_layout(s.det_layout, ctx->rb, ctx->U, ctx->I, ctx->c, s.index, waves);
     s.det_n_max = s.det_nw_max = 0;

@@ -332,9 +332,19 @@ void build_det_layout(DetSweepLayout& L, const RatingBlocks& rb, const SideLayou
   });
 }
 
+// MFHIP_TIMING: wall time of build_det_step's phases, summed over calls (det_build_phase_ns)
+std::atomic<int64_t> g_det_phase_ns[5];
+int64_t det_build_phase_ns(int ph) { return g_det_phase_ns[ph]; }
+
 void build_det_step(const RatingBlocks& rb, const SideLayout& U, const SideLayout& I, const DetSweepLayout& L,
                     const std::vector<int64_t>& blocks, const std::vector<int64_t>& seeds, bool seeded,
                     const DetStepOut& out, DetStepScratch* scratch) {
+  auto ph_t = std::chrono::steady_clock::now();
+  auto lap = [&](int ph) {
+    const auto now = std::chrono::steady_clock::now();
+    g_det_phase_ns[ph] += std::chrono::duration_cast<std::chrono::nanoseconds>(now - ph_t).count();
+    ph_t = now;
+  };
   const int32_t nb = rb.n_blocks;
   const int64_t nbk = static_cast<int64_t>(blocks.size());
   DetStepScratch local;
@@ -361,6 +371,7 @@ void build_det_step(const RatingBlocks& rb, const SideLayout& U, const SideLayou
     JavaRandom rng(seeded ? seeds[x] : static_cast<int64_t>(rseeds[x]));
     scala_shuffle(rng, order[x].data(), len);  // DSGDforMF.scala:392-393
   });
+  lap(0);
   // the rest runs over chunks of shuffle positions, so a large block does not hold up the step
   constexpr int64_t kChunk = int64_t{1} << 18;
   struct Chunk {
@@ -397,6 +408,7 @@ void build_det_step(const RatingBlocks& rb, const SideLayout& U, const SideLayou
   // waves, and per-chunk counts of waves and users
   std::vector<std::vector<int64_t>> wcur(ch.size());
   std::vector<std::vector<int32_t>> ucur(ch.size());
+  const DetEntry* const aos = rb.det_aos.empty() ? nullptr : rb.det_aos.data();
   parallel_tasks(static_cast<int64_t>(ch.size()), [&](int64_t t) {
     const Chunk c = ch[t];
     int64_t st, u0, nu, i0;
@@ -405,25 +417,39 @@ void build_det_step(const RatingBlocks& rb, const SideLayout& U, const SideLayou
     const int32_t* ord = order[c.x].data();
     wcur[t].assign(L.block_waves[blocks[c.x]], 0);
     ucur[t].assign(nu, 0);
-    constexpr int64_t kAhead = 16;  // the rating arrays are far larger than the caches
+    constexpr int64_t kAhead = 64;  // the rating arrays are far larger than the caches
     for (int64_t j = c.j0; j < c.j1; ++j) {
       if (j + kAhead < c.j1) {
         const int64_t ea = st + ord[j + kAhead];
-        __builtin_prefetch(&rb.urow[ea]);
-        __builtin_prefetch(&rb.irow[ea]);
-        __builtin_prefetch(&rb.r[ea]);
+        if (aos) {
+          __builtin_prefetch(aos + ea);
+        } else {
+          __builtin_prefetch(&rb.urow[ea]);
+          __builtin_prefetch(&rb.irow[ea]);
+          __builtin_prefetch(&rb.r[ea]);
+        }
       }
       const int64_t e = st + ord[j];
-      const uint32_t ur = rb.urow[e], ir = rb.irow[e];
+      uint32_t ur, ir;
+      if (aos) {
+        const DetEntry& de = aos[e];
+        ur = de.u;
+        ir = de.i;
+        gr[c.x][j] = de.r;
+      } else {
+        ur = rb.urow[e];
+        ir = rb.irow[e];
+        gr[c.x][j] = rb.r[e];
+      }
       gu[c.x][j] = ur;
       gi[c.x][j] = ir;
-      gr[c.x][j] = rb.r[e];
       const int32_t w = iw[ir - i0];
       wv[c.x][j] = w;
       wcur[t][w]++;
       ucur[t][ur - u0]++;
     }
   });
+  lap(1);
   // 3. per block: wave offsets, and each chunk's start per wave and per user (its counts turned
   // into exclusive prefixes over the block's chunks)
   parallel_tasks(nbk, [&](int64_t x) {
@@ -450,6 +476,7 @@ void build_det_step(const RatingBlocks& rb, const SideLayout& U, const SideLayou
       }
     }
   });
+  lap(2);
   // 4. per chunk: the scatter into wave-major order; useq = the user's count of earlier ratings
   // in shuffle order
   parallel_tasks(static_cast<int64_t>(ch.size()), [&](int64_t t) {
@@ -467,11 +494,13 @@ void build_det_step(const RatingBlocks& rb, const SideLayout& U, const SideLayou
       out.r[at] = gr[c.x][j];
     }
   });
-  // 5. items repeated back to back stay in registers
-  parallel_tasks(nbk, [&](int64_t x) {
-    const int32_t W = L.block_waves[blocks[x]];
-    for (int32_t w = 0; w < W; ++w) {
-      DetWave& dw = out.waves[w0[x] + w];
+  lap(3);
+  // 5. items repeated back to back stay in registers (over all waves of the step, 64 at a time:
+  // eight blocks alone left half of the host threads idle)
+  constexpr int64_t kWaveTask = 64;
+  parallel_tasks((w0[nbk] + kWaveTask - 1) / kWaveTask, [&](int64_t task) {
+    for (int64_t wg = task * kWaveTask; wg < std::min(w0[nbk], (task + 1) * kWaveTask); ++wg) {
+      DetWave& dw = out.waves[wg];
       const int64_t a = dw.begin, z = dw.begin + dw.count;
       bool single = z > a;
       for (int64_t y = a; y < z; ++y) {
@@ -482,6 +511,7 @@ void build_det_step(const RatingBlocks& rb, const SideLayout& U, const SideLayou
       dw.flags = single ? kDetWaveSingleItem : 0;  // the sweep's lean path (one item row, loaded and stored once)
     }
   });
+  lap(4);
 }
 
 // G trades launch/cell overhead and the record padding forced by heavy users (large G) against

@@ -79,6 +79,9 @@ struct RatingBlocks {
   RecVec<uint32_t> irow;        // global item row
   RecVec<double> r;
   std::vector<int64_t> src;     // input index per position (only when requested)
+  // deterministic sweep only: (urow, irow, r) interleaved, 16 B per rating, so the host build's
+  // shuffle-order gather reads one cache line per rating instead of three (prepare_det_sweep)
+  std::vector<struct DetEntry> det_aos;
   int64_t size(int64_t b) const { return start[b + 1] - start[b]; }
 };
 
@@ -161,6 +164,7 @@ struct DetStepOut {
   uint32_t* qf;  // useq | kDetKeepQ | kDetDeferQ
   double* r;
 };
+int64_t det_build_phase_ns(int phase);  // MFHIP_TIMING diagnostics of build_det_step (0..4)
 void build_det_step(const RatingBlocks& rb, const SideLayout& U, const SideLayout& I, const DetSweepLayout& L,
                     const std::vector<int64_t>& blocks, const std::vector<int64_t>& seeds, bool seeded,
                     const DetStepOut& out,
