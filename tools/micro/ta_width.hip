@@ -2,7 +2,7 @@
 // per SIMD, as in the systolic sweep) each stream 512-B row reads from L2-resident rows in three
 // shapes of the same bytes: 64 lanes x 8 B (dwordx2, the k = 128 sweep's rows), 32 lanes x 16 B
 // (dwordx4, half the lanes masked off) and 64 lanes x 16 B (two rows per instruction, 1 KB).
-// Reports ns per 512 B per wave.  Rows are random within a 16-MB table (L2 / MALL resident).
+// Reports ns per 512 B per wave and the CU's rate (24 loads in flight per wave, 8 waves per CU).  Rows are random within a 16-MB table (L2 / MALL resident).
 //
 //   hipcc -O3 --offload-arch=gfx950 -o ta_width ta_width.hip && ./ta_width
 #include <hip/hip_runtime.h>
@@ -21,7 +21,7 @@
   } while (0)
 
 constexpr int kIters = 4096;
-constexpr int kDepth = 8;  // loads in flight per wave
+constexpr int kDepth = 24;  // loads in flight per wave (enough to cover the latency: a throughput test)
 
 // MODE 0: 64 lanes x 8 B; MODE 1: 32 lanes x 16 B (lanes 32-63 idle); MODE 2: 64 lanes x 16 B (two rows)
 template <int MODE>
@@ -72,7 +72,7 @@ int main() {
   CK(hipMemcpy(rows, h.data(), nrows * 4, hipMemcpyHostToDevice));
   int cus = 0;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
-  const int blocks = cus;  // one 256-thread block (4 waves) per CU
+  const int blocks = 2 * cus;  // two 256-thread blocks (8 waves) per CU
   CK(hipMalloc(&out, (size_t)blocks * 256 * 4));
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
@@ -90,8 +90,10 @@ int main() {
       float ms = 0;
       CK(hipEventElapsedTime(&ms, a, b));
       const double rows_per_wave = (m == 2 ? 2.0 : 1.0) * kIters;
-      std::printf("%-44s %8.3f ms  %6.2f ns per 512-B row per wave (4 waves per CU, %d CUs)\n", names[m], ms,
-                  ms * 1e6 / rows_per_wave, cus);
+      const double rows_total = rows_per_wave * blocks * 4;
+      std::printf("%-44s %8.3f ms  %6.2f ns per 512-B row per wave (8 waves per CU, %d CUs); %.2f TB/s of rows, "
+                  "%.2f ns per instruction per CU\n", names[m], ms, ms * 1e6 / rows_per_wave, cus,
+                  rows_total * 512.0 / (ms * 1e-3) / 1e12, ms * 1e6 / (kIters * 8.0));
     }
   return 0;
 }
