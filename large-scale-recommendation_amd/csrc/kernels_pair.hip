@@ -46,6 +46,14 @@ namespace {
 #define MF_LAUNCH_RELEASE() ((void)0)
 #endif
 
+// experiment: the k = 256 lean single-run path back on (it does not repeat itself; kept to
+// reproduce profiles/r04_k256_repeatability.txt)
+#ifdef MFHIP_EXP_K256_LEAN
+constexpr bool kLeanK256 = true;
+#else
+constexpr bool kLeanK256 = false;
+#endif
+
 #ifdef MFHIP_EXP_ITEM_SC1
 constexpr int kItemPolicy = kSC1;
 #else
@@ -315,12 +323,12 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const ChunkRaw& L0, 
   // and its RMSE sat 0.27% off the repeatable runs', which the generic step and the lean path
   // with 8-B row halves agree on; the halves cost 30% at YAHOO, the generic step 3%
   // (profiles/r04_k256_repeatability.txt)
-  if constexpr (KPL >= 4) {
+  if constexpr (KPL >= 4 && !kLeanK256) {
   } else if (d.cells == kWaveSingleRun) {
     single_run_cell<KPL, UP, false>(C0, C1, RR, urs, irs, eta, vlane, voff, npairs, wait_clk);
     return;
   }
-  if constexpr (KPL >= 4) {
+  if constexpr (KPL >= 4 && !kLeanK256) {
   } else if (d.cells == kWaveSingleRunFwd) {
     single_run_cell<KPL, UP, true>(C0, C1, RR, urs, irs, eta, vlane, voff, npairs, wait_clk);
     return;

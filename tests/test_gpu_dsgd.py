@@ -444,6 +444,27 @@ def test_systolic_sweep_equals_substep_launches(monkeypatch, k, nb, G, hot, n):
     assert outs[1][2] < outs[0][2]  # the systolic path really ran (one launch per superstep)
 
 
+@pytest.mark.parametrize("config,scale", [("ML20M", 0.1), ("NFLX", 0.05), ("YAHOO", 0.05)])
+def test_fast_fit_repeats_itself_after_restart(config, scale):
+    """A fast fit has no atomics and a fixed plan, so mf_dsgd_restart + the same epochs must give
+    the same factors bit for bit (k = 64 / 128 / 256 through the BASELINE-shaped synthetics, whose
+    Zipf heads make single-run cells).  At k = 256 the round-4 lean single-run path with 16-B rows
+    did not (profiles/r04_k256_repeatability.txt)."""
+    d = synth.config(config, scale)
+    (u, i, r), _ = d.split()
+    _, _, _, k, nb = synth.CONFIGS[config]
+    p = L.default_params()
+    p.num_factors, p.num_blocks, p.iterations, p.seed, p.mode = k, nb, 2, 0, L.MODE_FAST_F32
+    with mfhip.Context(p) as ctx:
+        ctx.fit(u, i, r)
+        first = (ctx.factors(0)[1], ctx.factors(1)[1])
+        for _ in range(2):
+            ctx.restart()
+            ctx.run(2 * nb)
+            again = (ctx.factors(0)[1], ctx.factors(1)[1])
+            assert np.array_equal(first[0], again[0]) and np.array_equal(first[1], again[1])
+
+
 def test_systolic_multi_shard_matches_single(monkeypatch):
     set_knob(monkeypatch, "pair_sys", "1")
     d = synth.generate(2000, 500, 60000, seed=9)
