@@ -157,7 +157,7 @@ __device__ __forceinline__ void det_wave(const DetWave d, const uint32_t* __rest
   constexpr int NW = SINGLE ? 3 * KPL + 5 : 6 * KPL + 7;
   static_assert(NW < 64, "vmcnt range");
   const int lane = threadIdx.x;
-  const int64_t cnt = d.count;
+  const int32_t cnt = d.count;  // 32-bit: the entry tests are scalar compares, not 64-bit VALU ones
   const __amdgpu_buffer_rsrc_t urs = raw_rsrc(U, u_bytes), irs = raw_rsrc(I, i_bytes);
   uint32_t voff[KPL];
 #pragma unroll
@@ -209,7 +209,7 @@ __device__ __forceinline__ void det_wave(const DetWave d, const uint32_t* __rest
 #else
   auto stamp = [](int) {};
 #endif
-  auto entry = [&](const int s, const int64_t j) {
+  auto entry = [&](const int s, const int32_t j) {
     const int slot = s & 1;
     const uint32_t u = fu(s), qf = fq(s);
     const uint32_t i = SINGLE ? item0 : fi(s);
@@ -279,7 +279,7 @@ __device__ __forceinline__ void det_wave(const DetWave d, const uint32_t* __rest
   // compiler's wait counts then treat the rows loaded two entries back as just issued (vmcnt(3):
   // every entry waited for the previous entry's loads, a full memory round trip per update).
   // Only the last, partial chunk tests every entry.
-  for (int64_t c0 = 0;; c0 += CH) {
+  for (int32_t c0 = 0;; c0 += CH) {
     if (c0 + CH <= cnt) {
 #pragma unroll
       for (int s = 0; s < CH; ++s) entry(s, c0 + s);
