@@ -267,8 +267,9 @@ def online_leg(ctx, stream, a, batch=ONLINE_BATCH):
     buffer once): reported as first_batch_s, not in the median."""
     import numpy as np
     from mfhip import _lib as L
-    rates, launches = [], []
+    rates, launches, kms = [], [], []
     first = None
+    ctx.set_profiling(True)  # a few launches per batch: one event pair each, noise against ~6 ms
     for b in range(a.online_batches + 1):
         s = slice(b * batch, (b + 1) * batch)
         ctx.reset_stats()
@@ -280,12 +281,16 @@ def online_leg(ctx, stream, a, batch=ONLINE_BATCH):
             first = dt
             continue
         rates.append(batch / dt)
-        launches.append(ctx.stats()["kernel_launches"])
+        st = ctx.stats()
+        launches.append(st["kernel_launches"])
+        kms.append(st["kernel_ms"])
+    ctx.set_profiling(False)
     dtype = "f64" if ctx.params.mode == L.MODE_DETERMINISTIC_F64 else "f32"
     return {"metric": "online ratings/s (1M-rating micro-batches on the fitted model)",
             "value": round(float(np.median(rates)), 1), "unit": "ratings/s", "min": round(float(min(rates)), 1),
             "max": round(float(max(rates)), 1), "first_batch_s": round(first, 4),
             "batch": batch, "batches": a.online_batches, "launches_median": float(np.median(launches)),
+            "kernel_ms_median": round(float(np.median(kms)), 3),
             "flavour": "FlinkOnlineMF / SGDUpdater.nextFactors (lr 0.01)", "target": 10e6, "dtype": dtype,
             "kernel": "k_online_sweep (one persistent launch per batch: per-item waves, per-user tickets)",
             "timing": "end to end per micro-batch: host id lookup, H2D, device plan (kernels_online.hip), "

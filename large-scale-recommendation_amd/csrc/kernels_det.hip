@@ -112,8 +112,13 @@ __global__ __launch_bounds__(64) void k_online_sweep(const int64_t* __restrict__
                                                      const uint32_t* __restrict__ useq, T* U, T* I, int k, T eta,
                                                      int32_t* ticket, int32_t* err) {
   const int lane = threadIdx.x;
-  const int64_t j0 = wbeg[blockIdx.x], j1 = wbeg[blockIdx.x + 1];
-  if (j0 >= j1) return;
+  // this wave's updates as 32-bit offsets from its first one (uniform, so the loop's tests are
+  // scalar 32-bit compares; gfx9 has no scalar 64-bit less-than)
+  const int64_t jb = wbeg[blockIdx.x];
+  const int32_t j1 = static_cast<int32_t>(wbeg[blockIdx.x + 1] - jb);
+  if (j1 <= 0) return;
+  ent += jb;
+  useq += jb;
   __shared__ __attribute__((aligned(16))) T lds[64 * KPL];
   auto ld = [&](const T* row, int c) {
     const int f = lane + 64 * c;
@@ -129,7 +134,7 @@ __global__ __launch_bounds__(64) void k_online_sweep(const int64_t* __restrict__
   };
   // The item row stays in registers while consecutive updates of this wave share the item (a hot
   // item's chain).  User rows are loaded ahead into two slots: update j's row sits in slot
-  // (j - j0) & 1, loaded during update j - 2 when its ticket was already due (or during j - 1, or
+  // j & 1, loaded during update j - 2 when its ticket was already due (or during j - 1, or
   // else by j itself after waiting).  The loads ahead are issued after the update's stores, so the
   // drain before the ticket store waits for the stores only (vmcnt = the loads issued after them).
   // With every lane in use (k == 64 * KPL, so every store instruction really issues) the ticket
@@ -145,7 +150,7 @@ __global__ __launch_bounds__(64) void k_online_sweep(const int64_t* __restrict__
   bool ha = false, hb = false;
   bool have_q = false;
   uint32_t cur_i = 0;
-  auto step = [&](int64_t j, T (&slot)[KPL], bool& have, T (&oslot)[KPL], bool& ohave) {
+  auto step = [&](int32_t j, T (&slot)[KPL], bool& have, T (&oslot)[KPL], bool& ohave) {
     const uint32_t ur = ent[j].u, ir = ent[j].i;
     const int32_t q = static_cast<int32_t>(useq[j]);
     const T r = static_cast<T>(ent[j].r);
@@ -249,8 +254,8 @@ __global__ __launch_bounds__(64) void k_online_sweep(const int64_t* __restrict__
   };
   // whole pairs of steps, then an odd last one: no exit test between the steps of the loop body
   // (a join there makes the compiler's wait counts conservative, ticket_wait.hpp)
-  const int64_t jp = j0 + ((j1 - j0) & ~int64_t(1));
-  for (int64_t j = j0; j < jp; j += 2) {
+  const int32_t jp = j1 & ~1;
+  for (int32_t j = 0; j < jp; j += 2) {
     step(j, sa, ha, sb, hb);
     step(j + 1, sb, hb, sa, ha);
   }

@@ -41,7 +41,7 @@ s = f"{d['config']['workload']}: {d['value']/1e9:.3f} Gups {d['ms_per_step']} ms
 if r: s += f" | launch {r.get('avg_launch_us')} us frac {r.get('frac')} traffic_frac {r.get('traffic_frac')}"
 if det: s += f" | det {det['value']/1e6:.1f} Mups {det['ms_per_step']} ms eq {det.get('rmse_equal_to_ref')} launch {det.get('avg_launch_us')} us cold {det.get('cold_fit_s')}"
 for key, v in on.items():
-    s += f" | online {key} {v['value']/1e6:.1f} M/s"
+    s += f" | online {key} {v['value']/1e6:.1f} M/s kernel {v.get('kernel_ms_median')} ms"
 print(s)
 EOF
 }
