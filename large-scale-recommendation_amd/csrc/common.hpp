@@ -113,6 +113,7 @@ struct DevRatingBlocks {
 struct OnlineSweepScratch {
   DevBuf ukey, wkey, wkey2, iota, ux, wx, head, start, ticket, tmp;
   DevBuf in, wbeg, uticket, err, touched;  // the batch as uploaded; wave starts, tickets, error flag, counts
+  DevBuf dummy;                            // k_online_f32: a scratch ticket line per wave
 };
 
 // Pinned host staging buffer.
@@ -145,7 +146,10 @@ class PinnedBuf {
 //   MFHIP_DEBUG_PLAN                 planner diagnostics and the sweeps' error words on stderr;
 //   MFHIP_DEVICE_SHARERS             rank mode: ranks sharing one device (the one-GPU ring rehearsal);
 //   MFHIP_TEST                       "key=value,..." overrides the test suite uses to force the
-//                                    alternative paths it compares bit for bit (test_knob).
+//                                    alternative paths it compares bit for bit (test_knob); four of
+//                                    them (pair_sys=0, fast_kernel=cell, det_kernel=level,
+//                                    online_kernel=level) are also the supported production fallback
+//                                    from the persistent sweeps.
 // Experiment switches (hot-item replicas, group-model constants, wave traces, ...) exist only in a
 // build with -DMFHIP_EXPERIMENTS (make EXPERIMENTS=1); the default build never reads them.
 inline std::string test_knob(const char* key) {

@@ -50,8 +50,32 @@ __device__ __forceinline__ T seq_dot(const T (&prod)[KPL], int k) {
   return acc;
 }
 
+#include "online_f32.hpp"
 #include "seq_fold.hpp"
 #include "ticket_wait.hpp"
+
+// SGDUpdater.nextFactors of one rating in f32 with online_f32.hpp's arithmetic and k_online_f32's
+// row layout (kernels_online_sweep.hip), so the level replay equals the one-launch sweep bit for
+// bit (k <= 256).  pv / qv: the rows before the update; returns le = lr * e.
+template <int KPL>
+__device__ __forceinline__ float f32_online_rows(const float* p, const float* q, int k, int lane, float (&pv)[KPL],
+                                                 float (&qv)[KPL], int (&fi)[KPL], bool (&ok)[KPL], double r,
+                                                 float eta) {
+  const int nc = (k + 63) >> 6;  // the sweep's KPL
+  const bool full = k == 64 * nc && nc != 3;
+#pragma unroll
+  for (int c = 0; c < KPL; ++c) {
+    fi[c] = full ? lane * nc + c : lane + 64 * c;
+    ok[c] = c < nc && fi[c] < k;
+    pv[c] = ok[c] ? p[fi[c]] : 0.f;
+    qv[c] = ok[c] ? q[fi[c]] : 0.f;
+  }
+  float part = pv[0] * qv[0];
+#pragma unroll
+  for (int c = 1; c < KPL; ++c)
+    if (c < nc) part = __builtin_fmaf(pv[c], qv[c], part);
+  return f32_err(r, f32_wave_sum(part), eta);
+}
 
 template <typename T, int KPL, int ARITH>
 __global__ __launch_bounds__(256) void k_level(const DetEntry* __restrict__ ent, int64_t n,
@@ -65,6 +89,20 @@ __global__ __launch_bounds__(256) void k_level(const DetEntry* __restrict__ ent,
   const T r = static_cast<T>(ent[j].r);
   T* p = U + static_cast<size_t>(ur) * k;
   T* q = I + static_cast<size_t>(ir) * k;
+  if constexpr (sizeof(T) == 4 && ARITH == static_cast<int>(Arith::kSgdNext) && KPL <= 4) {
+    // f32 online: online_f32.hpp, as k_online_f32
+    float pv[KPL], qv[KPL];
+    int fi[KPL];
+    bool ok[KPL];
+    const float le = f32_online_rows<KPL>(p, q, k, lane, pv, qv, fi, ok, ent[j].r, eta);
+#pragma unroll
+    for (int c = 0; c < KPL; ++c)
+      if (ok[c]) {
+        p[fi[c]] = __builtin_fmaf(le, qv[c], pv[c]);
+        q[fi[c]] = __builtin_fmaf(le, pv[c], qv[c]);
+      }
+    return;
+  }
   T pv[KPL], qv[KPL], pr[KPL];
 #pragma unroll
   for (int c = 0; c < KPL; ++c) {
@@ -296,6 +334,30 @@ __global__ __launch_bounds__(256) void k_level_out(const DetEntry* __restrict__ 
   const T r = static_cast<T>(ent[j].r);
   T* p = U + static_cast<size_t>(ur) * k;
   T* q = I + static_cast<size_t>(ir) * k;
+  const size_t o = static_cast<size_t>(src[j]) * k;
+  if constexpr (sizeof(T) == 4 && KPL <= 4) {
+    // f32 online: online_f32.hpp, as k_online_f32 (the model rows bitwise the sweep's)
+    float pv[KPL], qv[KPL];
+    int fi[KPL];
+    bool ok[KPL];
+    const float le = f32_online_rows<KPL>(p, q, k, lane, pv, qv, fi, ok, ent[j].r, eta);
+#pragma unroll
+    for (int c = 0; c < KPL; ++c)
+      if (ok[c]) {
+        const float pn = __builtin_fmaf(le, qv[c], pv[c]), qn = __builtin_fmaf(le, pv[c], qv[c]);
+        p[fi[c]] = pn;
+        q[fi[c]] = qn;
+        if constexpr (OUT == 1) {
+          if (uout) uout[o + fi[c]] = static_cast<double>(pn);
+          if (iout) iout[o + fi[c]] = static_cast<double>(qn);
+        } else {
+          const float di = le * pv[c];
+          if (uout) uout[o + fi[c]] = static_cast<double>(pv[c] + di);
+          if (iout) iout[o + fi[c]] = static_cast<double>(di);
+        }
+      }
+    return;
+  }
   T pv[KPL], qv[KPL], pr[KPL];
 #pragma unroll
   for (int c = 0; c < KPL; ++c) {
@@ -306,7 +368,6 @@ __global__ __launch_bounds__(256) void k_level_out(const DetEntry* __restrict__ 
   }
   const T e = r - seq_dot<T, KPL>(pr, k);
   const T le = eta * e;
-  const size_t o = static_cast<size_t>(src[j]) * k;
 #pragma unroll
   for (int c = 0; c < KPL; ++c) {
     const int f = lane + 64 * c;

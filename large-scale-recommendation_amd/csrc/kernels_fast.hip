@@ -114,6 +114,8 @@ __device__ __forceinline__ void store_row(__amdgpu_buffer_rsrc_t rs, uint32_t of
         u4 x = {__float_as_uint(r.v[c]), __float_as_uint(r.v[c + 1]), __float_as_uint(r.v[c + 2]),
                 __float_as_uint(r.v[c + 3])};
         __builtin_amdgcn_raw_buffer_store_b128(x, rs, vo + c * 4u, off, AUX);
+        // two wait states before the data VGPRs may be rewritten (gfx950 store-data hazard, pair_device.hpp)
+        asm volatile("s_nop 1" ::"v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]));
       }
     }
   } else {

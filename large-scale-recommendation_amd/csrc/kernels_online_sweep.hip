@@ -1,0 +1,305 @@
+// kernels_online_sweep.hip -- the f32 online micro-batch in one persistent launch
+// (SGDUpdater.nextFactors in sequence order, core/FactorUpdater.scala:37-45, as FlinkOnlineMF.scala's
+// item operator applies it: FlinkOnlineMF.scala:112-137).  k <= 256; the f64 batch and wider f32 rows
+// keep k_online_sweep (kernels_det.hip).
+//
+// Schedule (kernels_online.hip, unchanged): wave w owns the items with row % W == w and applies
+// their updates in sequence order; an update waits for its user's earlier updates (other waves)
+// through a per-user ticket, the count of that user's updates done so far in the batch, and runs
+// when the ticket equals its useq.  A wave's updates are in increasing sequence position, so the
+// earliest unfinished update is always runnable: with every wave resident there is no deadlock.
+//
+// Pipeline (the hot item's wave is the batch's critical path, ~2.3k chained updates per NFLX 1M
+// batch; the previous kernel spent ~1.3 us on each, almost all of it memory round trips in the
+// chain: the ticket reads of the next updates were looked at after a ~128-add fold, the item row was
+// loaded when the item changed, and the previous update's stores were drained every update):
+//   * updates in chunks of 16 with the update's index a compile-time constant (every field a
+//     constant-lane v_readlane), full chunks without exit tests;
+//   * user AND item rows prefetched two updates ahead, after the current update's stores (an item
+//     row is only ever written by this wave; an item that recurs after another one was stored at
+//     the switch, before the prefetch, so a prefetched item row is always current);
+//   * the ticket of update j + 4 polled at update j (read at j + 2, when j + 4's row is prefetched
+//     only if it is already due), and tickets published two updates late: update j waits only for
+//     update j - 2's stores (vmcnt(NW): the operations issued after them), so a store's round trip
+//     overlaps two updates of compute.  A wave publishes every pending ticket before it blocks;
+//   * the dot product is online_f32.hpp's fixed tree (~10 dependent VALU operations, not a 128-add
+//     chain); the level replay uses the same arithmetic, so both give the same factors bit for bit.
+// Every update issues the same vector-memory operations (out-of-range offsets for rows it does not
+// move), so NW is a constant: tools/isa_check.py checks it against the built code.
+//
+// Bytes per update: B_f32(k) = 16k + 20 (an item row held in registers across a run
+// moves less) plus the 16-B update record, its 4-B useq and the ticket word.
+#include <hip/hip_ext.h>
+#include <hip/hip_runtime.h>
+
+#include "kernels.hpp"
+
+namespace mfhip {
+namespace {
+
+#include "online_f32.hpp"
+#include "ticket_wait.hpp"
+
+constexpr int kSC1 = 16;                // buffer cache policy: sc1 (L1 bypass, write-through)
+constexpr uint32_t kOOB = 0xFFFFF000u;  // a row offset past the slab: the load returns 0, no store
+constexpr int kOnChunk = 16;            // updates per register chunk
+
+__device__ __forceinline__ uint32_t rl(uint32_t v, int l) {
+  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), l));
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t raw_rsrc(const void* base, uint64_t bytes) {
+  const uint32_t n = bytes > 0xFFFFF000ull ? 0xFFFFF000u : static_cast<uint32_t>(bytes);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, n, 0x00020000);
+}
+// One row of k floats as this lane's KPL elements (online_f32.hpp layout).  FULL: one access of
+// 4 KPL bytes.  Else KPL 4-B accesses; a lane's element past k reads a clamped in-row address and
+// is zeroed, and its store is masked off (a voffset past the slab would not do: with an
+// out-of-range row offset in soffset the 32-bit sum can wrap back into range).
+template <int KPL, bool FULL>
+struct Rows {
+  static constexpr int OPS = FULL ? 1 : KPL;  // vector-memory operations per row
+  uint32_t voff[OPS];
+  bool valid[OPS];
+  __device__ Rows(int lane, int k) {
+    if constexpr (FULL) {
+      voff[0] = static_cast<uint32_t>(lane) * 4u * KPL;
+      valid[0] = true;
+    } else {
+#pragma unroll
+      for (int c = 0; c < KPL; ++c) {
+        valid[c] = lane + 64 * c < k;
+        voff[c] = static_cast<uint32_t>(valid[c] ? lane + 64 * c : k - 1) * 4u;
+      }
+    }
+  }
+  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rs, uint32_t off, float (&v)[KPL]) const {
+    if constexpr (FULL && KPL == 1) {
+      v[0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, voff[0], off, kSC1));
+    } else if constexpr (FULL && KPL == 2) {
+      const auto x = __builtin_amdgcn_raw_buffer_load_b64(rs, voff[0], off, kSC1);
+      v[0] = __uint_as_float(x[0]);
+      v[1] = __uint_as_float(x[1]);
+    } else if constexpr (FULL && KPL == 4) {
+      const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, voff[0], off, kSC1);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[c] = __uint_as_float(x[c]);
+    } else {
+#pragma unroll
+      for (int c = 0; c < KPL; ++c) {
+        const float x = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, voff[c], off, kSC1));
+        v[c] = valid[c] ? x : 0.f;
+      }
+    }
+  }
+  __device__ __forceinline__ void store(__amdgpu_buffer_rsrc_t rs, uint32_t off, const float (&v)[KPL]) const {
+    if constexpr (FULL && KPL == 1) {
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[0]), rs, voff[0], off, kSC1);
+    } else if constexpr (FULL && KPL == 2) {
+      using u2 = uint32_t __attribute__((ext_vector_type(2)));
+      __builtin_amdgcn_raw_buffer_store_b64(u2{__float_as_uint(v[0]), __float_as_uint(v[1])}, rs, voff[0], off, kSC1);
+    } else if constexpr (FULL && KPL == 4) {
+      using u4 = uint32_t __attribute__((ext_vector_type(4)));
+      const u4 d = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+      __builtin_amdgcn_raw_buffer_store_b128(d, rs, voff[0], off, kSC1);
+      // two wait states before the data VGPRs may be rewritten (gfx950 store-data hazard, pair_device.hpp)
+      asm volatile("s_nop 1" ::"v"(d[0]), "v"(d[1]), "v"(d[2]), "v"(d[3]));
+    } else {
+      // lane 0 is valid for every c (KPL = ceil(k / 64)), so every store issues
+#pragma unroll
+      for (int c = 0; c < KPL; ++c)
+        if (valid[c]) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[c]), rs, voff[c], off, kSC1);
+    }
+  }
+};
+
+// Update x of a wave: lane (x % 16) of chunk x / 16 holds its record (user row, item row, rating,
+// useq); records past the wave's end read as zeros (buffer range).
+struct OnChunk {
+  uint32_t u, i, q;
+  float r;
+};
+
+__device__ __forceinline__ void publish(int32_t* t, int32_t v, int lane) {
+  if (lane == 0) __hip_atomic_store(t, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int32_t poll_issue(const int32_t* t) {
+  return __hip_atomic_load(t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70 & ~0xF);
+}
+
+template <int KPL, bool FULL>
+__global__ __launch_bounds__(64) void k_online_f32(const int64_t* __restrict__ wbeg, const DetEntry* __restrict__ ent,
+                                                   const uint32_t* __restrict__ useq, float* U, float* I,
+                                                   uint64_t u_bytes, uint64_t i_bytes, int k, float eta,
+                                                   int32_t* ticket, int32_t* dummy_ticket, int32_t* err) {
+  using R = Rows<KPL, FULL>;
+  constexpr int CH = kOnChunk;
+  // operations issued after update j-2's stores up to update j's publish: j-2's loads (user row,
+  // item row, ticket poll) and all of j-1's (publish, user + item row stores, its loads)
+  constexpr int NW = (2 * R::OPS + 1) + (1 + 2 * R::OPS + 2 * R::OPS + 1);
+  static_assert(NW < 64, "vmcnt range");
+  const int lane = threadIdx.x;
+  const int64_t jb = wbeg[blockIdx.x];
+  const int32_t cnt = static_cast<int32_t>(wbeg[blockIdx.x + 1] - jb);
+  if (cnt <= 0) return;
+  dummy_ticket += 16 * static_cast<int64_t>(blockIdx.x);  // this wave's own scratch line
+  const R rows(lane, k);
+  const __amdgpu_buffer_rsrc_t urs = raw_rsrc(U, u_bytes), irs = raw_rsrc(I, i_bytes);
+  const __amdgpu_buffer_rsrc_t ers = raw_rsrc(ent + jb, static_cast<uint64_t>(cnt) * sizeof(DetEntry));
+  const __amdgpu_buffer_rsrc_t qrs = raw_rsrc(useq + jb, static_cast<uint64_t>(cnt) * 4u);
+  const uint32_t rowb = static_cast<uint32_t>(k) * 4u;
+  auto chunk = [&](int c) {
+    const uint32_t x = static_cast<uint32_t>(c * CH + (lane & (CH - 1)));
+    const auto e = __builtin_amdgcn_raw_buffer_load_b128(ers, x * 16u, 0, 0);
+    const double r = __longlong_as_double(static_cast<long long>((static_cast<uint64_t>(e[3]) << 32) | e[2]));
+    return OnChunk{e[0], e[1], __builtin_amdgcn_raw_buffer_load_b32(qrs, x * 4u, 0, 0), static_cast<float>(r)};
+  };
+  OnChunk C0 = chunk(0), C1 = chunk(1);
+  auto fu = [&](int s) { return s < CH ? rl(C0.u, s) : rl(C1.u, s - CH); };
+  auto fi = [&](int s) { return s < CH ? rl(C0.i, s) : rl(C1.i, s - CH); };
+  auto fq = [&](int s) { return s < CH ? rl(C0.q, s) : rl(C1.q, s - CH); };
+  auto fr = [&](int s) { return __uint_as_float(s < CH ? rl(__float_as_uint(C0.r), s) : rl(__float_as_uint(C1.r), s - CH)); };
+
+  float P[2][KPL], Q[2][KPL];
+  int32_t okP[2];  // the slot's user row was prefetched (its ticket was due)
+  int32_t tk[2];   // ticket polls, read two updates after they are issued
+  // prologue: updates 0 and 1 (their tickets read here), polls of updates 2 and 3
+#pragma unroll
+  for (int x = 0; x < 2; ++x) {
+    const bool live = x < cnt;
+    const uint32_t u = fu(x);
+    okP[x] = !live || __builtin_amdgcn_readfirstlane(poll_issue(ticket + u)) == static_cast<int32_t>(fq(x));
+    rows.load(urs, live && okP[x] ? u * rowb : kOOB, P[x]);
+    rows.load(irs, live && (x == 0 || fi(1) != fi(0)) ? fi(x) * rowb : kOOB, Q[x]);
+  }
+#pragma unroll
+  for (int x = 0; x < 2; ++x) tk[x] = poll_issue(x + 2 < cnt ? ticket + fu(x + 2) : dummy_ticket);
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  int32_t* pend0 = dummy_ticket;  // update j-2's ticket word and value
+  int32_t pv0 = 0;
+  int32_t* pend1 = dummy_ticket;  // update j-1's
+  int32_t pv1 = 0;
+  float q[KPL];  // the current item's row
+#pragma unroll
+  for (int c = 0; c < KPL; ++c) q[c] = 0.f;
+  uint32_t cur_i = 0;
+
+  // update j (chunk-relative s, a compile-time constant once unrolled); s + 4 < 2 CH
+  auto update = [&](const int s, const int32_t j) {
+    const int slot = s & 1;
+    const uint32_t u = fu(s), i = fi(s);
+    const int32_t qseq = static_cast<int32_t>(fq(s));
+    const float r = fr(s);
+    const uint32_t u2 = fu(s + 2), q2 = fq(s + 2), u4 = fu(s + 4);
+    const uint32_t i1 = fi(s + 1), i2 = fi(s + 2);
+    // 1. the user row, when its ticket was not due at prefetch time: publish the pending tickets
+    //    (after their stores), wait for ours, load now
+    if (!okP[slot]) {
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+      publish(pend0, pv0, lane);
+      publish(pend1, pv1, lane);
+      pend0 = pend1 = dummy_ticket;
+      wait_ticket_or_fail(ticket + u, qseq, err, lane);  // no early return (ticket_wait.hpp)
+      rows.load(urs, u * rowb, P[slot]);
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+    }
+    // 2. the item row: prefetched when the item changed, else the one in registers
+    if (j == 0 || i != cur_i) {
+#pragma unroll
+      for (int c = 0; c < KPL; ++c) q[c] = Q[slot][c];
+    }
+    cur_i = i;
+    // 3. the update (online_f32.hpp)
+    float p[KPL];
+#pragma unroll
+    for (int c = 0; c < KPL; ++c) p[c] = P[slot][c];
+    const float le = f32_err(static_cast<double>(r), f32_wave_sum(f32_lane_dot<KPL>(p, q)), eta);
+    f32_sgd_next<KPL>(p, q, le);
+    // 4. update j-2's stores have landed (NW younger operations may still fly): publish its ticket
+    wait_vmcnt<NW>();
+    publish(pend0, pv0, lane);
+    pend0 = pend1;
+    pv0 = pv1;
+    pend1 = ticket + u;
+    pv1 = qseq + 1;
+    // 5. stores: the user row, and the item row when the next update is on another item (or none)
+    const bool live1 = j + 1 < cnt, live2 = j + 2 < cnt;
+    rows.store(urs, u * rowb, p);
+    rows.store(irs, !live1 || i1 != i ? i * rowb : kOOB, q);
+    // 6. prefetch update j+2 into this slot: its user row if its ticket (polled at j-2) is due, its
+    //    item row if it starts another item's run
+    const int32_t okN = !live2 || __builtin_amdgcn_readfirstlane(tk[slot]) == static_cast<int32_t>(q2);
+    rows.load(urs, live2 && okN ? u2 * rowb : kOOB, P[slot]);
+    rows.load(irs, live2 && i2 != i1 ? i2 * rowb : kOOB, Q[slot]);
+    okP[slot] = okN;
+    // 7. poll update j+4's ticket (read at j+2)
+    tk[slot] = poll_issue(j + 4 < cnt ? ticket + u4 : dummy_ticket);
+  };
+  // full chunks run their updates with no exit test in between (ticket_wait.hpp, kernels_detsweep.hip)
+  for (int32_t c0 = 0;; c0 += CH) {
+    if (c0 + CH <= cnt) {
+#pragma unroll
+      for (int s = 0; s < CH; ++s) update(s, c0 + s);
+    } else {
+#pragma unroll
+      for (int s = 0; s < CH; ++s) {
+        if (c0 + s >= cnt) goto done;
+        update(s, c0 + s);
+      }
+    }
+    C0 = C1;
+    C1 = chunk(c0 / CH + 2);
+  }
+done:
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  publish(pend0, pv0, lane);
+  publish(pend1, pv1, lane);
+}
+
+template <int KPL, bool FULL>
+int capacity_of() {
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_online_f32<KPL, FULL>, 64, 0) != hipSuccess) return 0;
+  return cus * per_cu;
+}
+
+}  // namespace
+
+bool online_f32_supports(int k) { return k >= 1 && k <= 256; }
+
+// KPL = ceil(k / 64) floats per lane; FULL (contiguous, one access per row) when k == 64 KPL, KPL != 3
+int online_f32_capacity(int k) {
+  if (k <= 64) return k == 64 ? capacity_of<1, true>() : capacity_of<1, false>();
+  if (k <= 128) return k == 128 ? capacity_of<2, true>() : capacity_of<2, false>();
+  if (k <= 192) return capacity_of<3, false>();
+  if (k <= 256) return k == 256 ? capacity_of<4, true>() : capacity_of<4, false>();
+  return 0;
+}
+
+void launch_online_f32(hipStream_t st, int nw, const int64_t* wbeg, const DetEntry* ent, const uint32_t* useq, float* U,
+                       float* I, uint64_t u_bytes, uint64_t i_bytes, int k, double eta, int32_t* ticket,
+                       int32_t* dummy_ticket, int32_t* err, hipEvent_t ev0, hipEvent_t ev1) {
+  if (nw <= 0 || !online_f32_supports(k)) return;
+  const dim3 g(static_cast<unsigned>(nw)), b(64);
+  const float e = static_cast<float>(eta);
+#define MF_ON(KPL, FULL)                                                                                    \
+  hipExtLaunchKernelGGL((k_online_f32<KPL, FULL>), g, b, 0, st, ev0, ev1, 0, wbeg, ent, useq, U, I, u_bytes, \
+                        i_bytes, k, e, ticket, dummy_ticket, err)
+  if (k == 64) MF_ON(1, true);
+  else if (k < 64) MF_ON(1, false);
+  else if (k == 128) MF_ON(2, true);
+  else if (k < 128) MF_ON(2, false);
+  else if (k <= 192) MF_ON(3, false);
+  else if (k == 256) MF_ON(4, true);
+  else MF_ON(4, false);
+#undef MF_ON
+}
+
+}  // namespace mfhip

@@ -46,14 +46,6 @@ namespace {
 #define MF_LAUNCH_RELEASE() ((void)0)
 #endif
 
-// experiment: the k = 256 lean single-run path back on (it does not repeat itself; kept to
-// reproduce profiles/r04_k256_repeatability.txt)
-#ifdef MFHIP_EXP_K256_LEAN
-constexpr bool kLeanK256 = true;
-#else
-constexpr bool kLeanK256 = false;
-#endif
-
 #ifdef MFHIP_EXP_ITEM_SC1
 constexpr int kItemPolicy = kSC1;
 #else
@@ -67,7 +59,7 @@ constexpr int kItemPolicy = 0;
 // the previous pair's result (a user rating the item twice in a row), forwarded in registers.
 // IP = cache policy of the item-row accesses (kItemPolicy)
 template <int KPL, int UP, bool FWD, int IP = kItemPolicy>
-__device__ __forceinline__ void single_run_cell(Chunk C0, ChunkRaw C1, __amdgpu_buffer_rsrc_t RR,
+__device__ __forceinline__ void single_run_cell(Chunk C0, __amdgpu_buffer_rsrc_t RR,
                                                 __amdgpu_buffer_rsrc_t urs, __amdgpu_buffer_rsrc_t irs, float eta,
                                                 uint32_t vlane, uint32_t voff, int npairs, uint64_t& wait_clk) {
   (void)wait_clk;
@@ -89,10 +81,12 @@ __device__ __forceinline__ void single_run_cell(Chunk C0, ChunkRaw C1, __amdgpu_
   }
   drain_vmem();
   const float neta = vgpr_of(-eta);
+  ChunkRaw N{};  // the next chunk, loaded when the current one starts (keep_chunk)
   for (int c = 0;; ++c) {
 #pragma unroll
     for (int s = 0; s < CH; ++s) {
       if (c * CH + s >= npairs) goto run_done;
+      if (s == 0) N = chunk_load(RR, c + 1, vlane);
       const int slot = s % DS;
 #if defined(MFHIP_EXPERIMENTS) && defined(MFHIP_WAITPROBE)
       {  // experiment build: shader cycles spent waiting for this pair's prefetched user rows
@@ -102,8 +96,8 @@ __device__ __forceinline__ void single_run_cell(Chunk C0, ChunkRaw C1, __amdgpu_
       }
 #endif
       // the ring's next offsets (pair s + DS), named up front
-      const uint32_t noa = s + DS < CH ? rl(C0.ua, s + DS) : rl(C1.w0[0], s + DS - CH);
-      const uint32_t nob = s + DS < CH ? rl(C0.ub, s + DS) : rl(C1.w0[1], s + DS - CH);
+      const uint32_t noa = s + DS < CH ? rl(C0.ua, s + DS) : rl(N.w0[0], s + DS - CH);
+      const uint32_t nob = s + DS < CH ? rl(C0.ub, s + DS) : rl(N.w0[1], s + DS - CH);
       Row<KPL> pa;
       uint32_t osa;
       if constexpr (FWD) {
@@ -139,10 +133,10 @@ __device__ __forceinline__ void single_run_cell(Chunk C0, ChunkRaw C1, __amdgpu_
       RA[slot] = ld<KPL, UP>(urs, voff, noa);
       RB[slot] = ld<KPL, UP>(urs, voff, nob);
     }
-    C0 = chunk_convert(C1, eta);
-    C1 = chunk_load(RR, c + 2, vlane);
+    C0 = chunk_convert(N, eta);
   }
 run_done:
+  keep_chunk(N);
   st<KPL, IP>(irs, voff, item_off, q);
 }
 
@@ -150,8 +144,10 @@ run_done:
 // a zero high half, so every update of the generic code is a packed op on a half-empty register
 // (and re-zeroing moves).  Here rows are plain floats, and the two updates that share a pattern
 // run as one packed op: {plA, q1} = {ba, aa} * {pa, qa} + wa * {qa, pa} (v_pk_mul_f32, then
-// v_pk_fma_f32 with the halves swapped), likewise {plB, q} from {pb, qb0}.  Same arithmetic per
-// element as the generic step (one product, one fused multiply-add).
+// v_pk_fma_f32 with the halves swapped), likewise {plB, q} from {pb, qb0}.  Same operation count
+// per element as the generic step (one product, one fused multiply-add), but not the same rounding
+// order: the generic step writes s*x + w*y and leaves the contraction to the compiler, this one
+// rounds s*x first and fuses w*y into it.  Fast mode is judged on RMSE (tests/test_gpu_configs.py).
 template <int POL = 0>
 __device__ __forceinline__ float ld1(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t off) {
   return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, voff, off, POL));
@@ -167,7 +163,7 @@ __device__ __forceinline__ f2 pair_update(float s0, float s1, float w, float x, 
 }
 
 template <int UP, bool FWD, int IP = kItemPolicy>
-__device__ __forceinline__ void single_run_cell_k1(Chunk C0, ChunkRaw C1, __amdgpu_buffer_rsrc_t RR,
+__device__ __forceinline__ void single_run_cell_k1(Chunk C0, __amdgpu_buffer_rsrc_t RR,
                                                    __amdgpu_buffer_rsrc_t urs, __amdgpu_buffer_rsrc_t irs, float eta,
                                                    uint32_t vlane, uint32_t voff, int npairs) {
   constexpr int CH = kPairChunk;
@@ -185,13 +181,15 @@ __device__ __forceinline__ void single_run_cell_k1(Chunk C0, ChunkRaw C1, __amdg
   }
   drain_vmem();
   const float neta = vgpr_of(-eta);
+  ChunkRaw N{};  // the next chunk, loaded when the current one starts (keep_chunk)
   for (int c = 0;; ++c) {
 #pragma unroll
     for (int s = 0; s < CH; ++s) {
       if (c * CH + s >= npairs) goto run_done;
+      if (s == 0) N = chunk_load(RR, c + 1, vlane);
       const int slot = s % DS;
-      const uint32_t noa = s + DS < CH ? rl(C0.ua, s + DS) : rl(C1.w0[0], s + DS - CH);
-      const uint32_t nob = s + DS < CH ? rl(C0.ub, s + DS) : rl(C1.w0[1], s + DS - CH);
+      const uint32_t noa = s + DS < CH ? rl(C0.ua, s + DS) : rl(N.w0[0], s + DS - CH);
+      const uint32_t nob = s + DS < CH ? rl(C0.ub, s + DS) : rl(N.w0[1], s + DS - CH);
       float pa;
       uint32_t osa;
       if constexpr (FWD) {
@@ -222,15 +220,15 @@ __device__ __forceinline__ void single_run_cell_k1(Chunk C0, ChunkRaw C1, __amdg
       RA[slot] = ld1<UP>(urs, voff, noa);
       RB[slot] = ld1<UP>(urs, voff, nob);
     }
-    C0 = chunk_convert(C1, eta);
-    C1 = chunk_load(RR, c + 2, vlane);
+    C0 = chunk_convert(N, eta);
   }
 run_done:
+  keep_chunk(N);
   st1<IP>(irs, voff, item_off, q);
 }
 
 template <int D, int UP, int IP = kItemPolicy>
-__device__ __forceinline__ void generic_cell_k1(Chunk C0, ChunkRaw C1, __amdgpu_buffer_rsrc_t RR,
+__device__ __forceinline__ void generic_cell_k1(Chunk C0, __amdgpu_buffer_rsrc_t RR,
                                                 __amdgpu_buffer_rsrc_t urs, __amdgpu_buffer_rsrc_t irs, float eta,
                                                 uint32_t vlane, uint32_t voff, int npairs) {
   constexpr int CH = kPairChunk;
@@ -246,18 +244,20 @@ __device__ __forceinline__ void generic_cell_k1(Chunk C0, ChunkRaw C1, __amdgpu_
   drain_vmem();
   const float neta = vgpr_of(-eta);
   float q = 0.f;
+  ChunkRaw N{};  // the next chunk, loaded when the current one starts (keep_chunk)
   for (int c = 0;; ++c) {
 #pragma unroll
     for (int s = 0; s < CH; ++s) {
-      if (c * CH + s >= npairs) return;
+      if (c * CH + s >= npairs) goto cell_done;
+      if (s == 0) N = chunk_load(RR, c + 1, vlane);
       const int slot = s % D;
       const uint32_t fl = rl(C0.flags, s);
       const uint32_t osa = rl(C0.sa, s), osb = rl(C0.sb, s), osia = rl(C0.sia, s), osi = rl(C0.si, s);
       const bool nin = s + D < CH;
-      const uint32_t nua = nin ? rl(C0.ua, s + D) : rl(C1.w0[0], s + D - CH);
-      const uint32_t nub = nin ? rl(C0.ub, s + D) : rl(C1.w0[1], s + D - CH);
-      const uint32_t nia = nin ? rl(C0.ia, s + D) : rl(C1.w0[2], s + D - CH);
-      const uint32_t nib = nin ? rl(C0.ib, s + D) : rl(C1.w0[3], s + D - CH);
+      const uint32_t nua = nin ? rl(C0.ua, s + D) : rl(N.w0[0], s + D - CH);
+      const uint32_t nub = nin ? rl(C0.ub, s + D) : rl(N.w0[1], s + D - CH);
+      const uint32_t nia = nin ? rl(C0.ia, s + D) : rl(N.w0[2], s + D - CH);
+      const uint32_t nib = nin ? rl(C0.ib, s + D) : rl(N.w0[3], s + D - CH);
       const float kfa = static_cast<float>(fl & 0xFFu), kfb = static_cast<float>((fl >> 8) & 0xFFu);
       const float kq = static_cast<float>((fl >> 16) & 0xFFu);
       const float sr = rlf(C0.sr, s);
@@ -286,16 +286,21 @@ __device__ __forceinline__ void generic_cell_k1(Chunk C0, ChunkRaw C1, __amdgpu_
       QA[slot] = ld1<IP>(irs, voff, nia);
       QB[slot] = ld1<IP>(irs, voff, nib);
     }
-    C0 = chunk_convert(C1, eta);
-    C1 = chunk_load(RR, c + 2, vlane);
+    C0 = chunk_convert(N, eta);
   }
+cell_done:
+  keep_chunk(N);
 }
 
 // One cell (WaveDesc d) of the pair schedule, swept by the calling wave.  UP = cache policy of
-// the user-row loads and stores.  L0 / L1: the cell's first two record chunks, loaded by the
-// caller (the systolic sweep loads them while the previous cell's stores drain).
+// the user-row loads and stores.  L0: the cell's first record chunk, loaded by the caller (the
+// systolic sweep loads it while the previous cell's stores drain).  Chunk c + 1 is loaded when
+// chunk c starts and converted when it ends: a record is first read 49 pairs after its load, and
+// no register the chunk boundary copies is a load still in flight.  (Carrying the raw next chunk
+// across the loop, loaded at the boundary, put a vmcnt(3) -- a whole memory round trip -- at
+// every 56-pair chunk boundary: the compiler copies the loop-carried registers at the header.)
 template <int KPL, int D, int UP, int IP = kItemPolicy>
-__device__ __forceinline__ void pair_cell(const WaveDesc d, const ChunkRaw& L0, const ChunkRaw& L1,
+__device__ __forceinline__ void pair_cell(const WaveDesc d, const ChunkRaw& L0,
                                           const u4v* __restrict__ recs, __amdgpu_buffer_rsrc_t urs,
                                           __amdgpu_buffer_rsrc_t irs, float eta, int lane, uint64_t& wait_clk) {
   (void)wait_clk;
@@ -308,29 +313,21 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const ChunkRaw& L0, 
   const uint32_t voff = static_cast<uint32_t>(lane) * KPL * 4u;
 
   Chunk C0 = chunk_convert(L0, eta);  // current chunk
-  ChunkRaw C1 = L1;                   // next chunk, as loaded
   if constexpr (KPL == 1) {
     if (d.cells == kWaveSingleRun)
-      single_run_cell_k1<UP, false>(C0, C1, RR, urs, irs, eta, vlane, voff, npairs);
+      single_run_cell_k1<UP, false>(C0, RR, urs, irs, eta, vlane, voff, npairs);
     else if (d.cells == kWaveSingleRunFwd)
-      single_run_cell_k1<UP, true>(C0, C1, RR, urs, irs, eta, vlane, voff, npairs);
+      single_run_cell_k1<UP, true>(C0, RR, urs, irs, eta, vlane, voff, npairs);
     else
-      generic_cell_k1<D, UP>(C0, C1, RR, urs, irs, eta, vlane, voff, npairs);
+      generic_cell_k1<D, UP>(C0, RR, urs, irs, eta, vlane, voff, npairs);
     return;
   }
-  // k = 256 sweeps single-run cells with the generic step: with its 16-B rows the lean path did
-  // not repeat itself (a restart of the same fit gave other factors, every run, both kernels)
-  // and its RMSE sat 0.27% off the repeatable runs', which the generic step and the lean path
-  // with 8-B row halves agree on; the halves cost 30% at YAHOO, the generic step 3%
-  // (profiles/r04_k256_repeatability.txt)
-  if constexpr (KPL >= 4 && !kLeanK256) {
-  } else if (d.cells == kWaveSingleRun) {
-    single_run_cell<KPL, UP, false>(C0, C1, RR, urs, irs, eta, vlane, voff, npairs, wait_clk);
+  if (d.cells == kWaveSingleRun) {
+    single_run_cell<KPL, UP, false>(C0, RR, urs, irs, eta, vlane, voff, npairs, wait_clk);
     return;
   }
-  if constexpr (KPL >= 4 && !kLeanK256) {
-  } else if (d.cells == kWaveSingleRunFwd) {
-    single_run_cell<KPL, UP, true>(C0, C1, RR, urs, irs, eta, vlane, voff, npairs, wait_clk);
+  if (d.cells == kWaveSingleRunFwd) {
+    single_run_cell<KPL, UP, true>(C0, RR, urs, irs, eta, vlane, voff, npairs, wait_clk);
     return;
   }
   Row<KPL> plA, plB;  // the previous pair's updated user rows (forwarding)
@@ -354,10 +351,12 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const ChunkRaw& L0, 
 #pragma unroll
     for (int e = 0; e < NV; ++e) q.v[e] = f2{0.f, 0.f};
 
+    ChunkRaw N{};  // the next chunk, loaded when the current one starts (keep_chunk)
     for (int c = 0;; ++c) {
 #pragma unroll
       for (int s = 0; s < CH; ++s) {
-        if (c * CH + s >= npairs) return;
+        if (c * CH + s >= npairs) goto cell_done;
+        if (s == 0) N = chunk_load(RR, c + 1, vlane);
         const int slot = s % D;
 #if defined(MFHIP_EXPERIMENTS) && defined(MFHIP_WAITPROBE)
         {  // experiment build: shader cycles spent waiting for this pair's prefetched rows
@@ -371,10 +370,10 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const ChunkRaw& L0, 
         // before each store (a v_readlane feeding a buffer store's soffset costs an s_nop 4)
         const uint32_t osa = rl(C0.sa, s), osb = rl(C0.sb, s), osia = rl(C0.sia, s), osi = rl(C0.si, s);
         const bool nin = s + D < CH;  // offsets of pair s + D (the ring's next rows)
-        const uint32_t nua = nin ? rl(C0.ua, s + D) : rl(C1.w0[0], s + D - CH);
-        const uint32_t nub = nin ? rl(C0.ub, s + D) : rl(C1.w0[1], s + D - CH);
-        const uint32_t nia = nin ? rl(C0.ia, s + D) : rl(C1.w0[2], s + D - CH);
-        const uint32_t nib = nin ? rl(C0.ib, s + D) : rl(C1.w0[3], s + D - CH);
+        const uint32_t nua = nin ? rl(C0.ua, s + D) : rl(N.w0[0], s + D - CH);
+        const uint32_t nub = nin ? rl(C0.ub, s + D) : rl(N.w0[1], s + D - CH);
+        const uint32_t nia = nin ? rl(C0.ia, s + D) : rl(N.w0[2], s + D - CH);
+        const uint32_t nib = nin ? rl(C0.ib, s + D) : rl(N.w0[3], s + D - CH);
         // byte flags -> float coefficients (v_cvt_f32_ubyteN): forwarding, keep q, split
         const float kfa = static_cast<float>(fl & 0xFFu), kfb = static_cast<float>((fl >> 8) & 0xFFu);
         const float kq = static_cast<float>((fl >> 16) & 0xFFu);
@@ -415,9 +414,10 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const ChunkRaw& L0, 
         QA[slot] = ld<KPL, IP>(irs, voff, nia);
         QB[slot] = ld<KPL, IP>(irs, voff, nib);
       }
-      C0 = chunk_convert(C1, eta);
-      C1 = chunk_load(RR, c + 2, vlane);
+      C0 = chunk_convert(N, eta);
     }
+  cell_done:
+    keep_chunk(N);
 #undef MF_PREFETCH
   }
 }
@@ -433,7 +433,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   const __amdgpu_buffer_rsrc_t rr = cell_records(recs, d.base, d.steps);
   const uint32_t vlane = threadIdx.x * 64u;
   uint64_t wait_clk = 0;
-  pair_cell<KPL, D, 0>(d, chunk_load(rr, 0, vlane), chunk_load(rr, 1, vlane), recs, raw_rsrc(U, u_bytes),
+  pair_cell<KPL, D, 0>(d, chunk_load(rr, 0, vlane), recs, raw_rsrc(U, u_bytes),
                        raw_rsrc(I, i_bytes), eta, threadIdx.x, wait_clk);
   MF_LAUNCH_RELEASE();
   if (trace && threadIdx.x == 0) {
@@ -454,8 +454,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
 // agent-scope relaxed loads (sc1).  Progress words are monotonic across launches (base), so
 // they are never reset.  Every wave must be resident at once (the host checks occupancy); a
 // poll that exceeds ~1 s sets err[0] and the wave gives up (the host then fails loudly).
-// PRE: the next cell's first two record chunks are loaded right after a cell's last stores are
-// issued, so they arrive while those stores drain (vmcnt(8) waits for the stores only): a cell no
+// PRE: the next cell's first record chunk is loaded right after a cell's last stores are
+// issued, so it arrives while those stores drain (vmcnt(4) waits for the stores only): a cell no
 // longer starts with a record fetch on its critical path (an empty cell reads nothing; past the
 // last cell the last cell's records are read again, unused).  The neighbour's progress is polled
 // after the drain, as late as possible (read before the drain it was too often not yet there: an
@@ -484,14 +484,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   int32_t* nb_prog = prog + static_cast<int64_t>(w.nbr) * kProgStride;
   const __amdgpu_buffer_rsrc_t urs = raw_rsrc(U, u_bytes), irs = raw_rsrc(I, i_bytes);
   const uint32_t vlane = static_cast<uint32_t>(lane) * 64u;
-  auto first_chunks = [&](const WaveDesc& c, ChunkRaw& A, ChunkRaw& B) {  // an empty cell reads nothing
-    const __amdgpu_buffer_rsrc_t rr = cell_records(recs, c.base, c.steps);
-    A = chunk_load(rr, 0, vlane);
-    B = chunk_load(rr, 1, vlane);
+  auto first_chunks = [&](const WaveDesc& c, ChunkRaw& A) {  // an empty cell reads nothing
+    A = chunk_load(cell_records(recs, c.base, c.steps), 0, vlane);
   };
   WaveDesc d = my[0];
-  ChunkRaw L0, L1;
-  if (PRE) first_chunks(d, L0, L1);
+  ChunkRaw L0;
+  if (PRE) first_chunks(d, L0);
   for (int t = 0; t < w.G; ++t) {
     const WaveDesc dn = my[t + 1 < w.G ? t + 1 : t];  // scalar load, used after this cell
     if (t > 0 && w.G > 1) {
@@ -514,11 +512,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     const uint64_t c_start = __builtin_amdgcn_s_memrealtime();
     uint64_t c_clk = trace ? __builtin_amdgcn_s_memtime() : 0;
     uint64_t wait_clk = 0;
-    if (!PRE && d.steps > 0) first_chunks(d, L0, L1);
-    if (d.steps > 0) pair_cell<KPL, D, kSC1>(d, L0, L1, recs, urs, irs, eta, lane, wait_clk);
+    if (!PRE && d.steps > 0) first_chunks(d, L0);
+    if (d.steps > 0) pair_cell<KPL, D, kSC1>(d, L0, recs, urs, irs, eta, lane, wait_clk);
     if (PRE) {
-      first_chunks(dn, L0, L1);
-      __builtin_amdgcn_s_waitcnt(0x0F78);  // vmcnt(8): the 8 loads above may fly, every older store has landed
+      first_chunks(dn, L0);
+      __builtin_amdgcn_s_waitcnt(0x0F74);  // vmcnt(4): the 4 loads above may fly, every older store has landed
     } else {
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): every user-row store of this wave has landed
     }

@@ -480,9 +480,9 @@ void sync_all(mf_ctx* ctx) {
         // the context refuses further supersteps and reads until the fit is prepared again
         ctx->failed = eb == &s.fast_err
                           ? "fast sweep: a wave waited > 1 s for its neighbour (workgroups not co-resident?); "
-                            "set MFHIP_TEST=pair_sys=0 (or fast_kernel=cell)"
+                            "set MFHIP_TEST=pair_sys=0 (or fast_kernel=cell; INTEGRATION.md section 5)"
                           : "deterministic sweep: a wave waited > 1 s for a user ticket (waves not co-resident?); "
-                            "set MFHIP_TEST=det_kernel=level";
+                            "set MFHIP_TEST=det_kernel=level (INTEGRATION.md section 5)";
         fail(MF_ERR_TIMEOUT, ctx->failed);
       }
     }
@@ -1735,7 +1735,8 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
   int cap = 0;
   if (n > 0 && !outs && test_knob("online_kernel") != "level") {
     DeviceGuard g(s.device);
-    cap = online_sweep_capacity(k, ctx->f64);  // 0 (occupancy query failed): the level replay
+    // 0 (occupancy query failed): the level replay
+    cap = !ctx->f64 && online_f32_supports(k) ? online_f32_capacity(k) : online_sweep_capacity(k, ctx->f64);
   }
   // the sweep in arrival order takes the rows straight into its pinned upload buffer (user rows,
   // item rows, ratings: 16 B per rating), with no staging pass; otherwise they go to on_ur / on_ir
@@ -1890,7 +1891,14 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
     MF_HIP(hipMemsetAsync(sc.uticket.get(), 0, static_cast<size_t>(std::max<int64_t>(ctx->U.rows(), 1)) * 4, s.stream));
     sc.err.alloc(4);
     MF_HIP(hipMemsetAsync(sc.err.get(), 0, 4, s.stream));
-    {
+    if (!ctx->f64 && online_f32_supports(k)) {
+      sc.dummy.alloc(static_cast<size_t>(W) * 64);
+      LaunchTimer t(s, ctx->profiling, true);
+      launch_online_f32(s.stream, static_cast<int>(W), sc.wbeg.as<int64_t>(), s.det_dev.as<DetEntry>(),
+                        reinterpret_cast<const uint32_t*>(s.det_dev.as<char>() + ebytes), s.uf.as<float>(),
+                        s.itf.as<float>(), s.uf.bytes(), s.itf.bytes(), k, ctx->P.online_learning_rate,
+                        sc.uticket.as<int32_t>(), sc.dummy.as<int32_t>(), sc.err.as<int32_t>(), t.start(), t.stop());
+    } else {
       LaunchTimer t(s, ctx->profiling);
       launch_online_sweep(s.stream, static_cast<int>(W), sc.wbeg.as<int64_t>(), s.det_dev.as<DetEntry>(),
                           reinterpret_cast<const uint32_t*>(s.det_dev.as<char>() + ebytes), s.uf.get(), s.itf.get(), k,
@@ -1907,7 +1915,7 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
       // in the index: the model is partly updated, so the context refuses further work (as the
       // DSGD sweeps do, sync_all) until a fit is prepared again
       ctx->failed = "online sweep: a wave waited > 1 s for a user ticket (waves not co-resident?); "
-                    "set MFHIP_TEST=online_kernel=level";
+                    "set MFHIP_TEST=online_kernel=level (INTEGRATION.md section 5)";
       fail(MF_ERR_TIMEOUT, ctx->failed);
     }
     if (tu) *tu = touched[0];

@@ -5,6 +5,7 @@
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+typedef uint32_t u3v __attribute__((ext_vector_type(3)));
 
 __device__ __forceinline__ uint32_t rl(uint32_t v, int l) {
   return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), l));
@@ -75,6 +76,22 @@ __device__ __forceinline__ Row<KPL> ld(__amdgpu_buffer_rsrc_t rs, uint32_t voff,
   return r;
 }
 
+// A 16-B buffer store, then two wait states before its data VGPRs can be rewritten.  gfx950
+// reads a store's data after issuing it: a VALU that overwrites the data VGPRs right behind a
+// buffer_store_dwordx4 corrupts the stored row under load -- 1.2% of 16-B records with the offset
+// in an SGPR and no wait state, 1.5% with soffset 0 and one wait state, none with two
+// (tools/micro/store_data_hazard.hip, profiles/r05_store_data_hazard.txt).  LLVM pads one wait
+// state, and none at all when soffset is an SGPR (the table's exemption), so the round-4 k = 256
+// lean sweep, whose compiler reused the data VGPRs one or two instructions after the store, wrote
+// torn user rows: it did not repeat itself and biased RMSE by 0.27%.  The s_nop below takes the
+// data as operands, so no instruction can rewrite those VGPRs before it, and it is ordered after
+// the store (both have side effects).  tests/test_isa.py checks every wide store of the library.
+__device__ __forceinline__ void store_b128(u4v d, __amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t off, int pol_sc1) {
+  if (pol_sc1) __builtin_amdgcn_raw_buffer_store_b128(d, rs, voff, off, 16);
+  else __builtin_amdgcn_raw_buffer_store_b128(d, rs, voff, off, 0);
+  asm volatile("s_nop 1" ::"v"(d[0]), "v"(d[1]), "v"(d[2]), "v"(d[3]));
+}
+
 template <int KPL, int POL = 0>
 __device__ __forceinline__ void st(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t off, const Row<KPL>& r) {
   if constexpr (KPL == 1) {
@@ -83,11 +100,12 @@ __device__ __forceinline__ void st(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uin
     using u2 = uint32_t __attribute__((ext_vector_type(2)));
     __builtin_amdgcn_raw_buffer_store_b64(u2{__float_as_uint(r.v[0].x), __float_as_uint(r.v[0].y)}, rs, voff, off, POL);
   } else {
+    static_assert(POL == 0 || POL == 16, "store policy");
 #pragma unroll
     for (int c = 0; c < KPL / 4; ++c)
-      __builtin_amdgcn_raw_buffer_store_b128(u4v{__float_as_uint(r.v[2 * c].x), __float_as_uint(r.v[2 * c].y),
-                                                 __float_as_uint(r.v[2 * c + 1].x), __float_as_uint(r.v[2 * c + 1].y)},
-                                             rs, voff + 16u * c, off, POL);
+      store_b128(u4v{__float_as_uint(r.v[2 * c].x), __float_as_uint(r.v[2 * c].y), __float_as_uint(r.v[2 * c + 1].x),
+                     __float_as_uint(r.v[2 * c + 1].y)},
+                 rs, voff + 16u * c, off, POL == 16);
   }
 }
 
@@ -120,7 +138,8 @@ struct Chunk {
 __device__ __forceinline__ void drain_vmem() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
 struct ChunkRaw {
-  u4v w0, w1, w2, w3;
+  u4v w0, w1, w2;
+  u3v w3;  // the fourth word group's last word is unused: a 12-B load (no dead VGPR a load still writes)
 };
 
 // A cell's pair records as a raw buffer of exactly its records: a lane past the cell's last pair
@@ -133,12 +152,23 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t cell_records(const u4v* recs, 
 // Chunk c of the cell: pair c * kPairChunk + lane in lane `lane` (vlane = lane * 64).  Records are
 // read once: non-temporal (cache policy nt), so they do not push factor rows out of L2 / MALL.
 __device__ __forceinline__ ChunkRaw chunk_load(__amdgpu_buffer_rsrc_t rr, int c, uint32_t vlane) {
-  const uint32_t so = static_cast<uint32_t>(c) * kPairChunk * 64u;
+  // c is uniform, but the divergence analysis cannot always prove it through the cell loops'
+  // exits (the generic k = 128 loop's chunk loads became a readfirstlane waterfall): say so
+  const uint32_t so = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(c)) * kPairChunk * 64u;
   constexpr int kNT = 2;
   return ChunkRaw{__builtin_amdgcn_raw_buffer_load_b128(rr, vlane, so, kNT),
                   __builtin_amdgcn_raw_buffer_load_b128(rr, vlane + 16u, so, kNT),
                   __builtin_amdgcn_raw_buffer_load_b128(rr, vlane + 32u, so, kNT),
-                  __builtin_amdgcn_raw_buffer_load_b128(rr, vlane + 48u, so, kNT)};
+                  __builtin_amdgcn_raw_buffer_load_b96(rr, vlane + 48u, so, kNT)};
+}
+
+// A use of every word group of a chunk on a cell's exit path.  Without a use there, LLVM's IR
+// sinking pass moves each record load of chunk c + 1 (issued when chunk c starts) down to the
+// block of its first use -- 49 pairs later for the ring offsets, the chunk's end for the rest --
+// where the wave then waits a whole memory round trip for it.  The exit is reached from every
+// pair, so no block below the load dominates all uses and the loads stay where they are issued.
+__device__ __forceinline__ void keep_chunk(const ChunkRaw& r) {
+  __asm__ volatile("; keep %0 %1 %2 %3" ::"v"(r.w0[0]), "v"(r.w1[0]), "v"(r.w2[0]), "v"(r.w3[0]));
 }
 
 __device__ __forceinline__ Chunk chunk_convert(const ChunkRaw& r, float eta) {

@@ -444,12 +444,16 @@ def test_systolic_sweep_equals_substep_launches(monkeypatch, k, nb, G, hot, n):
     assert outs[1][2] < outs[0][2]  # the systolic path really ran (one launch per superstep)
 
 
-@pytest.mark.parametrize("config,scale", [("ML20M", 0.1), ("NFLX", 0.05), ("YAHOO", 0.05)])
-def test_fast_fit_repeats_itself_after_restart(config, scale):
+@pytest.mark.parametrize("config,scale,pair_sys", [("ML20M", 0.1, 1), ("NFLX", 0.05, 1), ("YAHOO", 0.05, 1),
+                                                   ("YAHOO", 0.05, 0)])
+def test_fast_fit_repeats_itself_after_restart(monkeypatch, config, scale, pair_sys):
     """A fast fit has no atomics and a fixed plan, so mf_dsgd_restart + the same epochs must give
     the same factors bit for bit (k = 64 / 128 / 256 through the BASELINE-shaped synthetics, whose
-    Zipf heads make single-run cells).  At k = 256 the round-4 lean single-run path with 16-B rows
-    did not (profiles/r04_k256_repeatability.txt)."""
+    Zipf heads make single-run cells; the systolic launch and the per-sub-step launches).  The
+    round-4 k = 256 lean single-run path did not: its compiled code rewrote the data VGPRs of
+    16-B user-row stores right behind the store, which gfx950 does not survive under load
+    (profiles/r05_store_data_hazard.txt); the stores now pin two wait states."""
+    set_knob(monkeypatch, "pair_sys", str(pair_sys))
     d = synth.config(config, scale)
     (u, i, r), _ = d.split()
     _, _, _, k, nb = synth.CONFIGS[config]
@@ -463,6 +467,23 @@ def test_fast_fit_repeats_itself_after_restart(config, scale):
             ctx.run(2 * nb)
             again = (ctx.factors(0)[1], ctx.factors(1)[1])
             assert np.array_equal(first[0], again[0]) and np.array_equal(first[1], again[1])
+
+
+@pytest.mark.parametrize("k", [64, 128, 256])
+@pytest.mark.parametrize("pair_sys", [0, 1])
+def test_fast_fit_repeats_itself_hot_item(monkeypatch, k, pair_sys):
+    """The lean single-run path (one long item run per cell) and the generic step repeat themselves
+    after a restart, bit for bit, at every row width and in both launch forms."""
+    set_knob(monkeypatch, "pair_sys", str(pair_sys))
+    d = hot_item_data(k)
+    with mfhip.Context(params(k, 3, 2, 3, mode=L.MODE_FAST_F32, lam=1.0, lr=0.002, fast_waves=-4,
+                              blocking=L.BLOCKING_REFERENCE)) as ctx:
+        ctx.fit(d.u, d.i, d.r)
+        first = (ctx.factors(0)[1], ctx.factors(1)[1])
+        for _ in range(2):
+            ctx.restart()
+            ctx.run(3 * 2)
+            assert np.array_equal(first[0], ctx.factors(0)[1]) and np.array_equal(first[1], ctx.factors(1)[1])
 
 
 def test_systolic_multi_shard_matches_single(monkeypatch):

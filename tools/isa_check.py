@@ -340,6 +340,7 @@ CHECKS = [
     (r"k_sweep_pair_sys", "all"),
     (r"k_det_sweep2", "prev"),
     (r"k_online_sweepId", "prev"),
+    (r"k_online_f32", "prev"),
 ]
 
 
