@@ -42,12 +42,6 @@ __device__ __forceinline__ double rld(double v, int l) {
 }
 
 __device__ __forceinline__ double uniform(double v) { return rld(v, 0); }
-__device__ __forceinline__ double ld_sc1(const double* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_sc1(double* p, double v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 #include "seq_fold.hpp"
 #include "ticket_wait.hpp"
@@ -63,25 +57,32 @@ __device__ __forceinline__ DetChunk det_chunk(const uint32_t* eu, const uint32_t
   return DetChunk{eu[x], ei[x], eq[x], er[x]};
 }
 
-__device__ __forceinline__ int32_t poll(const int32_t* t) {
-  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-// The same load without reading it: the wave waits for it only where the value is used.
-__device__ __forceinline__ int32_t poll_issue(const int32_t* t) {
-  return __hip_atomic_load(t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Lane 0 stores the ticket (one word, one request; the wave's earlier stores have drained).
-__device__ __forceinline__ void publish(int32_t* t, int32_t v, int lane) {
-  if (lane == 0) __hip_atomic_store(t, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t raw_rsrc(const void* base, uint64_t bytes) {
   const uint32_t n = bytes > 0xFFFFF000ull ? 0xFFFFF000u : static_cast<uint32_t>(bytes);
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, n, 0x00020000);
 }
 constexpr int kSC1 = 16;                   // buffer cache policy: sc1 (L1 bypass, write-through)
 constexpr uint32_t kOOB = 0xFFFFF000u;     // a row offset past the slab: the load returns 0, no store
+
+// Ticket words and lambda / omega through raw buffers with the word's byte offset in an SGPR: one
+// scalar shift per access instead of a 64-bit address and a select, and "none" is the out-of-range
+// offset kOOB (the load returns 0, the store is dropped) instead of a per-wave dummy word.  Every
+// lane touches the same word (same value): no exec mask around a publish.  sc1 loads and stores,
+// the agent-scope relaxed atomics of the hand-off (MI355X_MICROARCH.md, valid forms: buffer_load_dword
+// sc1 poll).
+__device__ __forceinline__ int32_t poll_issue(__amdgpu_buffer_rsrc_t trs, uint32_t off) {
+  return static_cast<int32_t>(__builtin_amdgcn_raw_buffer_load_b32(trs, 0, off, kSC1));
+}
+__device__ __forceinline__ int32_t poll(__amdgpu_buffer_rsrc_t trs, uint32_t off) {
+  return __builtin_amdgcn_readfirstlane(poll_issue(trs, off));
+}
+__device__ __forceinline__ void publish(__amdgpu_buffer_rsrc_t trs, uint32_t off, int32_t v) {
+  __builtin_amdgcn_raw_buffer_store_b32(static_cast<uint32_t>(v), trs, 0, off, kSC1);
+}
+__device__ __forceinline__ double ld_reg(__amdgpu_buffer_rsrc_t rs, uint32_t row) {
+  const auto x = __builtin_amdgcn_raw_buffer_load_b64(rs, 0, row * 8u, kSC1);
+  return __longlong_as_double(static_cast<long long>((static_cast<uint64_t>(x[1]) << 32) | x[0]));
+}
 
 template <int KPL>
 struct DRow {
@@ -159,6 +160,8 @@ __device__ __forceinline__ void det_wave(const DetWave d, const uint32_t* __rest
   const int lane = threadIdx.x;
   const int32_t cnt = d.count;  // 32-bit: the entry tests are scalar compares, not 64-bit VALU ones
   const __amdgpu_buffer_rsrc_t urs = raw_rsrc(U, u_bytes), irs = raw_rsrc(I, i_bytes);
+  const __amdgpu_buffer_rsrc_t trs = raw_rsrc(ticket, 0xFFFFF000ull);  // offsets are user rows * 4
+  const __amdgpu_buffer_rsrc_t rus = raw_rsrc(regU, 0xFFFFF000ull), ris = raw_rsrc(regI, 0xFFFFF000ull);
   uint32_t voff[KPL];
 #pragma unroll
   for (int c = 0; c < KPL; ++c) voff[c] = lane + 64 * c < k ? static_cast<uint32_t>(lane + 64 * c) * 8u : 0x80000000u;
@@ -181,20 +184,20 @@ __device__ __forceinline__ void det_wave(const DetWave d, const uint32_t* __rest
   for (int x = 0; x < 2; ++x) {
     const bool live = x < cnt;
     const uint32_t u = fu(x), i = fi(x), q = fq(x);
-    okP[x] = !live || poll(ticket + u) == static_cast<int32_t>(q & kDetUseqMask);
+    okP[x] = !live || poll(trs, u * 4u) == static_cast<int32_t>(q & kDetUseqMask);
     P[x] = ldrow<KPL>(urs, voff, live && okP[x] ? u * rowb : kOOB);
-    RU[x] = ld_sc1(regU + (live ? u : 0u));
+    RU[x] = ld_reg(rus, live ? u : 0u);
     if (!SINGLE || x == 0) {
       Q[x] = ldrow<KPL>(irs, voff, live && !(x > 0 && (q & kDetKeepQ)) ? i * rowb : kOOB);
-      RI[x] = ld_sc1(regI + (live ? i : 0u));
+      RI[x] = ld_reg(ris, live ? i : 0u);
     }
   }
 #pragma unroll
-  for (int x = 0; x < 2; ++x) tk[x] = poll_issue(x + 2 < cnt ? ticket + fu(x + 2) : dummy_ticket);
+  for (int x = 0; x < 2; ++x) tk[x] = poll_issue(trs, x + 2 < cnt ? fu(x + 2) * 4u : kOOB);
   __builtin_amdgcn_s_waitcnt(0x0F70);
-  int32_t* pend0 = dummy_ticket;  // entry j-2's ticket word and value
+  uint32_t pend0 = kOOB;  // entry j-2's ticket word (byte offset; kOOB: none) and value
   int32_t pv0 = 0;
-  int32_t* pend1 = dummy_ticket;  // entry j-1's
+  uint32_t pend1 = kOOB;  // entry j-1's
   int32_t pv1 = 0;
   double q[KPL];
 #pragma unroll
@@ -221,9 +224,9 @@ __device__ __forceinline__ void det_wave(const DetWave d, const uint32_t* __rest
     //    pending ticket (after its stores), wait for ours, load now
     if (!okP[slot]) {
       __builtin_amdgcn_s_waitcnt(0x0F70);
-      publish(pend0, pv0, lane);
-      publish(pend1, pv1, lane);
-      pend0 = pend1 = dummy_ticket;
+      publish(trs, pend0, pv0);
+      publish(trs, pend1, pv1);
+      pend0 = pend1 = kOOB;
       wait_ticket_or_fail(ticket + u, useq, err, lane);  // no early return (ticket_wait.hpp)
       P[slot] = ldrow<KPL>(urs, voff, u * rowb);
       __builtin_amdgcn_s_waitcnt(0x0F70);
@@ -250,10 +253,10 @@ __device__ __forceinline__ void det_wave(const DetWave d, const uint32_t* __rest
     }
     // 3. entry j-2's stores have landed (NW younger operations may still fly): publish its ticket
     wait_vmcnt<NW>();
-    publish(pend0, pv0, lane);
+    publish(trs, pend0, pv0);
     pend0 = pend1;
     pv0 = pv1;
-    pend1 = ticket + u;
+    pend1 = u * 4u;
     pv1 = useq + 1;
     // 4. entry j's stores
     strow<KPL>(urs, voff, u * rowb, pn);
@@ -264,14 +267,14 @@ __device__ __forceinline__ void det_wave(const DetWave d, const uint32_t* __rest
     const bool live2 = j + 2 < cnt;
     const int32_t okN = !live2 || __builtin_amdgcn_readfirstlane(tk[slot]) == static_cast<int32_t>(q2 & kDetUseqMask);
     P[slot] = ldrow<KPL>(urs, voff, live2 && okN ? u2 * rowb : kOOB);
-    RU[slot] = ld_sc1(regU + (live2 ? u2 : 0u));
+    RU[slot] = ld_reg(rus, live2 ? u2 : 0u);
     if (!SINGLE) {
       Q[slot] = ldrow<KPL>(irs, voff, live2 && !(q2 & kDetKeepQ) ? i2 * rowb : kOOB);
-      RI[slot] = ld_sc1(regI + (live2 ? i2 : 0u));
+      RI[slot] = ld_reg(ris, live2 ? i2 : 0u);
     }
     okP[slot] = okN;
     // 6. poll entry j+4's ticket (read at entry j+2)
-    tk[slot] = poll_issue(j + 4 < cnt ? ticket + u4 : dummy_ticket);
+    tk[slot] = poll_issue(trs, j + 4 < cnt ? u4 * 4u : kOOB);
     stamp(3);
   };
   // Full chunks run their CH entries with no exit test in between: a per-entry "j >= cnt" exit
@@ -296,8 +299,8 @@ __device__ __forceinline__ void det_wave(const DetWave d, const uint32_t* __rest
 done:
   if (SINGLE) strow<KPL>(irs, voff, item0 * rowb, q);  // the item row, once
   __builtin_amdgcn_s_waitcnt(0x0F70);
-  publish(pend0, pv0, lane);
-  publish(pend1, pv1, lane);
+  publish(trs, pend0, pv0);
+  publish(trs, pend1, pv1);
 #if defined(MFHIP_EXPERIMENTS) && defined(MFHIP_DET_PROBE)
   if (blockIdx.x == 0 && lane == 0)
     printf("[det probe] wave 0: %lld entries, cycles per entry: pre-fold %.0f fold %.0f post-fold %.0f prefetch %.0f\n",
@@ -313,9 +316,9 @@ __global__ __launch_bounds__(64) void k_det_sweep2(const DetWave* __restrict__ w
                                                    const double* __restrict__ regI, int k, double eta,
                                                    int32_t* ticket, int32_t* dummy_ticket, int32_t* err) {
   __shared__ __attribute__((aligned(16))) double lds[64 * KPL];
+  (void)dummy_ticket;  // "no ticket" is the out-of-range offset kOOB now
   const DetWave d = waves[blockIdx.x];
   if (d.count == 0) return;
-  dummy_ticket += 16 * static_cast<int64_t>(blockIdx.x);  // this wave's own scratch line
   if (d.flags & kDetWaveSingleItem)
     det_wave<KPL, FULL, true>(d, eu, ei, eq, er, U, I, u_bytes, i_bytes, regU, regI, k, eta, ticket, dummy_ticket, err, lds);
   else

@@ -30,6 +30,8 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
+#include <utility>
+
 #include "kernels.hpp"
 
 namespace mfhip {
@@ -71,71 +73,62 @@ __device__ __forceinline__ void single_run_cell(Chunk C0, __amdgpu_buffer_rsrc_t
   Row<KPL> RA[DS], RB[DS], plA, plB;
 #pragma unroll
   for (int e = 0; e < NV; ++e) plA.v[e] = plB.v[e] = f2{0.f, 0.f};
-  uint32_t oa[DS], ob[DS];
 #pragma unroll
   for (int s = 0; s < DS; ++s) {
-    oa[s] = rl(C0.ua, s);
-    ob[s] = rl(C0.ub, s);
-    RA[s] = ld<KPL, UP>(urs, voff, oa[s]);
-    RB[s] = ld<KPL, UP>(urs, voff, ob[s]);
+    RA[s] = ld<KPL, UP>(urs, voff, rl(C0.ua, s));
+    RB[s] = ld<KPL, UP>(urs, voff, rl(C0.ub, s));
   }
   drain_vmem();
   const float neta = vgpr_of(-eta);
-  ChunkRaw N{};  // the next chunk, loaded when the current one starts (keep_chunk)
-  for (int c = 0;; ++c) {
-#pragma unroll
-    for (int s = 0; s < CH; ++s) {
-      if (c * CH + s >= npairs) goto run_done;
-      if (s == 0) N = chunk_load(RR, c + 1, vlane);
-      const int slot = s % DS;
+  ChunkRaw N{};  // the next chunk (sweep_chunks loads it when the current one starts)
+  auto pair = [&](auto S) __attribute__((always_inline)) {
+    constexpr int s = decltype(S)::value;
+    const int slot = s % DS;
 #if defined(MFHIP_EXPERIMENTS) && defined(MFHIP_WAITPROBE)
-      {  // experiment build: shader cycles spent waiting for this pair's prefetched user rows
-        const uint64_t a = __builtin_amdgcn_s_memtime();
-        __builtin_amdgcn_s_waitcnt((4 * (DS - 1)) & 15 | (((4 * (DS - 1)) >> 4) << 14) | 0x0F70 & ~0xF);
-        wait_clk += __builtin_amdgcn_s_memtime() - a;
-      }
-#endif
-      // the ring's next offsets (pair s + DS), named up front
-      const uint32_t noa = s + DS < CH ? rl(C0.ua, s + DS) : rl(N.w0[0], s + DS - CH);
-      const uint32_t nob = s + DS < CH ? rl(C0.ub, s + DS) : rl(N.w0[1], s + DS - CH);
-      Row<KPL> pa;
-      uint32_t osa;
-      if constexpr (FWD) {
-        const uint32_t fl = rl(C0.flags, s);
-        osa = rl(C0.sa, s);
-        const float kfa = static_cast<float>(fl & 0xFFu), kfb = static_cast<float>((fl >> 8) & 0xFFu);
-#pragma unroll
-        for (int e = 0; e < NV; ++e) pa.v[e] = kfb * plB.v[e] + (kfa * plA.v[e] + RA[slot].v[e]);
-      } else {
-        osa = oa[slot];
-        pa = RA[slot];
-      }
-      const Row<KPL> pb = RB[slot];
-      float c1 = dot_part<KPL>(pa, q), c2 = dot_part<KPL>(pb, q), g = dot_part<KPL>(pb, pa);
-      wave_sum3(c1, c2, g);
-      // wa = eta eA, wb = eta eB for every pair of the chunk at once (lane s holds pair s)
-      const float wav = fmaf(c1, neta, C0.era);
-      const float wbv = fmaf(fmaf(wav, g, C0.aa * c2), neta, C0.erb);
-      const float wa = rlf(wav, s), wb = rlf(wbv, s);
-      const float aa = rlf(C0.aa, s), ab = rlf(C0.ab, s), ba = rlf(C0.ba, s), bb = rlf(C0.bb, s);
-#pragma unroll
-      for (int e = 0; e < NV; ++e) {
-        const f2 q0 = q.v[e], a0 = pa.v[e], b0 = pb.v[e];
-        const f2 q1 = aa * q0 + wa * a0;
-        plA.v[e] = ba * a0 + wa * q0;
-        plB.v[e] = bb * b0 + wb * q1;
-        q.v[e] = ab * q1 + wb * b0;
-      }
-      st<KPL, UP>(urs, voff, osa, plA);
-      st<KPL, UP>(urs, voff, ob[slot], plB);
-      oa[slot] = noa;
-      ob[slot] = nob;
-      RA[slot] = ld<KPL, UP>(urs, voff, noa);
-      RB[slot] = ld<KPL, UP>(urs, voff, nob);
+    {  // experiment build: shader cycles spent waiting for this pair's prefetched user rows
+      const uint64_t a = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_s_waitcnt((4 * (DS - 1)) & 15 | (((4 * (DS - 1)) >> 4) << 14) | 0x0F70 & ~0xF);
+      wait_clk += __builtin_amdgcn_s_memtime() - a;
     }
-    C0 = chunk_convert(N, eta);
-  }
-run_done:
+#endif
+    // the ring's next offsets (pair s + DS), named up front
+    const uint32_t noa = s + DS < CH ? rl(C0.ua, s + DS) : rl(N.w0[0], s + DS - CH);
+    const uint32_t nob = s + DS < CH ? rl(C0.ub, s + DS) : rl(N.w0[1], s + DS - CH);
+    Row<KPL> pa;
+    uint32_t osa;
+    if constexpr (FWD) {
+      const uint32_t fl = rl(C0.flags, s);
+      osa = rl(C0.sa, s);
+      const float kfa = static_cast<float>(fl & 0xFFu), kfb = static_cast<float>((fl >> 8) & 0xFFu);
+#pragma unroll
+      for (int e = 0; e < NV; ++e) pa.v[e] = kfb * plB.v[e] + (kfa * plA.v[e] + RA[slot].v[e]);
+    } else {
+      osa = rl(C0.ua, s);
+      pa = RA[slot];
+    }
+    const Row<KPL> pb = RB[slot];
+    float c1 = dot_part<KPL>(pa, q), c2 = dot_part<KPL>(pb, q), g = dot_part<KPL>(pb, pa);
+    wave_sum3(c1, c2, g);
+    // wa = eta eA, wb = eta eB for every pair of the chunk at once (lane s holds pair s)
+    const float wav = fmaf(c1, neta, C0.era);
+    const float wbv = fmaf(fmaf(wav, g, C0.aa * c2), neta, C0.erb);
+    const float wa = rlf(wav, s), wb = rlf(wbv, s);
+    const float aa = rlf(C0.aa, s), ab = rlf(C0.ab, s), ba = rlf(C0.ba, s), bb = rlf(C0.bb, s);
+#pragma unroll
+    for (int e = 0; e < NV; ++e) {
+      const f2 q0 = q.v[e], a0 = pa.v[e], b0 = pb.v[e];
+      const f2 q1 = aa * q0 + wa * a0;
+      plA.v[e] = ba * a0 + wa * q0;
+      plB.v[e] = bb * b0 + wb * q1;
+      q.v[e] = ab * q1 + wb * b0;
+    }
+    st<KPL, UP>(urs, voff, osa, plA);
+    st<KPL, UP>(urs, voff, rl(C0.ub, s), plB);
+    RA[slot] = ld<KPL, UP>(urs, voff, noa);
+    RB[slot] = ld<KPL, UP>(urs, voff, nob);
+  };
+  sweep_chunks<kPairChunk>(npairs, pair, [&](int c) { N = chunk_load(RR, c + 1, vlane); },
+                           [&] { C0 = chunk_convert(N, eta); });
   keep_chunk(N);
   st<KPL, IP>(irs, voff, item_off, q);
 }
@@ -171,58 +164,49 @@ __device__ __forceinline__ void single_run_cell_k1(Chunk C0, __amdgpu_buffer_rsr
   const uint32_t item_off = rl(C0.ia, 0);
   float q = ld1<IP>(irs, voff, item_off);
   float RA[DS], RB[DS], plA = 0.f, plB = 0.f;
-  uint32_t oa[DS], ob[DS];
 #pragma unroll
   for (int s = 0; s < DS; ++s) {
-    oa[s] = rl(C0.ua, s);
-    ob[s] = rl(C0.ub, s);
-    RA[s] = ld1<UP>(urs, voff, oa[s]);
-    RB[s] = ld1<UP>(urs, voff, ob[s]);
+    RA[s] = ld1<UP>(urs, voff, rl(C0.ua, s));
+    RB[s] = ld1<UP>(urs, voff, rl(C0.ub, s));
   }
   drain_vmem();
   const float neta = vgpr_of(-eta);
-  ChunkRaw N{};  // the next chunk, loaded when the current one starts (keep_chunk)
-  for (int c = 0;; ++c) {
-#pragma unroll
-    for (int s = 0; s < CH; ++s) {
-      if (c * CH + s >= npairs) goto run_done;
-      if (s == 0) N = chunk_load(RR, c + 1, vlane);
-      const int slot = s % DS;
-      const uint32_t noa = s + DS < CH ? rl(C0.ua, s + DS) : rl(N.w0[0], s + DS - CH);
-      const uint32_t nob = s + DS < CH ? rl(C0.ub, s + DS) : rl(N.w0[1], s + DS - CH);
-      float pa;
-      uint32_t osa;
-      if constexpr (FWD) {
-        const uint32_t fl = rl(C0.flags, s);
-        osa = rl(C0.sa, s);
-        const float kfa = static_cast<float>(fl & 0xFFu), kfb = static_cast<float>((fl >> 8) & 0xFFu);
-        pa = kfb * plB + (kfa * plA + RA[slot]);
-      } else {
-        osa = oa[slot];
-        pa = RA[slot];
-      }
-      const float pb = RB[slot];
-      float c1 = pa * q, c2 = pb * q, g = pb * pa;
-      wave_sum3(c1, c2, g);
-      const float wav = fmaf(c1, neta, C0.era);
-      const float wbv = fmaf(fmaf(wav, g, C0.aa * c2), neta, C0.erb);
-      const float wa = rlf(wav, s), wb = rlf(wbv, s);
-      const float aa = rlf(C0.aa, s), ab = rlf(C0.ab, s), ba = rlf(C0.ba, s), bb = rlf(C0.bb, s);
-      const f2 A = pair_update(ba, aa, wa, pa, q);    // {plA, q1}
-      const f2 B = pair_update(bb, ab, wb, pb, A.y);  // {plB, q}
-      plA = A.x;
-      plB = B.x;
-      q = B.y;
-      st1<UP>(urs, voff, osa, plA);
-      st1<UP>(urs, voff, ob[slot], plB);
-      oa[slot] = noa;
-      ob[slot] = nob;
-      RA[slot] = ld1<UP>(urs, voff, noa);
-      RB[slot] = ld1<UP>(urs, voff, nob);
+  ChunkRaw N{};  // the next chunk (sweep_chunks loads it when the current one starts)
+  auto pair = [&](auto S) __attribute__((always_inline)) {
+    constexpr int s = decltype(S)::value;
+    const int slot = s % DS;
+    const uint32_t noa = s + DS < CH ? rl(C0.ua, s + DS) : rl(N.w0[0], s + DS - CH);
+    const uint32_t nob = s + DS < CH ? rl(C0.ub, s + DS) : rl(N.w0[1], s + DS - CH);
+    float pa;
+    uint32_t osa;
+    if constexpr (FWD) {
+      const uint32_t fl = rl(C0.flags, s);
+      osa = rl(C0.sa, s);
+      const float kfa = static_cast<float>(fl & 0xFFu), kfb = static_cast<float>((fl >> 8) & 0xFFu);
+      pa = kfb * plB + (kfa * plA + RA[slot]);
+    } else {
+      osa = rl(C0.ua, s);
+      pa = RA[slot];
     }
-    C0 = chunk_convert(N, eta);
-  }
-run_done:
+    const float pb = RB[slot];
+    float c1 = pa * q, c2 = pb * q, g = pb * pa;
+    wave_sum3(c1, c2, g);
+    const float wav = fmaf(c1, neta, C0.era);
+    const float wbv = fmaf(fmaf(wav, g, C0.aa * c2), neta, C0.erb);
+    const float wa = rlf(wav, s), wb = rlf(wbv, s);
+    const float aa = rlf(C0.aa, s), ab = rlf(C0.ab, s), ba = rlf(C0.ba, s), bb = rlf(C0.bb, s);
+    const f2 A = pair_update(ba, aa, wa, pa, q);    // {plA, q1}
+    const f2 B = pair_update(bb, ab, wb, pb, A.y);  // {plB, q}
+    plA = A.x;
+    plB = B.x;
+    q = B.y;
+    st1<UP>(urs, voff, osa, plA);
+    st1<UP>(urs, voff, rl(C0.ub, s), plB);
+    RA[slot] = ld1<UP>(urs, voff, noa);
+    RB[slot] = ld1<UP>(urs, voff, nob);
+  };
+  sweep_chunks<kPairChunk>(npairs, pair, [&](int c) { N = chunk_load(RR, c + 1, vlane); },
+                           [&] { C0 = chunk_convert(N, eta); });
   keep_chunk(N);
   st1<IP>(irs, voff, item_off, q);
 }
@@ -244,61 +228,54 @@ __device__ __forceinline__ void generic_cell_k1(Chunk C0, __amdgpu_buffer_rsrc_t
   drain_vmem();
   const float neta = vgpr_of(-eta);
   float q = 0.f;
-  ChunkRaw N{};  // the next chunk, loaded when the current one starts (keep_chunk)
-  for (int c = 0;; ++c) {
-#pragma unroll
-    for (int s = 0; s < CH; ++s) {
-      if (c * CH + s >= npairs) goto cell_done;
-      if (s == 0) N = chunk_load(RR, c + 1, vlane);
-      const int slot = s % D;
-      const uint32_t fl = rl(C0.flags, s);
-      const uint32_t osa = rl(C0.sa, s), osb = rl(C0.sb, s), osia = rl(C0.sia, s), osi = rl(C0.si, s);
-      const bool nin = s + D < CH;
-      const uint32_t nua = nin ? rl(C0.ua, s + D) : rl(N.w0[0], s + D - CH);
-      const uint32_t nub = nin ? rl(C0.ub, s + D) : rl(N.w0[1], s + D - CH);
-      const uint32_t nia = nin ? rl(C0.ia, s + D) : rl(N.w0[2], s + D - CH);
-      const uint32_t nib = nin ? rl(C0.ib, s + D) : rl(N.w0[3], s + D - CH);
-      const float kfa = static_cast<float>(fl & 0xFFu), kfb = static_cast<float>((fl >> 8) & 0xFFu);
-      const float kq = static_cast<float>((fl >> 16) & 0xFFu);
-      const float sr = rlf(C0.sr, s);
-      const float pa = kfb * plB + (kfa * plA + PA[slot]);  // loads of forwarded rows return 0
-      const float pb = PB[slot];
-      const float qa = kq * q + QA[slot];
-      const float qbd = sr * qa + QB[slot];  // B's item before A's update: q (run) or qB (split)
-      float c1 = pa * qa, c2 = pb * qbd, g = pb * pa;
-      wave_sum3(c1, c2, g);
-      const float wav = fmaf(c1, neta, C0.era);
-      const float wbv = fmaf(fmaf(C0.sr * wav, g, C0.m * c2), neta, C0.erb);
-      const float wa = rlf(wav, s), wb = rlf(wbv, s);
-      const float aa = rlf(C0.aa, s), ab = rlf(C0.ab, s), ba = rlf(C0.ba, s), bb = rlf(C0.bb, s);
-      const f2 A = pair_update(ba, aa, wa, pa, qa);  // {plA, q1}
-      const float qb0 = sr * A.y + QB[slot];
-      const f2 B = pair_update(bb, ab, wb, pb, qb0);  // {plB, q}
-      plA = A.x;
-      plB = B.x;
-      q = B.y;
-      st1<UP>(urs, voff, osa, plA);
-      st1<UP>(urs, voff, osb, plB);
-      st1<IP>(irs, voff, osia, A.y);
-      st1<IP>(irs, voff, osi, q);
-      PA[slot] = ld1<UP>(urs, voff, nua);
-      PB[slot] = ld1<UP>(urs, voff, nub);
-      QA[slot] = ld1<IP>(irs, voff, nia);
-      QB[slot] = ld1<IP>(irs, voff, nib);
-    }
-    C0 = chunk_convert(N, eta);
-  }
-cell_done:
+  ChunkRaw N{};  // the next chunk (sweep_chunks loads it when the current one starts)
+  auto pair = [&](auto S) __attribute__((always_inline)) {
+    constexpr int s = decltype(S)::value;
+    const int slot = s % D;
+    const uint32_t fl = rl(C0.flags, s);
+    const uint32_t osa = rl(C0.sa, s), osb = rl(C0.sb, s), osia = rl(C0.sia, s), osi = rl(C0.si, s);
+    const bool nin = s + D < CH;
+    const uint32_t nua = nin ? rl(C0.ua, s + D) : rl(N.w0[0], s + D - CH);
+    const uint32_t nub = nin ? rl(C0.ub, s + D) : rl(N.w0[1], s + D - CH);
+    const uint32_t nia = nin ? rl(C0.ia, s + D) : rl(N.w0[2], s + D - CH);
+    const uint32_t nib = nin ? rl(C0.ib, s + D) : rl(N.w0[3], s + D - CH);
+    const float kfa = static_cast<float>(fl & 0xFFu), kfb = static_cast<float>((fl >> 8) & 0xFFu);
+    const float kq = static_cast<float>((fl >> 16) & 0xFFu);
+    const float sr = rlf(C0.sr, s);
+    const float pa = kfb * plB + (kfa * plA + PA[slot]);  // loads of forwarded rows return 0
+    const float pb = PB[slot];
+    const float qa = kq * q + QA[slot];
+    const float qbd = sr * qa + QB[slot];  // B's item before A's update: q (run) or qB (split)
+    float c1 = pa * qa, c2 = pb * qbd, g = pb * pa;
+    wave_sum3(c1, c2, g);
+    const float wav = fmaf(c1, neta, C0.era);
+    const float wbv = fmaf(fmaf(C0.sr * wav, g, C0.m * c2), neta, C0.erb);
+    const float wa = rlf(wav, s), wb = rlf(wbv, s);
+    const float aa = rlf(C0.aa, s), ab = rlf(C0.ab, s), ba = rlf(C0.ba, s), bb = rlf(C0.bb, s);
+    const f2 A = pair_update(ba, aa, wa, pa, qa);  // {plA, q1}
+    const float qb0 = sr * A.y + QB[slot];
+    const f2 B = pair_update(bb, ab, wb, pb, qb0);  // {plB, q}
+    plA = A.x;
+    plB = B.x;
+    q = B.y;
+    st1<UP>(urs, voff, osa, plA);
+    st1<UP>(urs, voff, osb, plB);
+    st1<IP>(irs, voff, osia, A.y);
+    st1<IP>(irs, voff, osi, q);
+    PA[slot] = ld1<UP>(urs, voff, nua);
+    PB[slot] = ld1<UP>(urs, voff, nub);
+    QA[slot] = ld1<IP>(irs, voff, nia);
+    QB[slot] = ld1<IP>(irs, voff, nib);
+  };
+  sweep_chunks<kPairChunk>(npairs, pair, [&](int c) { N = chunk_load(RR, c + 1, vlane); },
+                           [&] { C0 = chunk_convert(N, eta); });
   keep_chunk(N);
 }
 
 // One cell (WaveDesc d) of the pair schedule, swept by the calling wave.  UP = cache policy of
 // the user-row loads and stores.  L0: the cell's first record chunk, loaded by the caller (the
-// systolic sweep loads it while the previous cell's stores drain).  Chunk c + 1 is loaded when
-// chunk c starts and converted when it ends: a record is first read 49 pairs after its load, and
-// no register the chunk boundary copies is a load still in flight.  (Carrying the raw next chunk
-// across the loop, loaded at the boundary, put a vmcnt(3) -- a whole memory round trip -- at
-// every 56-pair chunk boundary: the compiler copies the loop-carried registers at the header.)
+// systolic sweep loads it while the previous cell's stores drain); sweep_chunks (pair_device.hpp)
+// loads chunk c + 1 when chunk c starts.
 template <int KPL, int D, int UP, int IP = kItemPolicy>
 __device__ __forceinline__ void pair_cell(const WaveDesc d, const ChunkRaw& L0,
                                           const u4v* __restrict__ recs, __amdgpu_buffer_rsrc_t urs,
@@ -351,72 +328,68 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const ChunkRaw& L0,
 #pragma unroll
     for (int e = 0; e < NV; ++e) q.v[e] = f2{0.f, 0.f};
 
-    ChunkRaw N{};  // the next chunk, loaded when the current one starts (keep_chunk)
-    for (int c = 0;; ++c) {
-#pragma unroll
-      for (int s = 0; s < CH; ++s) {
-        if (c * CH + s >= npairs) goto cell_done;
-        if (s == 0) N = chunk_load(RR, c + 1, vlane);
-        const int slot = s % D;
+    ChunkRaw N{};  // the next chunk (sweep_chunks loads it when the current one starts)
+  auto pair = [&](auto S) __attribute__((always_inline)) {
+    constexpr int s = decltype(S)::value;
+      const int slot = s % D;
 #if defined(MFHIP_EXPERIMENTS) && defined(MFHIP_WAITPROBE)
-        {  // experiment build: shader cycles spent waiting for this pair's prefetched rows
-          const uint64_t a = __builtin_amdgcn_s_memtime();
-          __builtin_amdgcn_s_waitcnt((8 * (D - 1)) & 15 | (((8 * (D - 1)) >> 4) << 14) | 0x0F70 & ~0xF);
-          wait_clk += __builtin_amdgcn_s_memtime() - a;
-        }
-#endif
-        const uint32_t fl = rl(C0.flags, s);
-        // store offsets named up front: the scheduler then reads them early instead of right
-        // before each store (a v_readlane feeding a buffer store's soffset costs an s_nop 4)
-        const uint32_t osa = rl(C0.sa, s), osb = rl(C0.sb, s), osia = rl(C0.sia, s), osi = rl(C0.si, s);
-        const bool nin = s + D < CH;  // offsets of pair s + D (the ring's next rows)
-        const uint32_t nua = nin ? rl(C0.ua, s + D) : rl(N.w0[0], s + D - CH);
-        const uint32_t nub = nin ? rl(C0.ub, s + D) : rl(N.w0[1], s + D - CH);
-        const uint32_t nia = nin ? rl(C0.ia, s + D) : rl(N.w0[2], s + D - CH);
-        const uint32_t nib = nin ? rl(C0.ib, s + D) : rl(N.w0[3], s + D - CH);
-        // byte flags -> float coefficients (v_cvt_f32_ubyteN): forwarding, keep q, split
-        const float kfa = static_cast<float>(fl & 0xFFu), kfb = static_cast<float>((fl >> 8) & 0xFFu);
-        const float kq = static_cast<float>((fl >> 16) & 0xFFu);
-        const float sr = rlf(C0.sr, s);  // 1 - split, from the chunk (one readlane, no convert + subtract)
-        Row<KPL> pa, pb, qa, qbd;
-#pragma unroll
-        for (int e = 0; e < NV; ++e) {
-          pa.v[e] = kfb * plB.v[e] + (kfa * plA.v[e] + PA[slot].v[e]);  // loads of forwarded rows return 0
-          pb.v[e] = PB[slot].v[e];
-          qa.v[e] = kq * q.v[e] + QA[slot].v[e];
-          qbd.v[e] = sr * qa.v[e] + QB[slot].v[e];  // B's item before A's update: q (run) or qB (split)
-        }
-        float c1 = dot_part<KPL>(pa, qa), c2 = dot_part<KPL>(pb, qbd), g = dot_part<KPL>(pb, pa);
-        wave_sum3(c1, c2, g);
-        // wa = eta eA, wb = eta eB in the chunk layout (lane s = pair s); a split pair has no
-        // coupling to A's update (sr = 0, m = 1)
-        const float wav = fmaf(c1, neta, C0.era);
-        const float wbv = fmaf(fmaf(C0.sr * wav, g, C0.m * c2), neta, C0.erb);
-        const float wa = rlf(wav, s), wb = rlf(wbv, s);
-        const float aa = rlf(C0.aa, s), ab = rlf(C0.ab, s), ba = rlf(C0.ba, s), bb = rlf(C0.bb, s);
-        Row<KPL> q1;
-#pragma unroll
-        for (int e = 0; e < NV; ++e) {
-          const f2 q0 = qa.v[e], a0 = pa.v[e], b0 = pb.v[e];
-          q1.v[e] = aa * q0 + wa * a0;
-          plA.v[e] = ba * a0 + wa * q0;
-          const f2 qb0 = sr * q1.v[e] + QB[slot].v[e];
-          plB.v[e] = bb * b0 + wb * qb0;
-          q.v[e] = ab * qb0 + wb * b0;
-        }
-        st<KPL, UP>(urs, voff, osa, plA);
-        st<KPL, UP>(urs, voff, osb, plB);
-        st<KPL, IP>(irs, voff, osia, q1);
-        st<KPL, IP>(irs, voff, osi, q);
-        // rows of pair j+D (after this pair's stores)
-        PA[slot] = ld<KPL, UP>(urs, voff, nua);
-        PB[slot] = ld<KPL, UP>(urs, voff, nub);
-        QA[slot] = ld<KPL, IP>(irs, voff, nia);
-        QB[slot] = ld<KPL, IP>(irs, voff, nib);
+      {  // experiment build: shader cycles spent waiting for this pair's prefetched rows
+        const uint64_t a = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_s_waitcnt((8 * (D - 1)) & 15 | (((8 * (D - 1)) >> 4) << 14) | 0x0F70 & ~0xF);
+        wait_clk += __builtin_amdgcn_s_memtime() - a;
       }
-      C0 = chunk_convert(N, eta);
-    }
-  cell_done:
+#endif
+      const uint32_t fl = rl(C0.flags, s);
+      // store offsets named up front: the scheduler then reads them early instead of right
+      // before each store (a v_readlane feeding a buffer store's soffset costs an s_nop 4)
+      const uint32_t osa = rl(C0.sa, s), osb = rl(C0.sb, s), osia = rl(C0.sia, s), osi = rl(C0.si, s);
+      const bool nin = s + D < CH;  // offsets of pair s + D (the ring's next rows)
+      const uint32_t nua = nin ? rl(C0.ua, s + D) : rl(N.w0[0], s + D - CH);
+      const uint32_t nub = nin ? rl(C0.ub, s + D) : rl(N.w0[1], s + D - CH);
+      const uint32_t nia = nin ? rl(C0.ia, s + D) : rl(N.w0[2], s + D - CH);
+      const uint32_t nib = nin ? rl(C0.ib, s + D) : rl(N.w0[3], s + D - CH);
+      // byte flags -> float coefficients (v_cvt_f32_ubyteN): forwarding, keep q, split
+      const float kfa = static_cast<float>(fl & 0xFFu), kfb = static_cast<float>((fl >> 8) & 0xFFu);
+      const float kq = static_cast<float>((fl >> 16) & 0xFFu);
+      const float sr = rlf(C0.sr, s);  // 1 - split, from the chunk (one readlane, no convert + subtract)
+      Row<KPL> pa, pb, qa, qbd;
+#pragma unroll
+      for (int e = 0; e < NV; ++e) {
+        pa.v[e] = kfb * plB.v[e] + (kfa * plA.v[e] + PA[slot].v[e]);  // loads of forwarded rows return 0
+        pb.v[e] = PB[slot].v[e];
+        qa.v[e] = kq * q.v[e] + QA[slot].v[e];
+        qbd.v[e] = sr * qa.v[e] + QB[slot].v[e];  // B's item before A's update: q (run) or qB (split)
+      }
+      float c1 = dot_part<KPL>(pa, qa), c2 = dot_part<KPL>(pb, qbd), g = dot_part<KPL>(pb, pa);
+      wave_sum3(c1, c2, g);
+      // wa = eta eA, wb = eta eB in the chunk layout (lane s = pair s); a split pair has no
+      // coupling to A's update (sr = 0, m = 1)
+      const float wav = fmaf(c1, neta, C0.era);
+      const float wbv = fmaf(fmaf(C0.sr * wav, g, C0.m * c2), neta, C0.erb);
+      const float wa = rlf(wav, s), wb = rlf(wbv, s);
+      const float aa = rlf(C0.aa, s), ab = rlf(C0.ab, s), ba = rlf(C0.ba, s), bb = rlf(C0.bb, s);
+      Row<KPL> q1;
+#pragma unroll
+      for (int e = 0; e < NV; ++e) {
+        const f2 q0 = qa.v[e], a0 = pa.v[e], b0 = pb.v[e];
+        q1.v[e] = aa * q0 + wa * a0;
+        plA.v[e] = ba * a0 + wa * q0;
+        const f2 qb0 = sr * q1.v[e] + QB[slot].v[e];
+        plB.v[e] = bb * b0 + wb * qb0;
+        q.v[e] = ab * qb0 + wb * b0;
+      }
+      st<KPL, UP>(urs, voff, osa, plA);
+      st<KPL, UP>(urs, voff, osb, plB);
+      st<KPL, IP>(irs, voff, osia, q1);
+      st<KPL, IP>(irs, voff, osi, q);
+      // rows of pair j+D (after this pair's stores)
+      PA[slot] = ld<KPL, UP>(urs, voff, nua);
+      PB[slot] = ld<KPL, UP>(urs, voff, nub);
+      QA[slot] = ld<KPL, IP>(irs, voff, nia);
+      QB[slot] = ld<KPL, IP>(irs, voff, nib);
+  };
+  sweep_chunks<kPairChunk>(npairs, pair, [&](int c) { N = chunk_load(RR, c + 1, vlane); },
+                           [&] { C0 = chunk_convert(N, eta); });
     keep_chunk(N);
 #undef MF_PREFETCH
   }

@@ -1179,6 +1179,11 @@ void prepare_det_sweep(mf_ctx* ctx) {
   const uint64_t k8 = static_cast<uint64_t>(ctx->P.num_factors) * 8;
   if (static_cast<uint64_t>(ctx->U.rows()) * k8 >= 0xFFFFF000ull || static_cast<uint64_t>(ctx->I.rows()) * k8 >= 0xFFFFF000ull)
     return;  // the sweep addresses each f64 slab with 32-bit offsets
+  // k not a multiple of 64: lanes past k use voffset 0x80000000, and with the out-of-range row
+  // offset kOOB in soffset the 32-bit sum wraps to 0x7FFFF000 -- inside a slab of 2 GiB or more
+  if (ctx->P.num_factors % 64 != 0 &&
+      (static_cast<uint64_t>(ctx->U.rows()) * k8 >= 0x7FFFF000ull || static_cast<uint64_t>(ctx->I.rows()) * k8 >= 0x7FFFF000ull))
+    return;
   int32_t waves = std::max(1, cap / 2);
   if (const std::string v = test_knob("det_waves"); !v.empty()) waves = std::clamp(std::atoi(v.c_str()), 1, cap);
   const int32_t n = ctx->nb;

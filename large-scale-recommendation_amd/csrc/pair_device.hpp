@@ -188,6 +188,52 @@ __device__ __forceinline__ Chunk chunk_convert(const ChunkRaw& r, float eta) {
   return ch;
 }
 
+// Calls f(std::integral_constant<int, 0>{}) ... f(integral_constant<int, N - 1>{}) in order: the
+// pair index is a compile-time constant in every copy of the step (constant readlane lanes,
+// constant ring slots).  unroll_while stops after the first call that returns false.
+template <typename F, int... S>
+__device__ __forceinline__ void unroll_seq(F&& f, std::integer_sequence<int, S...>) {
+  (f(std::integral_constant<int, S>{}), ...);
+}
+template <typename F, int... S>
+__device__ __forceinline__ void unroll_while_seq(F&& f, std::integer_sequence<int, S...>) {
+  (void)(f(std::integral_constant<int, S>{}) && ...);
+}
+
+// The pairs of one cell, CH per record chunk: pair(integral_constant<int, s>) runs pair s of the
+// current chunk, load_next(c) loads chunk c + 1 when chunk c starts (a record is first read 49 pairs
+// later), advance() makes it current.  Full chunks run without exit tests and with a scheduling
+// barrier between pairs; only the last, partial chunk tests each pair.  (With a per-pair exit in
+// every chunk -- the natural loop -- the structurizer's flow blocks for 56 exits ran on the normal
+// path too and copied ring registers whose loads were still in flight: a vmcnt(3) wait, one memory
+// round trip, at every chunk boundary.  The barriers keep the scheduler from interleaving pairs of
+// the now branch-free chunk, which pulled later pairs' uses of just-loaded rows forward.)
+template <int CH, typename P, typename L, typename A>
+__device__ __forceinline__ void sweep_chunks(int npairs, P&& pair, L&& load_next, A&& advance) {
+  const int full = __builtin_amdgcn_readfirstlane(npairs / CH);
+  const int rem = __builtin_amdgcn_readfirstlane(npairs - full * CH);  // uniform: scalar tests
+  int c = 0;
+  for (; c < full; ++c) {
+    load_next(c);
+    unroll_seq(
+        [&](auto S) __attribute__((always_inline)) {
+          __builtin_amdgcn_sched_barrier(0);
+          pair(S);
+        },
+        std::make_integer_sequence<int, CH>{});
+    advance();
+  }
+  load_next(c);
+  unroll_while_seq(
+      [&](auto S) __attribute__((always_inline)) {
+        if (decltype(S)::value >= rem) return false;
+        __builtin_amdgcn_sched_barrier(0);
+        pair(S);
+        return true;
+      },
+      std::make_integer_sequence<int, CH>{});
+}
+
 // -eta in a VGPR: the per-pair scalar recurrence runs in the chunk layout (lane s = pair s), where
 // each step reads one SGPR (a wave sum) and takes -eta from a register, so no SGPR is copied to a
 // VGPR first (one SGPR per VALU instruction on gfx9).

@@ -77,8 +77,8 @@ def test_no_store_data_hazard_in_the_library(kern):
     assert not bad, bad[:5]
 
 
-@pytest.mark.parametrize("kernel_re,mode", ic.CHECKS)
-def test_flag_stores_wait_for_the_rows_they_publish(kern, kernel_re, mode):
-    bad, n = ic.flag_store_violations(kern, kernel_re, ic.progress_flag, mode)
+@pytest.mark.parametrize("kernel_re,mode,flag", ic.CHECKS)
+def test_flag_stores_wait_for_the_rows_they_publish(kern, kernel_re, mode, flag):
+    bad, n = ic.flag_store_violations(kern, kernel_re, flag, mode)
     assert n > 0, f"no flag store found in {kernel_re}"
     assert not bad, bad[:5]

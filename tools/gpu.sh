@@ -38,10 +38,11 @@ r = d.get("roofline") or {}
 det = d.get("deterministic") or {}
 on = d.get("online") or {}
 s = f"{d['config']['workload']}: {d['value']/1e9:.3f} Gups {d['ms_per_step']} ms/step rmse {d.get('rmse')} rel {d.get('rmse_rel')}"
-if r: s += f" | launch {r.get('avg_launch_us')} us frac {r.get('frac')} traffic_frac {r.get('traffic_frac')}"
+if r: s += f" | launch {r.get('avg_launch_us')} us frac {r.get('frac')} requested {r.get('requested_frac')} traffic_frac {r.get('traffic_frac')}"
 if det: s += f" | det {det['value']/1e6:.1f} Mups {det['ms_per_step']} ms eq {det.get('rmse_equal_to_ref')} launch {det.get('avg_launch_us')} us cold {det.get('cold_fit_s')}"
 for key, v in on.items():
-    s += f" | online {key} {v['value']/1e6:.1f} M/s kernel {v.get('kernel_ms_median')} ms"
+    ro = v.get("roofline") or {}
+    s += f" | online {key} {v['value']/1e6:.1f} M/s kernel {v.get('kernel_ms_median')} ms frac {ro.get('frac')} alg {ro.get('algorithmic_frac')}"
 print(s)
 EOF
 }

@@ -334,13 +334,18 @@ def progress_flag(x):
     return x.mn == "global_store_dword" and " sc1" in f" {x.ops}"
 
 
+def buffer_ticket(x):
+    """k_det_sweep2's tickets: one-dword sc1 buffer stores (its f64 rows are dwordx2)."""
+    return x.mn == "buffer_store_dword" and " sc1" in f" {x.ops}"
+
+
 CHECKS = [
-    # (kernel regex, mode): the systolic sweep publishes a cell only after ALL its stores landed; the
-    # det sweep publishes entry j-2's ticket at entry j (entry j-1's stores may fly)
-    (r"k_sweep_pair_sys", "all"),
-    (r"k_det_sweep2", "prev"),
-    (r"k_online_sweepId", "prev"),
-    (r"k_online_f32", "prev"),
+    # (kernel regex, mode, flag predicate): the systolic sweep publishes a cell only after ALL its
+    # stores landed; the ticket sweeps publish update j-2's ticket at update j (j-1's stores may fly)
+    (r"k_sweep_pair_sys", "all", progress_flag),
+    (r"k_det_sweep2", "prev", buffer_ticket),
+    (r"k_online_sweepId", "prev", progress_flag),
+    (r"k_online_f32", "prev", progress_flag),
 ]
 
 
@@ -353,8 +358,8 @@ def main():
     print(f"{len(kern)} kernels")
     for h in store_hazards(kern, a.ws):
         print("STORE-DATA HAZARD", h)
-    for rx, mode in CHECKS:
-        bad, n = flag_store_violations(kern, rx, progress_flag, mode)
+    for rx, mode, flag in CHECKS:
+        bad, n = flag_store_violations(kern, rx, flag, mode)
         print(f"{rx}: {n} flag stores checked, {len(bad)} violations")
         for b in bad[:10]:
             print("  ", b)
