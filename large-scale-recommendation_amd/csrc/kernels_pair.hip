@@ -101,7 +101,7 @@ __device__ __forceinline__ void single_run_cell(Chunk C0, __amdgpu_buffer_rsrc_t
       osa = rl(C0.sa, s);
       const float kfa = static_cast<float>(fl & 0xFFu), kfb = static_cast<float>((fl >> 8) & 0xFFu);
 #pragma unroll
-      for (int e = 0; e < NV; ++e) pa.v[e] = kfb * plB.v[e] + (kfa * plA.v[e] + RA[slot].v[e]);
+      for (int e = 0; e < NV; ++e) pa.v[e] = vfma(kfb, plB.v[e], vfma(kfa, plA.v[e], RA[slot].v[e]));
     } else {
       osa = rl(C0.ua, s);
       pa = RA[slot];
@@ -117,10 +117,10 @@ __device__ __forceinline__ void single_run_cell(Chunk C0, __amdgpu_buffer_rsrc_t
 #pragma unroll
     for (int e = 0; e < NV; ++e) {
       const f2 q0 = q.v[e], a0 = pa.v[e], b0 = pb.v[e];
-      const f2 q1 = aa * q0 + wa * a0;
-      plA.v[e] = ba * a0 + wa * q0;
-      plB.v[e] = bb * b0 + wb * q1;
-      q.v[e] = ab * q1 + wb * b0;
+      const f2 q1 = vfma(wa, a0, aa * q0);
+      plA.v[e] = vfma(wa, q0, ba * a0);
+      plB.v[e] = vfma(wb, q1, bb * b0);
+      q.v[e] = vfma(wb, b0, ab * q1);
     }
     st<KPL, UP>(urs, voff, osa, plA);
     st<KPL, UP>(urs, voff, rl(C0.ub, s), plB);
@@ -355,10 +355,10 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const ChunkRaw& L0,
       Row<KPL> pa, pb, qa, qbd;
 #pragma unroll
       for (int e = 0; e < NV; ++e) {
-        pa.v[e] = kfb * plB.v[e] + (kfa * plA.v[e] + PA[slot].v[e]);  // loads of forwarded rows return 0
+        pa.v[e] = vfma(kfb, plB.v[e], vfma(kfa, plA.v[e], PA[slot].v[e]));  // loads of forwarded rows return 0
         pb.v[e] = PB[slot].v[e];
-        qa.v[e] = kq * q.v[e] + QA[slot].v[e];
-        qbd.v[e] = sr * qa.v[e] + QB[slot].v[e];  // B's item before A's update: q (run) or qB (split)
+        qa.v[e] = vfma(kq, q.v[e], QA[slot].v[e]);
+        qbd.v[e] = vfma(sr, qa.v[e], QB[slot].v[e]);  // B's item before A's update: q (run) or qB (split)
       }
       float c1 = dot_part<KPL>(pa, qa), c2 = dot_part<KPL>(pb, qbd), g = dot_part<KPL>(pb, pa);
       wave_sum3(c1, c2, g);
@@ -372,11 +372,11 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const ChunkRaw& L0,
 #pragma unroll
       for (int e = 0; e < NV; ++e) {
         const f2 q0 = qa.v[e], a0 = pa.v[e], b0 = pb.v[e];
-        q1.v[e] = aa * q0 + wa * a0;
-        plA.v[e] = ba * a0 + wa * q0;
-        const f2 qb0 = sr * q1.v[e] + QB[slot].v[e];
-        plB.v[e] = bb * b0 + wb * qb0;
-        q.v[e] = ab * qb0 + wb * b0;
+        q1.v[e] = vfma(wa, a0, aa * q0);
+        plA.v[e] = vfma(wa, q0, ba * a0);
+        const f2 qb0 = vfma(sr, q1.v[e], QB[slot].v[e]);
+        plB.v[e] = vfma(wb, qb0, bb * b0);
+        q.v[e] = vfma(wb, b0, ab * qb0);
       }
       st<KPL, UP>(urs, voff, osa, plA);
       st<KPL, UP>(urs, voff, osb, plB);

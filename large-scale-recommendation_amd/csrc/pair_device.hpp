@@ -109,6 +109,10 @@ __device__ __forceinline__ void st(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uin
   }
 }
 
+// s * x + y as one packed fused multiply-add (v_pk_fma_f32): the compiler does not contract a
+// scalar-times-vector product into the add by itself (it emitted v_pk_mul + v_pk_add)
+__device__ __forceinline__ f2 vfma(float s, f2 x, f2 y) { return __builtin_elementwise_fma(f2{s, s}, x, y); }
+
 template <int KPL>
 __device__ __forceinline__ float dot_part(const Row<KPL>& a, const Row<KPL>& b) {
   f2 acc = a.v[0] * b.v[0];
