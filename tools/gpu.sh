@@ -11,7 +11,8 @@
 #   bench:<tag>:<bench.py args>            one bench line -> <tag>.json, summary printed
 #   ab:<tag>:<reps>:<envA>|<envB>[|...]:<bench.py args>
 #                                          alternating A/B of environment settings on the bench line
-#   prof:<tag>:<kernel>:<cfg>:<mode>:<rank>:<bench.py args>
+#   prof:<tag>:<kernel>:<cfg>:<mode>:<rank>:<bench.py args>   (<kernel> may be k1=sfx1,k2=sfx2,...:
+#                                          one traffic_<cfg>_<sfx>.json per kernel of the same run)
 #                                          rocprofv3 --kernel-trace --stats, then separate --pmc FETCH_SIZE
 #                                          and --pmc WRITE_SIZE passes, summarised per launch of <kernel>
 #                                          (tools/pmc_summary.py) -> traffic_<tag>.json, stats_<tag>.csv
@@ -90,11 +91,18 @@ for step in "$@"; do
       cd "$R"
       stats=$(ls "$O"/kt_$tag/*kernel_stats.csv | head -1)
       cp "$stats" "$O/stats_$tag.csv"
-      python3 tools/pmc_summary.py --stats "$stats" --fetch $(ls "$O"/fetch_$tag/*counter_collection.csv | head -1) \
-        --write $(ls "$O"/write_$tag/*counter_collection.csv | head -1) --kernel "$kern" --config "$cfg" --mode "$mode" \
-        --rank "$rank" --out "$O/traffic_$tag.json" > /dev/null || { echo "pmc summary $tag failed"; exit 1; }
+      # <kernel> may list several kernels of the same run, kernel=suffix,...: each is summarised to
+      # traffic_<cfg>_<suffix>.json (mode = suffix); a bare kernel name writes traffic_<tag>.json
+      IFS=',' read -ra KS <<< "$kern"
+      for ks in "${KS[@]}"; do
+        kn=${ks%%=*}; sfx=${ks#*=}
+        if [ "$sfx" = "$ks" ]; then out="$O/traffic_$tag.json"; md=$mode; else out="$O/traffic_${cfg}_$sfx.json"; md=$sfx; fi
+        python3 tools/pmc_summary.py --stats "$stats" --fetch $(ls "$O"/fetch_$tag/*counter_collection.csv | head -1) \
+          --write $(ls "$O"/write_$tag/*counter_collection.csv | head -1) --kernel "$kn" --config "$cfg" --mode "$md" \
+          --rank "$rank" --out "$out" > /dev/null || { echo "pmc summary $tag $kn failed"; exit 1; }
+        echo "traffic $kn: $(tr -d '\n ' < "$out" | cut -c1-260)"
+      done
       rm -rf "$O/fetch_$tag" "$O/write_$tag"
-      echo "traffic $tag: $(tr -d '\n ' < "$O/traffic_$tag.json" | cut -c1-260)"
       head -6 "$O/stats_$tag.csv" | cut -c1-150 ;;
     pmc)
       IFS=':' read -r tag ctrs args <<< "$rest"
