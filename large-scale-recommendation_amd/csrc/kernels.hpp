@@ -115,6 +115,17 @@ void launch_det_sweep(hipStream_t st, const DetWave* waves, int nw, const uint32
                       const double* regU, const double* regI, int k, double eta, int32_t* ticket,
                       int32_t* dummy_ticket, int32_t* err, hipEvent_t ev0, hipEvent_t ev1);
 
+// Split single-item chains (k = 64, 128, 256; kernels_detsweep.hip k_det_sweep_split): blocks of
+// two wave slots, slots[2b + w] for wave w (nslots even, nslots / 2 blocks, all resident at once:
+// nslots <= det_split_capacity(k), counted in wave slots; 0 = k not supported).  A block whose
+// slot 0 is a single-item wave runs it as a chain wave plus a helper wave (slot 1 ignored, by
+// convention kDetWaveHelper); any other slot is an ordinary k_det_sweep2 wave (count 0: none).
+int det_split_capacity(int k);
+void launch_det_sweep_split(hipStream_t st, const DetWave* slots, int nslots, const uint32_t* eu, const uint32_t* ei,
+                            const uint32_t* eq, const double* er, double* U, double* I, uint64_t u_bytes,
+                            uint64_t i_bytes, const double* regU, const double* regI, int k, double eta,
+                            int32_t* ticket, int32_t* err, hipEvent_t ev0, hipEvent_t ev1);
+
 // Gather-dot over resolved pairs (row -1 = unknown id).  out[j] = p.q summed left to right in
 // f64 (predictRating's ddot).  When r != nullptr every workgroup writes partials[3*wg + c]:
 //   c=0: sum (r - p.q)^2, c=1: matched count, c=2: sum mult*((r-p.q)^2 + lambda*(p.p + q.q)).

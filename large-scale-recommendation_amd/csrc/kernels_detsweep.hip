@@ -153,11 +153,10 @@ __device__ __forceinline__ void det_wave(const DetWave d, const uint32_t* __rest
                                          const uint32_t* __restrict__ eq, const double* __restrict__ er, double* U,
                                          double* I, uint64_t u_bytes, uint64_t i_bytes, const double* __restrict__ regU,
                                          const double* __restrict__ regI, int k, double eta, int32_t* ticket,
-                                         int32_t* dummy_ticket, int32_t* err, double* lds) {
+                                         int32_t* dummy_ticket, int32_t* err, double* lds, int lane) {
   constexpr int CH = kDetChunk;
   constexpr int NW = SINGLE ? 3 * KPL + 5 : 6 * KPL + 7;
   static_assert(NW < 64, "vmcnt range");
-  const int lane = threadIdx.x;
   const int32_t cnt = d.count;  // 32-bit: the entry tests are scalar compares, not 64-bit VALU ones
   const __amdgpu_buffer_rsrc_t urs = raw_rsrc(U, u_bytes), irs = raw_rsrc(I, i_bytes);
   const __amdgpu_buffer_rsrc_t trs = raw_rsrc(ticket, 0xFFFFF000ull);  // offsets are user rows * 4
@@ -308,6 +307,359 @@ done:
 #endif
 }
 
+// ---------------------------------------------------------------------------------------------
+// Split single-item chains (k == 64 KPL).  A single wave issues at most one instruction every
+// ~4 shader cycles whatever its kind (profiles/r05_fold_fill_microbench.txt: one VALU, readlane,
+// permlane or mov between two fold steps adds 4.0 cycles), so an update costs ~4 cycles per
+// instruction of the wave that runs it: the 128-step fold (512 cycles at k = 128) plus ~170 more
+// instructions of loads, ticket logic, the user-row update and stores -- ~1250 cycles, 521 ns per
+// update of the hottest item's chain, which bounds the superstep.  The chain itself needs only the
+// fold, e, the item-row update and the next products.  So a single-item wave is a pair of waves
+// of one workgroup:
+//   * the CHAIN wave (det_chain) runs the item recurrence -- products, fold, e = r - dot, the item
+//     row update (DSGDforMF.scala:405, :409-410) -- and nothing else: its operands arrive in LDS;
+//   * the HELPER wave (det_helper) does everything around it: entry fields, ticket polls, user-row
+//     loads (issued kLinkLA entries ahead), the LDS hand-over, the user-row update (:407-408) with
+//     the e the chain wave publishes in LDS, the stores, the tickets, and the item row at the end.
+//     It repeats the item-row update itself (the same operations on the same bits, so its copy of
+//     q is bitwise the chain wave's) rather than receiving q through LDS.
+// LDS link, slot j % kLinkR per entry j (every array per lane, so no access conflicts):
+//   helper -> chain: p (the user row), r, ru, then tag = j (the slot is filled);
+//   chain -> helper: e (the error), then done = j + 1 (entries finished).
+// LDS operations of one wave execute in order, so a reader that sees tag / done also sees the
+// data written before it; volatile accesses keep the compiler from reordering them.
+// Slot reuse: the helper refills slot j % R with entry j + R only after done > j (the chain has
+// read everything of entry j), and the chain overwrites e of slot j % R at entry j + R, which needs
+// entry j + R's tag, written after the helper read e_j.  No deadlock: the helper blocks on a ticket
+// only for the entry it is about to finish (every earlier entry published first), as det_wave does.
+constexpr int kLinkR = 4;   // LDS slots
+constexpr int kLinkLA = 6;  // helper: user rows loaded this many entries before their LDS hand-over
+constexpr int kLinkD = kLinkR + kLinkLA;  // load distance (entries)
+constexpr int kLinkRing = 8;              // register slots of loaded rows (>= kLinkLA, divides kDetChunk)
+static_assert(kDetChunk % kLinkRing == 0 && kLinkRing >= kLinkLA && kDetChunk % kLinkR == 0, "link ring sizes");
+static_assert(kLinkD + 2 < 2 * kDetChunk, "fields of entry j + D + 2 must be in the two chunks");
+
+// Per lane: its KPL row elements contiguous (ds_read/write_b128 at KPL >= 2), {r, ru} as one 16-B
+// word; e, tag and done one word each.
+template <int KPL>
+struct DetLink {
+  double p[kLinkR][64][KPL];
+  double rr[kLinkR][64][2];  // {r, ru}
+  double e[kLinkR][64];
+  int32_t tag[kLinkR][64];
+  int32_t done[64];
+};
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+// volatile LDS pointers (address space 3: ds_read / ds_write; through a generic pointer a volatile
+// access becomes a flat access that waits for vmcnt and lgkmcnt both)
+#define MFHIP_LDS(T) __attribute__((address_space(3))) volatile T
+template <typename T>
+__device__ __forceinline__ MFHIP_LDS(T) * lds(T* p) {
+  return (MFHIP_LDS(T)*)p;
+}
+template <int KPL>
+__device__ __forceinline__ void link_put_row(MFHIP_LDS(double) * at, const double (&v)[KPL]) {
+  if constexpr (KPL == 1) {
+    at[0] = v[0];
+  } else {
+#pragma unroll
+    for (int c = 0; c < KPL; c += 2) ((MFHIP_LDS(dbl2)*)at)[c / 2] = dbl2{v[c], v[c + 1]};
+  }
+}
+template <int KPL>
+__device__ __forceinline__ void link_get_row(MFHIP_LDS(double) * at, double (&v)[KPL]) {
+  if constexpr (KPL == 1) {
+    v[0] = at[0];
+  } else {
+#pragma unroll
+    for (int c = 0; c < KPL; c += 2) {
+      const dbl2 x = ((MFHIP_LDS(dbl2)*)at)[c / 2];
+      v[c] = x.x;
+      v[c + 1] = x.y;
+    }
+  }
+}
+
+template <typename F>
+__device__ __forceinline__ void link_wait(F v, int32_t want, int32_t* err, int lane) {
+  uint32_t n = 0;
+  while (__builtin_amdgcn_readfirstlane(v()) < want) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++n > (1u << 22)) {
+      if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // the flag store is not a row store a ticket publishes
+      break;
+    }
+  }
+}
+
+template <int KPL>
+__device__ __forceinline__ void det_chain(const DetWave d, const uint32_t* __restrict__ ei, const double* I,
+                                          uint64_t i_bytes, const double* __restrict__ regI, double eta,
+                                          DetLink<KPL>& L, int32_t* err, int lane) {
+  const int32_t cnt = d.count;
+  const __amdgpu_buffer_rsrc_t irs = raw_rsrc(I, i_bytes);
+  const __amdgpu_buffer_rsrc_t ris = raw_rsrc(regI, 0xFFFFF000ull);
+  uint32_t voff[KPL];
+#pragma unroll
+  for (int c = 0; c < KPL; ++c) voff[c] = static_cast<uint32_t>(lane + 64 * c) * 8u;
+  const uint32_t item = __builtin_amdgcn_readfirstlane(ei[d.begin]);
+  const DRow<KPL> Q0 = ldrow<KPL>(irs, voff, item * (64u * KPL * 8u));
+  const double ri = uniform(ld_reg(ris, item));
+  double q[KPL];
+#pragma unroll
+  for (int c = 0; c < KPL; ++c) q[c] = Q0.v[c];
+  MFHIP_LDS(int32_t)* tag = lds(&L.tag[0][0]);
+  MFHIP_LDS(double)* lp = lds(&L.p[0][0][0]);
+  MFHIP_LDS(double)* lrr = lds(&L.rr[0][0][0]);
+  MFHIP_LDS(double)* le = lds(&L.e[0][0]);
+  MFHIP_LDS(int32_t)* ldone = lds(&L.done[0]);
+  double P[2][KPL], R[2];
+  auto get = [&](int s, int sl) {  // slot sl's row and r into register slot s
+    link_get_row<KPL>(lp + (sl * 64 + lane) * KPL, P[s]);
+    R[s] = lrr[(sl * 64 + lane) * 2];
+  };
+  // entry m's operands from its slot (after its tag)
+  auto fetch = [&](int s, int32_t m) {
+    const int sl = m % kLinkR;
+    link_wait([&] { return tag[sl * 64 + lane]; }, m, err, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    get(s, sl);
+  };
+  // per register slot: an entry whose operands have to be read again when it starts (-1: none;
+  // its slot was not filled yet when entry j - 2 ended -- rare).  Only the entry about to run may
+  // block: the helper hands entry j over at the latest when it has finished entry j - 1.  A slot is
+  // read right after its tag, unconditionally (the reads execute after the tag read, in order, so
+  // they see the row whenever the tag did; stale data is read again).
+  int32_t want[2] = {-1, -1};
+  fetch(0, 0);
+  {
+    const int32_t t1 = tag[1 * 64 + lane];
+    get(1, 1);
+    if (cnt > 1 && __builtin_amdgcn_readfirstlane(t1) < 1) want[1] = 1;
+  }
+  auto entry = [&](const int s, const int32_t j) {
+    if (want[s] == j) fetch(s, j);
+    double pr[KPL];
+#pragma unroll
+    for (int c = 0; c < KPL; ++c) pr[c] = P[s][c] * q[c];
+    const int sl2 = (j + 2) % kLinkR;
+    const int32_t t2 = tag[sl2 * 64 + lane];  // read before the fold, tested after it
+    const double dot = seq_fold_dpp<double, KPL>(pr);
+    const double e = R[s] - dot;  // :405
+#pragma unroll
+    for (int c = 0; c < KPL; ++c) q[c] = q[c] - eta * (ri * q[c] - e * P[s][c]);  // :409-410
+    le[(j % kLinkR) * 64 + lane] = e;
+    ldone[lane] = j + 1;
+    // entry j + 2's operands into this register slot
+    get(s, sl2);
+    want[s] = (j + 2 < cnt && __builtin_amdgcn_readfirstlane(t2) < j + 2) ? j + 2 : -1;
+  };
+  for (int32_t c0 = 0;; c0 += 4) {
+    if (c0 + 4 <= cnt) {
+      entry(0, c0);
+      entry(1, c0 + 1);
+      entry(0, c0 + 2);
+      entry(1, c0 + 3);
+    } else {
+      if (c0 < cnt) entry(0, c0);
+      if (c0 + 1 < cnt) entry(1, c0 + 1);
+      if (c0 + 2 < cnt) entry(0, c0 + 2);
+      break;
+    }
+  }
+}
+
+template <int KPL>
+__device__ __forceinline__ void det_helper(const DetWave d, const uint32_t* __restrict__ eu, const uint32_t* __restrict__ ei,
+                                           const uint32_t* __restrict__ eq, const double* __restrict__ er, double* U,
+                                           double* I, uint64_t u_bytes, uint64_t i_bytes,
+                                           const double* __restrict__ regU, const double* __restrict__ regI,
+                                           double eta, int32_t* ticket, DetLink<KPL>& L, int32_t* err, int lane) {
+  constexpr int CH = kDetChunk, R = kLinkR, D = kLinkD, RING = kLinkRing;
+  // vector-memory operations per entry, in issue order (the wait before a ticket is published
+  // counts on them -- change the entry, change NW):
+  //   publish 1 | user store KPL | user load KPL, ru 1 | poll 1
+  // NW = the operations issued after entry j-2's stores up to entry j's publish: entry j-2's loads
+  // and poll, all of entry j-1's: (KPL + 2) + (2 KPL + 3).
+  constexpr int NW = 3 * KPL + 5;
+  static_assert(NW < 64, "vmcnt range");
+  const int32_t cnt = d.count;
+  const __amdgpu_buffer_rsrc_t urs = raw_rsrc(U, u_bytes), irs = raw_rsrc(I, i_bytes);
+  const __amdgpu_buffer_rsrc_t trs = raw_rsrc(ticket, 0xFFFFF000ull);
+  const __amdgpu_buffer_rsrc_t rus = raw_rsrc(regU, 0xFFFFF000ull), ris = raw_rsrc(regI, 0xFFFFF000ull);
+  uint32_t voff[KPL];
+#pragma unroll
+  for (int c = 0; c < KPL; ++c) voff[c] = static_cast<uint32_t>(lane + 64 * c) * 8u;
+  constexpr uint32_t rowb = 64u * KPL * 8u;
+  auto chunk = [&](int64_t c) { return det_chunk(eu, ei, eq, er, d.begin + c * CH + (lane & (CH - 1))); };
+  DetChunk C0 = chunk(0), C1 = chunk(1);
+  auto fu = [&](int s) { return s < CH ? rl(C0.u, s) : rl(C1.u, s - CH); };
+  auto fq = [&](int s) { return s < CH ? rl(C0.q, s) : rl(C1.q, s - CH); };
+  auto fr = [&](int s) { return rld(s < CH ? C0.r : C1.r, s < CH ? s : s - CH); };
+  const uint32_t item = rl(C0.i, 0);
+  const DRow<KPL> Q0 = ldrow<KPL>(irs, voff, item * rowb);
+  const double ri = uniform(ld_reg(ris, item));
+  double q[KPL];
+#pragma unroll
+  for (int c = 0; c < KPL; ++c) q[c] = Q0.v[c];
+  MFHIP_LDS(int32_t)* tag = lds(&L.tag[0][0]);
+  MFHIP_LDS(double)* lp = lds(&L.p[0][0][0]);
+  MFHIP_LDS(double)* lrr = lds(&L.rr[0][0][0]);
+  MFHIP_LDS(double)* le = lds(&L.e[0][0]);
+  MFHIP_LDS(int32_t)* ldone = lds(&L.done[0]);
+  auto put = [&](int32_t m, const double (&p)[KPL], double r, double ru) {  // entry m into its slot
+    const int sl = m % R;
+    link_put_row<KPL>(lp + (sl * 64 + lane) * KPL, p);
+    ((MFHIP_LDS(dbl2)*)lrr)[sl * 64 + lane] = dbl2{r, ru};
+    tag[sl * 64 + lane] = m;  // last: the slot is filled
+  };
+  double PR[RING][KPL], RU[RING];  // loaded user rows of entries j + R .. j + D - 1 (slot m % RING)
+  uint32_t okR = 0;                // bit m % RING: entry m's row was loaded (its ticket was ready)
+  uint32_t later = 0;              // bit m % R: entry m is not in its slot yet (handed over when it runs)
+  int32_t tk[2];                   // polls of entries j + D and j + D + 1
+  // prologue (entries 0 .. D-1): rows of entries with a ready ticket; 0 .. R-1 go to their slots
+  for (int x = 0; x < D; ++x) {
+    const bool live = x < cnt;
+    const uint32_t u = fu(x);
+    const bool ok = live && poll(trs, u * 4u) == static_cast<int32_t>(fq(x) & kDetUseqMask);
+    const DRow<KPL> p = ldrow<KPL>(urs, voff, ok ? u * rowb : kOOB);
+    const double ru = ld_reg(rus, live ? u : 0u);
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    if (x < R) {
+      if (ok) put(x, p.v, fr(x), ru);
+      else if (live) later |= 1u << (x % R);
+    } else {
+#pragma unroll
+      for (int c = 0; c < KPL; ++c) PR[x % RING][c] = p.v[c];
+      RU[x % RING] = ru;
+      if (ok) okR |= 1u << (x % RING);
+    }
+  }
+#pragma unroll
+  for (int x = 0; x < 2; ++x) tk[x] = poll_issue(trs, D + x < cnt ? fu(D + x) * 4u : kOOB);
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  uint32_t pend0 = kOOB, pend1 = kOOB;  // entries j-2 / j-1: ticket word byte offsets (kOOB: none)
+  int32_t pv0 = 0, pv1 = 0;
+  auto entry = [&](const int s, const int32_t j) {
+    const uint32_t u = fu(s), qf = fq(s);
+    const int32_t useq = static_cast<int32_t>(qf & kDetUseqMask);
+    // a. entry j's row when its ticket was not ready in time: publish every pending ticket
+    //    (after its stores), wait for ours, hand the row over now
+    if (later & (1u << (j % R))) {
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+      publish(trs, pend0, pv0);
+      publish(trs, pend1, pv1);
+      pend0 = pend1 = kOOB;
+      wait_ticket_or_fail(ticket + u, useq, err, lane);
+      const DRow<KPL> p = ldrow<KPL>(urs, voff, u * rowb);
+      const double ru = ld_reg(rus, u);
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+      put(j, p.v, fr(s), ru);
+      later &= ~(1u << (j % R));
+    }
+    // b. the chain wave's e of entry j
+    link_wait([&] { return ldone[lane]; }, j + 1, err, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    const int sl = j % R;
+    const double e = le[sl * 64 + lane];
+    const double ru = lrr[(sl * 64 + lane) * 2 + 1];
+    double p[KPL], pn[KPL];
+    link_get_row<KPL>(lp + (sl * 64 + lane) * KPL, p);
+    // c. the user row (:407-408) and this wave's copy of the item row (:409-410, old p)
+#pragma unroll
+    for (int c = 0; c < KPL; ++c) {
+      pn[c] = p[c] - eta * (ru * p[c] - e * q[c]);
+      q[c] = q[c] - eta * (ri * q[c] - e * p[c]);
+    }
+    // d. entry j-2's stores have landed: publish its ticket; entry j's stores
+    wait_vmcnt<NW>();
+    publish(trs, pend0, pv0);
+    pend0 = pend1;
+    pv0 = pv1;
+    pend1 = u * 4u;
+    pv1 = useq + 1;
+    strow<KPL>(urs, voff, u * rowb, pn);
+    // e. entry j + R into slot j % R (the chain wave is done with entry j)
+    const int32_t m = j + R;
+    if (m < cnt) {
+      if (okR & (1u << (m % RING))) put(m, PR[m % RING], fr(s + R), RU[m % RING]);
+      else later |= 1u << (m % R);
+    }
+    // f. load entry j + D's row if its ticket (polled two entries ago) is ready
+    const int32_t m2 = j + D;
+    const bool ok2 = m2 < cnt && __builtin_amdgcn_readfirstlane(tk[j & 1]) == static_cast<int32_t>(fq(s + D) & kDetUseqMask);
+    const uint32_t u2 = fu(s + D);
+    const DRow<KPL> p2 = ldrow<KPL>(urs, voff, ok2 ? u2 * rowb : kOOB);
+#pragma unroll
+    for (int c = 0; c < KPL; ++c) PR[m2 % RING][c] = p2.v[c];
+    RU[m2 % RING] = ld_reg(rus, m2 < cnt ? u2 : 0u);
+    okR = ok2 ? (okR | (1u << (m2 % RING))) : (okR & ~(1u << (m2 % RING)));
+    // g. poll entry j + D + 2's ticket
+    tk[j & 1] = poll_issue(trs, m2 + 2 < cnt ? fu(s + D + 2) * 4u : kOOB);
+  };
+  for (int32_t c0 = 0;; c0 += CH) {
+    if (c0 + CH <= cnt) {
+#pragma unroll
+      for (int s = 0; s < CH; ++s) entry(s, c0 + s);
+    } else {
+#pragma unroll
+      for (int s = 0; s < CH; ++s) {
+        if (c0 + s >= cnt) goto done;
+        entry(s, c0 + s);
+      }
+    }
+    C0 = C1;
+    C1 = chunk(c0 / CH + 2);
+  }
+done:
+  // the loads of the last entries' look-ahead (rows, lambda/omega, polls past the wave's end) are
+  // used here, so the compiler keeps every one of them on the path through the last chunk: the
+  // wait before each publish counts them
+#pragma unroll
+  for (int x = 0; x < RING; ++x) {
+#pragma unroll
+    for (int c = 0; c < KPL; ++c) asm volatile("" ::"v"(PR[x][c]));
+    asm volatile("" ::"v"(RU[x]));
+  }
+  asm volatile("" ::"v"(tk[0]), "v"(tk[1]));
+  strow<KPL>(irs, voff, item * rowb, q);  // the item row, once
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  publish(trs, pend0, pv0);
+  publish(trs, pend1, pv1);
+}
+
+// Blocks of two wave slots: slots[2b + w] is wave w's descriptor.  A single-item wave's slot 1 is
+// its helper (kDetWaveHelper: the same entries); any other slot runs det_wave (count 0: nothing).
+template <int KPL>
+__global__ __launch_bounds__(128) void k_det_sweep_split(const DetWave* __restrict__ slots, const uint32_t* __restrict__ eu,
+                                                         const uint32_t* __restrict__ ei, const uint32_t* __restrict__ eq,
+                                                         const double* __restrict__ er, double* U, double* I,
+                                                         uint64_t u_bytes, uint64_t i_bytes,
+                                                         const double* __restrict__ regU,
+                                                         const double* __restrict__ regI, double eta, int32_t* ticket,
+                                                         int32_t* err) {
+  __shared__ __attribute__((aligned(16))) DetLink<KPL> link;
+  const int w = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
+  const int lane = static_cast<int>(threadIdx.x) & 63;
+  const DetWave d0 = slots[2 * blockIdx.x];
+  const DetWave d = slots[2 * blockIdx.x + w];
+  if ((d0.flags & kDetWaveSingleItem) && d0.count > 0) {  // a chain / helper pair (both waves)
+    if (w == 1) {
+#pragma unroll
+      for (int sl = 0; sl < kLinkR; ++sl) link.tag[sl][lane] = -1;
+      link.done[lane] = 0;
+    }
+    __syncthreads();
+    if (w == 0) det_chain<KPL>(d0, ei, I, i_bytes, regI, eta, link, err, lane);
+    else det_helper<KPL>(d0, eu, ei, eq, er, U, I, u_bytes, i_bytes, regU, regI, eta, ticket, link, err, lane);
+    return;
+  }
+  if (d.count == 0) return;
+  det_wave<KPL, true, false>(d, eu, ei, eq, er, U, I, u_bytes, i_bytes, regU, regI, 64 * KPL, eta, ticket, nullptr, err,
+                             nullptr, lane);
+}
+
 template <int KPL, bool FULL>
 __global__ __launch_bounds__(64) void k_det_sweep2(const DetWave* __restrict__ waves, const uint32_t* __restrict__ eu,
                                                    const uint32_t* __restrict__ ei, const uint32_t* __restrict__ eq,
@@ -320,10 +672,11 @@ __global__ __launch_bounds__(64) void k_det_sweep2(const DetWave* __restrict__ w
   const DetWave d = waves[blockIdx.x];
   if (d.count == 0) return;
   if (d.flags & kDetWaveSingleItem)
-    det_wave<KPL, FULL, true>(d, eu, ei, eq, er, U, I, u_bytes, i_bytes, regU, regI, k, eta, ticket, dummy_ticket, err, lds);
+    det_wave<KPL, FULL, true>(d, eu, ei, eq, er, U, I, u_bytes, i_bytes, regU, regI, k, eta, ticket, dummy_ticket, err, lds,
+                              static_cast<int>(threadIdx.x));
   else
     det_wave<KPL, FULL, false>(d, eu, ei, eq, er, U, I, u_bytes, i_bytes, regU, regI, k, eta, ticket, dummy_ticket, err,
-                               lds);
+                               lds, static_cast<int>(threadIdx.x));
 }
 
 template <int KPL>
@@ -336,7 +689,38 @@ int det_capacity(bool full) {
   return st == hipSuccess ? cus * per_cu : 0;
 }
 
+template <int KPL>
+int det_split_cap() {
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_det_sweep_split<KPL>, 128, 0) != hipSuccess) return 0;
+  return 2 * cus * per_cu;
+}
+
 }  // namespace
+
+int det_split_capacity(int k) {
+  if (k == 64) return det_split_cap<1>();
+  if (k == 128) return det_split_cap<2>();
+  if (k == 256) return det_split_cap<4>();
+  return 0;
+}
+
+void launch_det_sweep_split(hipStream_t st, const DetWave* slots, int nslots, const uint32_t* eu, const uint32_t* ei,
+                            const uint32_t* eq, const double* er, double* U, double* I, uint64_t u_bytes,
+                            uint64_t i_bytes, const double* regU, const double* regI, int k, double eta,
+                            int32_t* ticket, int32_t* err, hipEvent_t ev0, hipEvent_t ev1) {
+  if (nslots <= 0) return;
+  const dim3 g(static_cast<unsigned>(nslots / 2)), b(128);
+#define MF_DETS(KPL)                                                                                           \
+  hipExtLaunchKernelGGL((k_det_sweep_split<KPL>), g, b, 0, st, ev0, ev1, 0, slots, eu, ei, eq, er, U, I, u_bytes, \
+                        i_bytes, regU, regI, eta, ticket, err)
+  if (k == 64) MF_DETS(1);
+  else if (k == 128) MF_DETS(2);
+  else if (k == 256) MF_DETS(4);
+#undef MF_DETS
+}
 
 // the co-resident wave count of the instance launch_det_sweep picks for k
 int det_sweep_capacity(int k) {

@@ -11,6 +11,7 @@
 //    per GPU (mf_create_rank) uses RCCL send/recv over xGMI.
 //  * Every shard keeps full-size factor slabs with the global row numbering, so a block moves
 //    by copying its row range; only the rows a shard currently owns are current.
+#include <array>
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -143,6 +144,9 @@ struct mf_ctx {
   bool fast_pair = false;         // two updates per step (kernels_pair.hip), k in {64, 128, 256}
   bool fast_sys = false;          // pair cells as one systolic launch per superstep (k_sweep_pair_sys)
   bool det_sweep = false;         // deterministic mode: one persistent k_det_sweep launch per superstep
+  bool det_split = false;         // ... with single-item chains split over two waves (k_det_sweep_split)
+  bool det_alone = true;          // ... the longest chains on CUs of their own (det_slot_table)
+  int64_t det_split_blocks = 0;   // resident blocks of k_det_sweep_split (per device share)
   bool ring_overlap = false;      // fast systolic sweep, >1 shard, c >= 2: the ring step overlaps the sweep
   // fast-mode hot-item replicas (plan.hpp SplitItem), an experiment outside the product surface:
   // MFHIP_ITEM_SPLIT=m sweeps an item with more than m ratings in one rating block as ceil(r / m)
@@ -909,12 +913,13 @@ void ring_shift(mf_ctx* ctx, int64_t superstep) {
 struct DetOffsets {
   size_t waves, u, i, qf, r, total;
 };
+int64_t det_slot_room(int64_t nw);
 DetOffsets det_offsets(int64_t n, int64_t nw) {
   auto up = [](size_t x) { return (x + 255) & ~static_cast<size_t>(255); };
   DetOffsets o;
   const size_t ne = static_cast<size_t>(n + kDetPad);  // the sweep reads whole chunks past a wave's end
   o.waves = 0;
-  o.u = up(static_cast<size_t>(nw) * sizeof(DetWave));
+  o.u = up(static_cast<size_t>(det_slot_room(nw)) * sizeof(DetWave));  // room for the split sweep's slot table
   o.i = o.u + up(ne * 4);
   o.qf = o.i + up(ne * 4);
   o.r = o.qf + up(ne * 4);
@@ -947,6 +952,49 @@ struct DetRunClock {
 };
 DetRunClock g_det_clock;
 const bool g_det_timing = std::getenv("MFHIP_TIMING") != nullptr;
+
+// The split sweep's slot table (kernels.hpp launch_det_sweep_split), in place over the nw waves of
+// build_det_step (the buffer holds det_slot_room(nw)): each single-item wave with its helper slot,
+// longest first (block 0 is the hottest chain), then the other waves two per block; empty waves
+// dropped.  The chains within half of the longest (at most kDetAlone) bound the superstep, so they
+// get a CU each: the dispatcher deals block b to XCD b % 8 and, inside it, CU (b / 8) % 32, so
+// blocks b + 256 m share block b's CU -- those positions stay empty (both waves leave at once)
+// while the table has at most max_blocks blocks.  Returns the slot count (even).
+constexpr int64_t kDetAlone = 64;
+int64_t det_slot_room(int64_t nw) { return 2 * nw + 2 * kDetAlone * (2 * nw / 256 + 2) + 2; }
+int64_t det_slot_table(DetWave* waves, int64_t nw, int64_t max_blocks, bool alone) {
+  std::vector<DetWave> single, multi;
+  for (int64_t w = 0; w < nw; ++w) {
+    if (waves[w].count == 0) continue;
+    ((waves[w].flags & kDetWaveSingleItem) ? single : multi).push_back(waves[w]);
+  }
+  std::stable_sort(single.begin(), single.end(), [](const DetWave& a, const DetWave& b) { return a.count > b.count; });
+  std::vector<std::array<DetWave, 2>> blocks;
+  for (const DetWave& d : single) blocks.push_back({d, DetWave{d.begin, 0, kDetWaveHelper}});
+  for (size_t x = 0; x < multi.size(); x += 2)
+    blocks.push_back({multi[x], x + 1 < multi.size() ? multi[x + 1] : DetWave{0, 0, 0}});
+  if (blocks.empty()) blocks.push_back({DetWave{0, 0, 0}, DetWave{0, 0, 0}});
+  int64_t H = 0;  // chains that get a CU each
+  if (alone)
+    while (H < std::min<int64_t>(kDetAlone, static_cast<int64_t>(single.size())) && 2 * single[H].count >= single[0].count)
+      ++H;
+  const int64_t nb = static_cast<int64_t>(blocks.size());
+  int64_t empties = 0;
+  for (int64_t b = 256; b < nb + empties; ++b) empties += (b % 256) < H;
+  if (nb + empties > max_blocks) empties = 0, H = 0;  // no room: the plain order
+  int64_t n = 0, next = 0;
+  for (int64_t b = 0; next < nb; ++b) {
+    if (b >= 256 && (b % 256) < H) {
+      waves[n++] = DetWave{0, 0, 0};
+      waves[n++] = DetWave{0, 0, 0};
+    } else {
+      waves[n++] = blocks[next][0];
+      waves[n++] = blocks[next][1];
+      ++next;
+    }
+  }
+  return n;
+}
 
 // Host side of one superstep for every local shard, into det_buf[slot] (runs on a worker thread
 // while the device runs the previous superstep).
@@ -981,6 +1029,7 @@ void det_build(mf_ctx* ctx, int64_t superstep, int slot) {
       db.keeps += (out.qf[x] & kDetKeepQ) != 0;
       db.defers += (out.qf[x] & kDetDeferQ) != 0;
     }
+    if (ctx->det_split) db.nw = det_slot_table(out.waves, db.nw, ctx->det_split_blocks, ctx->det_alone);
   }
 }
 
@@ -1060,12 +1109,20 @@ void det_run(mf_ctx* ctx, int64_t count) {
       MF_HIP(hipStreamWaitEvent(sh.stream, db.copied, 0));
       MF_HIP(hipMemsetAsync(sh.det_ticket.get(), 0, sh.det_ticket.bytes(), sh.stream));
       LaunchTimer tm(sh, ctx->profiling, true);
-      launch_det_sweep(sh.stream, reinterpret_cast<const DetWave*>(dp + o.waves), static_cast<int>(db.nw),
-                       reinterpret_cast<const uint32_t*>(dp + o.u), reinterpret_cast<const uint32_t*>(dp + o.i),
-                       reinterpret_cast<const uint32_t*>(dp + o.qf), reinterpret_cast<const double*>(dp + o.r),
-                       sh.uf.as<double>(), sh.itf.as<double>(), sh.uf.bytes(), sh.itf.bytes(), sh.regu.as<double>(),
-                       sh.regi.as<double>(), k, eta, sh.det_ticket.as<int32_t>(),
-                       sh.det_scratch.as<int32_t>(), sh.det_err.as<int32_t>(), tm.start(), tm.stop());
+      if (ctx->det_split)
+        launch_det_sweep_split(sh.stream, reinterpret_cast<const DetWave*>(dp + o.waves), static_cast<int>(db.nw),
+                               reinterpret_cast<const uint32_t*>(dp + o.u), reinterpret_cast<const uint32_t*>(dp + o.i),
+                               reinterpret_cast<const uint32_t*>(dp + o.qf), reinterpret_cast<const double*>(dp + o.r),
+                               sh.uf.as<double>(), sh.itf.as<double>(), sh.uf.bytes(), sh.itf.bytes(),
+                               sh.regu.as<double>(), sh.regi.as<double>(), k, eta, sh.det_ticket.as<int32_t>(),
+                               sh.det_err.as<int32_t>(), tm.start(), tm.stop());
+      else
+        launch_det_sweep(sh.stream, reinterpret_cast<const DetWave*>(dp + o.waves), static_cast<int>(db.nw),
+                         reinterpret_cast<const uint32_t*>(dp + o.u), reinterpret_cast<const uint32_t*>(dp + o.i),
+                         reinterpret_cast<const uint32_t*>(dp + o.qf), reinterpret_cast<const double*>(dp + o.r),
+                         sh.uf.as<double>(), sh.itf.as<double>(), sh.uf.bytes(), sh.itf.bytes(), sh.regu.as<double>(),
+                         sh.regi.as<double>(), k, eta, sh.det_ticket.as<int32_t>(),
+                         sh.det_scratch.as<int32_t>(), sh.det_err.as<int32_t>(), tm.start(), tm.stop());
       MF_HIP(hipGetLastError());
       MF_HIP(hipEventRecord(db.swept, sh.stream));
       ctx->stats.updates += db.n;
@@ -1166,6 +1223,8 @@ struct PhaseClock {
 // capacity (shared by the shards on that device; MFHIP_TEST det_waves= overrides).
 void prepare_det_sweep(mf_ctx* ctx) {
   if (test_knob("det_kernel") == "level") return;
+  // single-item chains split over two waves where k allows (MFHIP_TEST det_split=0: one wave each)
+  const bool split = test_knob("det_split") != "0" && det_split_capacity(ctx->P.num_factors) > 0;
   int cap = 1 << 30;
   for (auto& s : ctx->shards) {
     DeviceGuard g(s.device);
@@ -1173,7 +1232,10 @@ void prepare_det_sweep(mf_ctx* ctx) {
     for (auto& o : ctx->shards) sharers += o.device == s.device;
     if (const char* v = std::getenv("MFHIP_DEVICE_SHARERS"))
       if (ctx->rank_mode) sharers = std::max(sharers, std::atoi(v));
-    cap = std::min(cap, det_sweep_capacity(ctx->P.num_factors) / std::max(1, sharers));
+    // in wave slots; the split sweep's helpers take one each, at most one per wave of the layout
+    // (waves = cap / 2 below), so the slot table stays within the resident capacity
+    cap = std::min(cap, (split ? det_split_capacity(ctx->P.num_factors) : det_sweep_capacity(ctx->P.num_factors)) /
+                            std::max(1, sharers));
   }
   if (cap < 1) return;
   const uint64_t k8 = static_cast<uint64_t>(ctx->P.num_factors) * 8;
@@ -1222,6 +1284,9 @@ void prepare_det_sweep(mf_ctx* ctx) {
     MF_HIP(hipMemsetAsync(s.det_err.get(), 0, 16, s.stream));
   }
   ctx->det_sweep = true;
+  ctx->det_split = split;
+  ctx->det_split_blocks = cap / 2;
+  ctx->det_alone = test_knob("det_alone") != "0";
 }
 
 void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, int64_t n) {

@@ -135,6 +135,7 @@ struct DetWave {
   int32_t flags;  // kDetWaveSingleItem
 };
 constexpr int32_t kDetWaveSingleItem = 1;  // every entry of the wave updates one item
+constexpr int32_t kDetWaveHelper = 2;      // split sweep: the helper slot of a single-item wave
 static_assert(sizeof(DetWave) == 16, "DetWave is one 16-B word");
 
 struct DetSweepLayout {

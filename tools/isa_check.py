@@ -344,6 +344,7 @@ CHECKS = [
     # stores landed; the ticket sweeps publish update j-2's ticket at update j (j-1's stores may fly)
     (r"k_sweep_pair_sys", "all", progress_flag),
     (r"k_det_sweep2", "prev", buffer_ticket),
+    (r"k_det_sweep_split", "prev", buffer_ticket),
     (r"k_online_sweepId", "prev", progress_flag),
     (r"k_online_f32", "prev", progress_flag),
 ]
