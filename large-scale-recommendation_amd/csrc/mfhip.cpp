@@ -53,8 +53,10 @@ struct DeviceGuard {
 
 // Deterministic persistent sweep: one superstep's entries, staged in pinned memory by a host
 // thread while earlier supersteps run, then copied to the device (fixed SoA offsets).  A ring of
-// kDetSlots buffers: the host builds supersteps s+1 and s+2 (two builders, each one thread per
-// rating block) while the device runs s.
+// kDetSlots buffers: the host builds supersteps s+1 and s+2 (two builders at once) while the device
+// runs s.  On the GPU box (16 host threads) one NFLX build takes ~28 ms alone and about as long
+// with another beside it, i.e. ~14 ms per superstep -- the split sweep's ~14.4 ms launch; a third
+// builder does not raise that rate (three at once: ~44 ms each, the host threads are saturated).
 constexpr int kDetSlots = 3;
 struct DetBuf {
   PinnedBuf pin;
@@ -1056,9 +1058,9 @@ void det_run(mf_ctx* ctx, int64_t count) {
   };
   std::future<void> builds[kDetSlots];
   constexpr int kAhead = kDetSlots - 1;  // supersteps built ahead of the one launched
-  // the previous run's speculative builds of supersteps s0, s0+1 (slots 0, 1) are taken over;
+  // the previous run's speculative builds of supersteps s0 .. s0+kAhead-1 (slots 0 ..) are taken over;
   // any other is joined and dropped (a taken-over build is waited for like the run's own)
-  bool prebuilt[kDetSlots] = {false, false, false};
+  bool prebuilt[kDetSlots] = {};
   for (int slot = 0; slot < kDetSlots; ++slot) {
     const int64_t built = ctx->det_spec_s[slot];
     ctx->det_spec_s[slot] = -1;  // before anything can throw: a slot is never taken over twice
@@ -1251,7 +1253,7 @@ void prepare_det_sweep(mf_ctx* ctx) {
   const int32_t n = ctx->nb;
   {  // the build's shuffle-order gather reads one 16-B record per rating
     const int64_t total = ctx->rb.start.empty() ? 0 : ctx->rb.start.back();
-    ctx->rb.det_aos.resize(static_cast<size_t>(total));
+    resize_huge(ctx->rb.det_aos, static_cast<size_t>(total));  // random reads: fewer TLB misses
     DetEntry* a = ctx->rb.det_aos.data();
     parallel_for(total, [&](int64_t b, int64_t e, int) {
       for (int64_t x = b; x < e; ++x) a[x] = DetEntry{ctx->rb.urow[x], ctx->rb.irow[x], ctx->rb.r[x]};

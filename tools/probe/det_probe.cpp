@@ -39,6 +39,8 @@ int main(int argc, char** argv) {
   build_side(I, i.data(), n, nb, 0, true);
   RatingBlocks rb;
   build_rating_blocks(rb, U, I, u.data(), i.data(), r.data(), n, 0, nb, true);
+  rb.det_aos.resize(rb.start.back());  // as prepare_det_sweep
+  for (int64_t x = 0; x < rb.start.back(); ++x) rb.det_aos[x] = DetEntry{rb.urow[x], rb.irow[x], rb.r[x]};
   DetSweepLayout L;
   build_det_layout(L, rb, U, I, nb, 0, waves);
   for (int s = 1; s <= steps; ++s) {
@@ -68,8 +70,12 @@ int main(int argc, char** argv) {
     };
     mix(w.data(), w.size() * sizeof(DetWave));
     mix(ou.data(), ne * 4); mix(oi.data(), ne * 4); mix(oq.data(), ne * 4); mix(orr.data(), ne * 8);
-    std::printf("superstep %d: %lld entries %lld waves  build %.1f ms  digest %016llx\n", s, (long long)ne,
-                (long long)nw, dt * 1e3, (unsigned long long)h);
+    static int64_t prev[5] = {0, 0, 0, 0, 0};
+    double ph[5];
+    for (int x = 0; x < 5; ++x) ph[x] = (det_build_phase_ns(x) - prev[x]) / 1e6, prev[x] = det_build_phase_ns(x);
+    std::printf("superstep %d: %lld entries %lld waves  build %.1f ms (shuffle %.1f gather %.1f prefix %.1f scatter %.1f "
+                "flags %.1f)  digest %016llx\n", s, (long long)ne, (long long)nw, dt * 1e3, ph[0], ph[1], ph[2], ph[3],
+                ph[4], (unsigned long long)h);
   }
   return 0;
 }
