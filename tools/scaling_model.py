@@ -12,6 +12,7 @@ chip, the best a lightly loaded GPU can do).
     python tools/scaling_model.py /tmp/scale_probe.txt [t_run_loaded t_mix_loaded t_run_iso cell_ns]
 """
 import collections
+import gzip
 import sys
 
 path = sys.argv[1]
@@ -22,7 +23,7 @@ cell_ns = float(sys.argv[5]) if len(sys.argv) > 5 else 2500.0  # per non-empty c
 ring_us = 20.0  # one item-block send/recv per superstep (1.1 MB over one xGMI link + launch), not overlapped at c = 1
 
 waves = collections.defaultdict(list)  # (G, rank, sm) -> [(cells, run, mix)]
-for line in open(path):
+for line in (gzip.open(path, "rt") if path.endswith(".gz") else open(path)):
     if not line.startswith("SCALE"):
         continue
     f = line.split()
