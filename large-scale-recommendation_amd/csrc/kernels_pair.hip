@@ -362,6 +362,11 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const ChunkRaw& L0,
       }
       float c1 = dot_part<KPL>(pa, qa), c2 = dot_part<KPL>(pb, qbd), g = dot_part<KPL>(pb, pa);
       wave_sum3(c1, c2, g);
+#ifdef MFHIP_EXP_PAD_VALU  // sensitivity experiment: N extra VALU issue slots per mixed pair
+#define MF_STR2(x) #x
+#define MF_STR(x) MF_STR2(x)
+      asm volatile(".rept " MF_STR(MFHIP_EXP_PAD_VALU) "\n\tv_nop\n\t.endr");
+#endif
       // wa = eta eA, wb = eta eB in the chunk layout (lane s = pair s); a split pair has no
       // coupling to A's update (sr = 0, m = 1)
       const float wav = fmaf(c1, neta, C0.era);
