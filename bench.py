@@ -172,7 +172,13 @@ def rmse_reference(a, arrays):
     return rec
 
 
-def det_kernel_name():
+def det_kernel_name(k):
+    """The persistent deterministic sweep the library picks (mfhip.cpp prepare_det_sweep): the
+    split single-item chains (chain + helper wave) where k = 64 KPL, KPL in {1, 2, 4}, unless
+    MFHIP_TEST det_split=0."""
+    knobs = dict(x.split("=", 1) for x in os.environ.get("MFHIP_TEST", "").split(",") if "=" in x)
+    if k in (64, 128, 256) and knobs.get("det_split") != "0":
+        return "k_det_sweep_split"
     return "k_det_sweep2"
 
 
@@ -187,7 +193,7 @@ def det_roofline(a, k, sp):
     ksec = sp["kernel_ms"] / 1e3
     alg = sp["updates"] * (32 * k + 24) / ksec / 1e9
     da = argparse.Namespace(**{**vars(a), "mode": "det"})
-    traffic, src = pmc_traffic(da, k, 0, det_kernel_name(), round(sp["kernel_ms"] * 1e3 / launches, 2))
+    traffic, src = pmc_traffic(da, k, 0, det_kernel_name(k), round(sp["kernel_ms"] * 1e3 / launches, 2))
     tr_gbs = traffic / (ksec / launches) / 1e9 if traffic else None
     head = tr_gbs if tr_gbs is not None else alg
     return {"bound": "hbm", "achieved": round(head, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -245,7 +251,7 @@ def det_leg(a, k, nb, train, test, ref, stream):
         online = online_leg(ctx, stream, a) if stream is not None else None
     return {"metric": "SGD rating updates/sec, deterministic f64 (the reference's exact update order)",
             "value": round(st["updates"] / el, 1), "unit": "updates/s", "dtype": "f64", "epochs": a.det_epochs,
-            "ms_per_step": round(el * 1e3 / a.det_epochs, 3), "kernel": det_kernel_name(),
+            "ms_per_step": round(el * 1e3 / a.det_epochs, 3), "kernel": det_kernel_name(k),
             "avg_launch_us": round(sp["kernel_ms"] * 1e3 / max(sp["kernel_launches"], 1), 2),
             "roofline": det_roofline(a, k, sp),
             "launches_per_epoch": sp["kernel_launches"], "prepare_s": round(t_prep, 2),
@@ -424,7 +430,7 @@ def main():
         launches = st_p["kernel_launches"]
         ksec = st_p["kernel_ms"] / 1e3
         achieved = st_p["moved_bytes"] / ksec / 1e9  # GB/s, this rank's sweep kernel
-        kname = L.lib().mf_fast_kernel_name(k).decode() if a.mode == "fast" else det_kernel_name()
+        kname = L.lib().mf_fast_kernel_name(k).decode() if a.mode == "fast" else det_kernel_name(k)
         launch_us = round(st_p["kernel_ms"] * 1e3 / max(launches, 1), 2)
         # the committed PMC summaries are one-GPU runs: a rank of an N-GPU ring runs other launches
         traffic, traffic_src = pmc_traffic(a, k, st["groups"], kname, launch_us) if D.world == 1 else (None, None)

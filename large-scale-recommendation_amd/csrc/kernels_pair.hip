@@ -78,7 +78,7 @@ __device__ __forceinline__ void single_run_cell(Chunk C0, __amdgpu_buffer_rsrc_t
     RA[s] = ld<KPL, UP>(urs, voff, rl(C0.ua, s));
     RB[s] = ld<KPL, UP>(urs, voff, rl(C0.ub, s));
   }
-  drain_vmem();
+  if constexpr (KPL >= 4) drain_vmem();  // prefill_wait (pair_device.hpp)
   const float neta = vgpr_of(-eta);
   ChunkRaw N{};  // the next chunk (sweep_chunks loads it when the current one starts)
   auto pair = [&](auto S) __attribute__((always_inline)) {
@@ -169,7 +169,7 @@ __device__ __forceinline__ void single_run_cell_k1(Chunk C0, __amdgpu_buffer_rsr
     RA[s] = ld1<UP>(urs, voff, rl(C0.ua, s));
     RB[s] = ld1<UP>(urs, voff, rl(C0.ub, s));
   }
-  drain_vmem();
+  // no drain after the prefill (pair_device.hpp drain_vmem)
   const float neta = vgpr_of(-eta);
   ChunkRaw N{};  // the next chunk (sweep_chunks loads it when the current one starts)
   auto pair = [&](auto S) __attribute__((always_inline)) {
@@ -225,7 +225,7 @@ __device__ __forceinline__ void generic_cell_k1(Chunk C0, __amdgpu_buffer_rsrc_t
     QA[s] = ld1<IP>(irs, voff, rl(C0.ia, s));
     QB[s] = ld1<IP>(irs, voff, rl(C0.ib, s));
   }
-  drain_vmem();
+  // no drain after the prefill (pair_device.hpp drain_vmem)
   const float neta = vgpr_of(-eta);
   float q = 0.f;
   ChunkRaw N{};  // the next chunk (sweep_chunks loads it when the current one starts)
@@ -322,7 +322,7 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const ChunkRaw& L0,
     } while (0)
 #pragma unroll
     for (int s = 0; s < D; ++s) MF_PREFETCH(s, C0.ua, C0.ub, C0.ia, C0.ib, s);
-    drain_vmem();
+    if constexpr (KPL >= 4) drain_vmem();  // prefill_wait (pair_device.hpp)
     const float neta = vgpr_of(-eta);
     Row<KPL> q;
 #pragma unroll

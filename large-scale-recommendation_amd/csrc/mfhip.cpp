@@ -1285,6 +1285,12 @@ void prepare_det_sweep(mf_ctx* ctx) {
     s.det_err.alloc(16);
     MF_HIP(hipMemsetAsync(s.det_err.get(), 0, 16, s.stream));
   }
+  // the sweep's host build reads only det_aos from here on: release the (user row, item row,
+  // rating) arrays it was made from (16 B per rating; ~11.5 GB at full YAHOO)
+  ctx->reaper.drop(ctx->rb.urow);
+  ctx->reaper.drop(ctx->rb.irow);
+  ctx->reaper.drop(ctx->rb.r);
+  ctx->reaper.release();
   ctx->det_sweep = true;
   ctx->det_split = split;
   ctx->det_split_blocks = cap / 2;

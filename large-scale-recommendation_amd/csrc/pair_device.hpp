@@ -135,10 +135,13 @@ struct Chunk {
 // chunk ahead and only converted (eta folded in) when it becomes current, so nothing reads a
 // just-loaded register at the chunk boundary and the factor-row ring keeps running across it
 // (converting at load time made every chunk boundary wait for its own record loads).
-// s_waitcnt vmcnt(0) the compiler can see (gfx9 encoding: expcnt 7, lgkmcnt 15).  Issued once
-// after a wave's initial prefetch: otherwise the loop header inherits the preheader's "just
-// loaded" ring rows and the compiler drains the ring at EVERY chunk boundary (vmcnt(0) in the
-// header, i.e. once per 56 pairs).
+// s_waitcnt vmcnt(0) the compiler can see (gfx9 encoding: expcnt 7, lgkmcnt 15).  Round 4 issued
+// it after a cell's ring prefill: otherwise the loop header inherited the preheader's "just loaded"
+// ring rows and the compiler drained the ring at every chunk boundary.  With the exit-free chunk
+// loop (sweep_chunks) the header waits are the same with or without it at KPL <= 2
+// (tools/isa_waits.py), so those cells start on their first pair's rows instead of waiting for the
+// whole ring (~56 loads issued back to back, ~0.25 us per cell); KPL = 4 keeps it (without it
+// its header waits turn conservative).
 __device__ __forceinline__ void drain_vmem() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
 struct ChunkRaw {
