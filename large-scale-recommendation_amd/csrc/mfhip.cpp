@@ -1362,6 +1362,14 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
         cap = std::min(cap, sweep_pair_sys_capacity(k));
         simds = std::min(simds, 4 * cus);
       }
+      // the group model's wave budget: at most two waves per CU at k <= 128, three at k = 256.  A
+      // pair step slows sharply with the waves that share its CU (its row traffic goes through the
+      // CU's one vector-memory path): NFLX 178 -> 231 ns per mixed pair from two to three waves per
+      // CU, YAHOO 301 -> 560 from three to four (profiles/r05_*_wave_trace.txt), which the model's
+      // fixed per-pair cost does not see.  Measured (profiles/r05_wave_budget.txt): NFLX 21.34 ->
+      // 21.01-21.03 ms per epoch (656 -> 512 waves), YAHOO 228.1 -> 220.8 ms (1004 -> 768), ML20M
+      // unchanged (its model optimum, 461 waves, is below the budget).
+      simds = std::min(simds, (k <= 128 ? 2 : 3) * (simds / 4));
       if (const std::string v = test_knob("sys_waves"); !v.empty()) simds = std::max(8, std::atoi(v.c_str()));
       if (ctx->P.fast_waves == 0 && test_knob("block_groups") != "0") {
         block_groups.assign(nb2, 0);
