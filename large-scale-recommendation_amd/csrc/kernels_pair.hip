@@ -66,8 +66,8 @@ __device__ __forceinline__ void single_run_cell(Chunk C0, __amdgpu_buffer_rsrc_t
                                                 uint32_t vlane, uint32_t voff, int npairs, uint64_t& wait_clk) {
   (void)wait_clk;
   constexpr int NV = Row<KPL>::NV;
-  constexpr int CH = kPairChunk;
-  constexpr int DS = kPairRingSingle;
+  constexpr int CH = pair_chunk(KPL);
+  constexpr int DS = pair_ring(KPL);
   const uint32_t item_off = rl(C0.ia, 0);
   Row<KPL> q = ld<KPL, IP>(irs, voff, item_off);
   Row<KPL> RA[DS], RB[DS], plA, plB;
@@ -127,7 +127,7 @@ __device__ __forceinline__ void single_run_cell(Chunk C0, __amdgpu_buffer_rsrc_t
     RA[slot] = ld<KPL, UP>(urs, voff, noa);
     RB[slot] = ld<KPL, UP>(urs, voff, nob);
   };
-  sweep_chunks<kPairChunk>(npairs, pair, [&](int c) { N = chunk_load(RR, c + 1, vlane); },
+  sweep_chunks<CH>(npairs, pair, [&](int c) { N = chunk_load<CH>(RR, c + 1, vlane); },
                            [&] { C0 = chunk_convert(N, eta); });
   keep_chunk(N);
   st<KPL, IP>(irs, voff, item_off, q);
@@ -159,8 +159,8 @@ template <int UP, bool FWD, int IP = kItemPolicy>
 __device__ __forceinline__ void single_run_cell_k1(Chunk C0, __amdgpu_buffer_rsrc_t RR,
                                                    __amdgpu_buffer_rsrc_t urs, __amdgpu_buffer_rsrc_t irs, float eta,
                                                    uint32_t vlane, uint32_t voff, int npairs) {
-  constexpr int CH = kPairChunk;
-  constexpr int DS = kPairRingSingle;
+  constexpr int CH = pair_chunk(1);
+  constexpr int DS = pair_ring(1);
   const uint32_t item_off = rl(C0.ia, 0);
   float q = ld1<IP>(irs, voff, item_off);
   float RA[DS], RB[DS], plA = 0.f, plB = 0.f;
@@ -205,7 +205,7 @@ __device__ __forceinline__ void single_run_cell_k1(Chunk C0, __amdgpu_buffer_rsr
     RA[slot] = ld1<UP>(urs, voff, noa);
     RB[slot] = ld1<UP>(urs, voff, nob);
   };
-  sweep_chunks<kPairChunk>(npairs, pair, [&](int c) { N = chunk_load(RR, c + 1, vlane); },
+  sweep_chunks<CH>(npairs, pair, [&](int c) { N = chunk_load<CH>(RR, c + 1, vlane); },
                            [&] { C0 = chunk_convert(N, eta); });
   keep_chunk(N);
   st1<IP>(irs, voff, item_off, q);
@@ -215,7 +215,7 @@ template <int D, int UP, int IP = kItemPolicy>
 __device__ __forceinline__ void generic_cell_k1(Chunk C0, __amdgpu_buffer_rsrc_t RR,
                                                 __amdgpu_buffer_rsrc_t urs, __amdgpu_buffer_rsrc_t irs, float eta,
                                                 uint32_t vlane, uint32_t voff, int npairs) {
-  constexpr int CH = kPairChunk;
+  constexpr int CH = pair_chunk(1);
   float plA = 0.f, plB = 0.f;
   float PA[D], PB[D], QA[D], QB[D];
 #pragma unroll
@@ -267,7 +267,7 @@ __device__ __forceinline__ void generic_cell_k1(Chunk C0, __amdgpu_buffer_rsrc_t
     QA[slot] = ld1<IP>(irs, voff, nia);
     QB[slot] = ld1<IP>(irs, voff, nib);
   };
-  sweep_chunks<kPairChunk>(npairs, pair, [&](int c) { N = chunk_load(RR, c + 1, vlane); },
+  sweep_chunks<CH>(npairs, pair, [&](int c) { N = chunk_load<CH>(RR, c + 1, vlane); },
                            [&] { C0 = chunk_convert(N, eta); });
   keep_chunk(N);
 }
@@ -282,7 +282,7 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const ChunkRaw& L0,
                                           __amdgpu_buffer_rsrc_t irs, float eta, int lane, uint64_t& wait_clk) {
   (void)wait_clk;
   constexpr int NV = Row<KPL>::NV;
-  constexpr int CH = kPairChunk;
+  constexpr int CH = pair_chunk(KPL);
   static_assert(CH % D == 0, "ring slots must repeat every chunk");
   const int npairs = d.steps;
   const __amdgpu_buffer_rsrc_t RR = cell_records(recs, d.base, npairs);
@@ -393,7 +393,7 @@ __device__ __forceinline__ void pair_cell(const WaveDesc d, const ChunkRaw& L0,
       QA[slot] = ld<KPL, IP>(irs, voff, nia);
       QB[slot] = ld<KPL, IP>(irs, voff, nib);
   };
-  sweep_chunks<kPairChunk>(npairs, pair, [&](int c) { N = chunk_load(RR, c + 1, vlane); },
+  sweep_chunks<CH>(npairs, pair, [&](int c) { N = chunk_load<CH>(RR, c + 1, vlane); },
                            [&] { C0 = chunk_convert(N, eta); });
     keep_chunk(N);
 #undef MF_PREFETCH
@@ -411,7 +411,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   const __amdgpu_buffer_rsrc_t rr = cell_records(recs, d.base, d.steps);
   const uint32_t vlane = threadIdx.x * 64u;
   uint64_t wait_clk = 0;
-  pair_cell<KPL, D, 0>(d, chunk_load(rr, 0, vlane), recs, raw_rsrc(U, u_bytes),
+  pair_cell<KPL, D, 0>(d, chunk_load<pair_chunk(KPL)>(rr, 0, vlane), recs, raw_rsrc(U, u_bytes),
                        raw_rsrc(I, i_bytes), eta, threadIdx.x, wait_clk);
   MF_LAUNCH_RELEASE();
   if (trace && threadIdx.x == 0) {
@@ -463,7 +463,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   const __amdgpu_buffer_rsrc_t urs = raw_rsrc(U, u_bytes), irs = raw_rsrc(I, i_bytes);
   const uint32_t vlane = static_cast<uint32_t>(lane) * 64u;
   auto first_chunks = [&](const WaveDesc& c, ChunkRaw& A) {  // an empty cell reads nothing
-    A = chunk_load(cell_records(recs, c.base, c.steps), 0, vlane);
+    A = chunk_load<pair_chunk(KPL)>(cell_records(recs, c.base, c.steps), 0, vlane);
   };
   WaveDesc d = my[0];
   ChunkRaw L0;
@@ -523,7 +523,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
 template <int KPL>
 void dispatch(hipStream_t st, const WaveDesc* waves, int nwaves, const PairRec* recs, float* U, float* I,
               uint64_t ub, uint64_t ib, float eta, uint64_t* trace, hipEvent_t ev0, hipEvent_t ev1) {
-  hipExtLaunchKernelGGL((k_sweep_pair<KPL, kPairRing>), dim3(static_cast<unsigned>(nwaves)), dim3(64), 0, st, ev0, ev1,
+  hipExtLaunchKernelGGL((k_sweep_pair<KPL, pair_ring(KPL)>), dim3(static_cast<unsigned>(nwaves)), dim3(64), 0, st, ev0, ev1,
                         0, waves, reinterpret_cast<const u4v*>(recs), U, I, ub, ib, eta, trace);
 }
 
@@ -537,7 +537,7 @@ template <int KPL>
 void dispatch_sys(hipStream_t st, const SysWave* sw, const WaveDesc* sys, int nw, int lbase, const PairRec* recs,
                   float* U, float* I, uint64_t ub, uint64_t ib, float eta, int32_t* prog, uint32_t base, int32_t* err,
                   uint64_t* trace, hipEvent_t ev0, hipEvent_t ev1, const int32_t* place) {
-  hipExtLaunchKernelGGL((k_sweep_pair_sys<KPL, kPairRing, kCellPreload<KPL>>), dim3(static_cast<unsigned>(nw)),
+  hipExtLaunchKernelGGL((k_sweep_pair_sys<KPL, pair_ring(KPL), kCellPreload<KPL>>), dim3(static_cast<unsigned>(nw)),
                         dim3(64), 0, st, ev0, ev1, 0, sw, sys, nw, lbase, reinterpret_cast<const u4v*>(recs), U, I, ub,
                         ib, eta, prog, base, err, trace, place);
 }
@@ -547,7 +547,7 @@ int sys_capacity() {
   int dev = 0, cus = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sweep_pair_sys<KPL, kPairRing, kCellPreload<KPL>>, 64,
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sweep_pair_sys<KPL, pair_ring(KPL), kCellPreload<KPL>>, 64,
                                                    0) != hipSuccess)
     return 0;
   return cus * per_cu;

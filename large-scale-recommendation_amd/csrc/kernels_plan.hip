@@ -257,6 +257,7 @@ struct PairArgs {
   double* bytes;             // per wave: requested bytes
   int64_t nwaves;
   double row_bytes;
+  int32_t ring;  // the sweep's ring depth for this k (plan.hpp pair_ring)
 };
 
 // build_pair_plan's per-cell body (plan.cpp), one thread per wave.
@@ -325,9 +326,9 @@ __global__ __launch_bounds__(kPlanThreads) void k_pair_waves(PairArgs A) {
     for (const PairRec* r = first; single && r < out; ++r)
       single = !(r->flags & kPairSplit) && (r == first || (r->flags & kPairKeepQ)) && r->ub == r->sb &&
                (r + 1 < out ? r->si == kOffOOB : r->si == first[0].ia);
-    if (single) {  // the lean path's ring: a loaded user row was stored >= kPairRingSingle pairs back
-      constexpr int kR = kPairRingSingle - 1;
-      uint32_t ring[kR > 0 ? kR : 1][2];
+    if (single) {  // the lean path's ring: a loaded user row was stored >= A.ring pairs back
+      const int kR = A.ring - 1;
+      uint32_t ring[kPairPlanRing][2];
       for (auto& rr : ring) rr[0] = rr[1] = kOffOOB;
       for (const PairRec* r = first; single && r < out; ++r) {
         const int64_t j = r - first;
@@ -641,6 +642,7 @@ void emit_and_pair(hipStream_t st, const PlanBlocks& pb, DevBuf& dE, DevBuf& dcs
   P.bytes = dbytes.as<double>();
   P.nwaves = nwaves;
   P.row_bytes = 4.0 * k;
+  P.ring = pair_ring(pair_kpl(k));
   if (nwaves > 0) {
     hipLaunchKernelGGL(k_pair_waves, dim3(plan_grid(nwaves)), dim3(kPlanThreads), 0, st, P);
     MF_HIP(hipGetLastError());

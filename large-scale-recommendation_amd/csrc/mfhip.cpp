@@ -1434,7 +1434,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
       DeviceGuard g(s0.device);
       device_fast_schedule(s0.stream, dev_rb, ctx->rb, ctx->U, ctx->I, Gb, ctx->P.lambda,
                            static_cast<uint64_t>(ctx->P.seed) * 0x9E3779B97F4A7C15ULL + 1, fp, ctx->c, s0.index, k,
-                           dummy, 2 * kPairRing, dev_pp, dev_pairs);
+                           dummy, 2 * kPairPlanRing, dev_pp, dev_pairs);
       dev_rb = DevRatingBlocks();
     } else {
       if (ctx->rb.urow.empty() && dev_rb.urow.get()) {  // a host-built plan after all
@@ -1444,7 +1444,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
       }
       build_fast_plan(fp, ctx->rb, ctx->U, ctx->I, ctx->G_fast, k, ctx->P.lambda,
                       static_cast<uint64_t>(ctx->P.seed) * 0x9E3779B97F4A7C15ULL + 1, dummy, nullptr,
-                      ctx->fast_pair ? 2 * kPairRing : kHazardWindow, block_groups.empty() ? nullptr : &block_groups,
+                      ctx->fast_pair ? 2 * kPairPlanRing : kHazardWindow, block_groups.empty() ? nullptr : &block_groups,
                       ctx->item_split, static_cast<uint32_t>(ctx->I.rows() + 1), dev_plan ? &entries : nullptr);
     }
     MF_REQUIRE(static_cast<uint64_t>(ctx->I.rows() + 1 + fp.scratch_rows) * k * 4 < (1ull << 32),
@@ -1453,7 +1453,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
       Shard& s0 = ctx->shards[0];
       DeviceGuard g(s0.device);
       clk.lap("cell order (host)");
-      device_pair_schedule(s0.stream, entries, fp, ctx->nb, ctx->c, s0.index, k, dummy, 2 * kPairRing, false, dev_pp,
+      device_pair_schedule(s0.stream, entries, fp, ctx->nb, ctx->c, s0.index, k, dummy, 2 * kPairPlanRing, false, dev_pp,
                            dev_pairs);
       ctx->reaper.drop(entries);
     }
@@ -2670,7 +2670,7 @@ int mf_fast_plan_window(int32_t k, int32_t* window_out) {
   return guarded([&] {
     MF_REQUIRE(window_out, "null");
     const FastKernel fk = choose_fast_kernel(k);
-    *window_out = fk == FastKernel::kPair ? 2 * kPairRing : kHazardWindow;
+    *window_out = fk == FastKernel::kPair ? 2 * kPairPlanRing : kHazardWindow;
   });
 }
 

@@ -156,12 +156,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t cell_records(const u4v* recs, 
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<u4v*>(recs + 4 * base), 0,
                                            static_cast<uint32_t>(npairs > 0 ? npairs : 0) * 64u, 0x00020000);
 }
-// Chunk c of the cell: pair c * kPairChunk + lane in lane `lane` (vlane = lane * 64).  Records are
+// Chunk c of the cell: pair c * CH + lane in lane `lane` (vlane = lane * 64).  Records are
 // read once: non-temporal (cache policy nt), so they do not push factor rows out of L2 / MALL.
+template <int CH>
 __device__ __forceinline__ ChunkRaw chunk_load(__amdgpu_buffer_rsrc_t rr, int c, uint32_t vlane) {
   // c is uniform, but the divergence analysis cannot always prove it through the cell loops'
   // exits (the generic k = 128 loop's chunk loads became a readfirstlane waterfall): say so
-  const uint32_t so = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(c)) * kPairChunk * 64u;
+  const uint32_t so = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(c)) * CH * 64u;
   constexpr int kNT = 2;
   return ChunkRaw{__builtin_amdgcn_raw_buffer_load_b128(rr, vlane, so, kNT),
                   __builtin_amdgcn_raw_buffer_load_b128(rr, vlane + 16u, so, kNT),

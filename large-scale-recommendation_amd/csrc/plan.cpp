@@ -1177,11 +1177,11 @@ void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, in
                  (r + 1 < out ? r->si == kOffOOB : r->si == first[0].ia);
         if (!single) why = (r->flags & kPairSplit) ? 2 : !(r == first || (r->flags & kPairKeepQ)) ? 3 : r->ub != r->sb ? 4 : 5;
       }
-      // the lean path prefetches kPairRingSingle pairs ahead: a user row it loads must have
-      // been stored by an earlier pair at least that far back
-      if (single) {  // the stores of the previous kPairRingSingle - 1 pairs, as a ring
-        constexpr int kR = kPairRingSingle - 1;
-        uint32_t ring[kR > 0 ? kR : 1][2];
+      // the lean path prefetches pair_ring pairs ahead: a user row it loads must have been
+      // stored by an earlier pair at least that far back
+      if (single) {  // the stores of the previous pair_ring - 1 pairs, as a ring
+        const int kR = pair_ring(pair_kpl(k)) - 1;
+        uint32_t ring[kPairPlanRing][2];
         for (auto& rr : ring) rr[0] = rr[1] = kOffOOB;
         for (const PairRec* r = first; single && r < out; ++r) {
           const int64_t j = r - first;

@@ -254,14 +254,31 @@ struct WaveDesc {
 // pair, A ends its item run, B starts one); a step whose B would repeat A's user gets a
 // no-op B.  Row fields are byte offsets, kOffOOB = no load (the row is forwarded in registers
 // or the record is a no-op) / no store.
-constexpr int kPairRing = 7;    // pairs prefetched ahead: 8 VMEM ops per pair, vmcnt <= 63
-constexpr int kPairChunk = 56;  // pair records per register chunk (a multiple of kPairRing)
-// Single-run waves (one item run, kWaveSingleRun) move only user rows (4 VMEM ops per pair) and
-// could run a ring twice as deep; 14 measured no faster than 7 (the step is not load-latency
-// bound), so they share kPairRing.  build_pair_plan checks that every user row such a wave
-// loads was last stored at least kPairRingSingle pairs earlier (or is forwarded in registers).
-constexpr int kPairRingSingle = kPairRing;
-static_assert(kPairChunk % kPairRing == 0 && kPairChunk % kPairRingSingle == 0, "ring slots must repeat every chunk");
+// The plan's hazard window is 2 * kPairPlanRing records: a user row is loaded at most kPairPlanRing
+// pairs before its update, so inside a cell a user recurs either at the next record (forwarded in
+// registers) or at least that far on.  The sweeps prefetch pair_ring(KPL) <= kPairPlanRing pairs
+// ahead (8 VMEM operations per pair, vmcnt <= 63), measured per row width (round 5,
+// profiles/r05_pair_ring.txt): a deeper ring is NOT faster -- the pair step is not load-latency
+// bound, and fewer rows in flight per wave leave the CU's memory path less crowded and a cell's
+// ring prefill shorter: NFLX (KPL 2) 21.0 -> 20.27 ms at 6, ML20M (KPL 1) 4.93 -> 4.82 at 4,
+// YAHOO (KPL 4) 237 -> 230 ms at 4.  Records come in chunks of pair_chunk(KPL) pairs (one per lane,
+// a multiple of the ring).  Single-run waves (kWaveSingleRun, 4 VMEM ops per pair) use the same
+// ring; build_pair_plan checks that every user row such a wave loads was last stored at least
+// pair_ring pairs earlier (or is forwarded in registers).
+constexpr int kPairPlanRing = 7;
+#ifdef MFHIP_EXP_PAIR_RING  // experiment: one ring depth / chunk for every row width
+constexpr int pair_ring(int) { return MFHIP_EXP_PAIR_RING; }
+constexpr int pair_chunk(int) { return MFHIP_EXP_PAIR_CHUNK; }
+#else
+constexpr int pair_ring(int kpl) { return kpl == 2 ? 6 : 4; }
+constexpr int pair_chunk(int kpl) { return kpl == 2 ? 60 : 56; }
+#endif
+constexpr int pair_kpl(int k) { return k <= 64 ? 1 : k <= 128 ? 2 : 4; }
+static_assert(pair_chunk(1) % pair_ring(1) == 0 && pair_chunk(2) % pair_ring(2) == 0 &&
+                  pair_chunk(4) % pair_ring(4) == 0, "ring slots must repeat every chunk");
+static_assert(pair_ring(1) <= kPairPlanRing && pair_ring(2) <= kPairPlanRing && pair_ring(4) <= kPairPlanRing &&
+                  pair_chunk(1) <= 64 && pair_chunk(2) <= 64 && pair_chunk(4) <= 64,
+              "the plan window covers the ring; a chunk is one record per lane");
 // Flags are one byte each (0 or 1), so the kernel turns each into a float coefficient with a
 // single v_cvt_f32_ubyteN.
 constexpr uint32_t kPairFwdA = 1u << 0;    // A's user row = previous pair's A result (registers)
@@ -304,7 +321,7 @@ struct PairPlan {
   int64_t noop_halves = 0;       // pair halves that are no-ops (planner padding, repeated users)
   std::vector<double> sm_bytes;  // per superstep index: bytes the sweep requests (records + in-range rows)
 };
-// The plan window must be >= 2 * kPairRing records.  substep_waves: order the cells (and
+// The plan window must be >= 2 * kPairPlanRing records.  substep_waves: order the cells (and
 // pp.waves / sub_off) per sub-step (sm, t), longest first, for the per-sub-step launches (needs a
 // uniform G); otherwise per superstep, and only the systolic tables are meaningful.
 // cell_pairs (tables only): the pair count of every cell, indexed like fp.cell_off; the records
