@@ -1362,14 +1362,11 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
         cap = std::min(cap, sweep_pair_sys_capacity(k));
         simds = std::min(simds, 4 * cus);
       }
-      // the group model's wave budget: at most two waves per CU at k <= 128, three at k = 256.  A
-      // pair step slows sharply with the waves that share its CU (its row traffic goes through the
-      // CU's one vector-memory path): NFLX 178 -> 231 ns per mixed pair from two to three waves per
-      // CU, YAHOO 301 -> 560 from three to four (profiles/r05_*_wave_trace.txt), which the model's
-      // fixed per-pair cost does not see.  Measured (profiles/r05_wave_budget.txt): NFLX 21.34 ->
-      // 21.01-21.03 ms per epoch (656 -> 512 waves), YAHOO 228.1 -> 220.8 ms (1004 -> 768), ML20M
-      // unchanged (its model optimum, 461 waves, is below the budget).
-      simds = std::min(simds, (k <= 128 ? 2 : 3) * (simds / 4));
+      // the group model's wave budget: one wave per SIMD.  (With the round-4 ring of 7 pairs a budget
+      // of two waves per CU at k <= 128 and three at k = 256 was faster -- a pair step slowed sharply
+      // with the waves sharing its CU; with the per-width rings of round 5 (plan.hpp pair_ring) the
+      // model's own choice is best again: NFLX 20.0 ms with 656 waves vs 20.24 with 512, YAHOO 223.7
+      // vs 232.0 ms with 1004 vs 768; profiles/r05_wave_budget.txt.)
       if (const std::string v = test_knob("sys_waves"); !v.empty()) simds = std::max(8, std::atoi(v.c_str()));
       if (ctx->P.fast_waves == 0 && test_knob("block_groups") != "0") {
         block_groups.assign(nb2, 0);
@@ -1434,7 +1431,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
       DeviceGuard g(s0.device);
       device_fast_schedule(s0.stream, dev_rb, ctx->rb, ctx->U, ctx->I, Gb, ctx->P.lambda,
                            static_cast<uint64_t>(ctx->P.seed) * 0x9E3779B97F4A7C15ULL + 1, fp, ctx->c, s0.index, k,
-                           dummy, 2 * kPairPlanRing, dev_pp, dev_pairs);
+                           dummy, pair_window(k), dev_pp, dev_pairs);
       dev_rb = DevRatingBlocks();
     } else {
       if (ctx->rb.urow.empty() && dev_rb.urow.get()) {  // a host-built plan after all
@@ -1444,7 +1441,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
       }
       build_fast_plan(fp, ctx->rb, ctx->U, ctx->I, ctx->G_fast, k, ctx->P.lambda,
                       static_cast<uint64_t>(ctx->P.seed) * 0x9E3779B97F4A7C15ULL + 1, dummy, nullptr,
-                      ctx->fast_pair ? 2 * kPairPlanRing : kHazardWindow, block_groups.empty() ? nullptr : &block_groups,
+                      ctx->fast_pair ? pair_window(k) : kHazardWindow, block_groups.empty() ? nullptr : &block_groups,
                       ctx->item_split, static_cast<uint32_t>(ctx->I.rows() + 1), dev_plan ? &entries : nullptr);
     }
     MF_REQUIRE(static_cast<uint64_t>(ctx->I.rows() + 1 + fp.scratch_rows) * k * 4 < (1ull << 32),
@@ -1453,7 +1450,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
       Shard& s0 = ctx->shards[0];
       DeviceGuard g(s0.device);
       clk.lap("cell order (host)");
-      device_pair_schedule(s0.stream, entries, fp, ctx->nb, ctx->c, s0.index, k, dummy, 2 * kPairPlanRing, false, dev_pp,
+      device_pair_schedule(s0.stream, entries, fp, ctx->nb, ctx->c, s0.index, k, dummy, pair_window(k), false, dev_pp,
                            dev_pairs);
       ctx->reaper.drop(entries);
     }
@@ -2670,7 +2667,7 @@ int mf_fast_plan_window(int32_t k, int32_t* window_out) {
   return guarded([&] {
     MF_REQUIRE(window_out, "null");
     const FastKernel fk = choose_fast_kernel(k);
-    *window_out = fk == FastKernel::kPair ? 2 * kPairPlanRing : kHazardWindow;
+    *window_out = fk == FastKernel::kPair ? pair_window(k) : kHazardWindow;
   });
 }
 

@@ -254,9 +254,9 @@ struct WaveDesc {
 // pair, A ends its item run, B starts one); a step whose B would repeat A's user gets a
 // no-op B.  Row fields are byte offsets, kOffOOB = no load (the row is forwarded in registers
 // or the record is a no-op) / no store.
-// The plan's hazard window is 2 * kPairPlanRing records: a user row is loaded at most kPairPlanRing
-// pairs before its update, so inside a cell a user recurs either at the next record (forwarded in
-// registers) or at least that far on.  The sweeps prefetch pair_ring(KPL) <= kPairPlanRing pairs
+// The plan's hazard window (pair_window(k) >= 2 * pair_ring(KPL) records): a user row is loaded
+// pair_ring pairs before its update, so inside a cell a user recurs either at the next record
+// (forwarded in registers) or at least that far on; kPairPlanRing bounds the ring.  The sweeps prefetch pair_ring(KPL) <= kPairPlanRing pairs
 // ahead (8 VMEM operations per pair, vmcnt <= 63), measured per row width (round 5,
 // profiles/r05_pair_ring.txt): a deeper ring is NOT faster -- the pair step is not load-latency
 // bound, and fewer rows in flight per wave leave the CU's memory path less crowded and a cell's
@@ -274,6 +274,11 @@ constexpr int pair_ring(int kpl) { return kpl == 2 ? 6 : 4; }
 constexpr int pair_chunk(int kpl) { return kpl == 2 ? 60 : 56; }
 #endif
 constexpr int pair_kpl(int k) { return k <= 64 ? 1 : k <= 128 ? 2 : 4; }
+// The plan window for k (>= 2 * pair_ring): the smallest one at k = 64 (fewer padding records:
+// ML20M 4.82 -> 4.65 ms), 2 * kPairPlanRing above (NFLX 20.3 vs 20.8 ms at 12, YAHOO 215 vs 232 ms
+// at 8: the wider window orders the cells better than the padding it adds costs;
+// profiles/r05_pair_ring.txt)
+constexpr int pair_window(int k) { return k <= 64 ? 2 * pair_ring(1) : 2 * kPairPlanRing; }
 static_assert(pair_chunk(1) % pair_ring(1) == 0 && pair_chunk(2) % pair_ring(2) == 0 &&
                   pair_chunk(4) % pair_ring(4) == 0, "ring slots must repeat every chunk");
 static_assert(pair_ring(1) <= kPairPlanRing && pair_ring(2) <= kPairPlanRing && pair_ring(4) <= kPairPlanRing &&
