@@ -24,7 +24,7 @@
 // dropped), which is also how forwarded rows and no-op records are expressed.  Rows of pair
 // j+D are loaded after the stores of pair j; the host keeps every row adjacent (forwarded in
 // registers) or at least 2D records apart inside a cell (plan window), so a prefetched row is
-// always current.  8 operations x D = 7 pairs stay under vmcnt's 63.  A cell that is a single
+// always current.  8 operations x D pairs stay under vmcnt's 63 (D = plan.hpp pair_ring: 4 or 6).  A cell that is a single
 // item run (hot items) takes a leaner loop with no item traffic at all.
 // B_f32(k) = 16k + 20 algorithmic bytes per update.
 #include <hip/hip_ext.h>
