@@ -1377,9 +1377,9 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
             std::vector<int64_t> size(nb2, 0);
             for (int64_t b = 0; b < nb2; ++b) size[b] = ctx->rb.size(b);
             gb = choose_block_groups(size, device_block_tops(s.stream, dev_rb, ctx->rb, ctx->I), ctx->nb, ctx->c,
-                                     s.index, simds);
+                                     s.index, simds, sys_cell_ns(k));
           } else {
-            gb = choose_block_groups(ctx->rb, ctx->I, ctx->c, s.index, simds, ctx->item_split);
+            gb = choose_block_groups(ctx->rb, ctx->I, ctx->c, s.index, simds, ctx->item_split, sys_cell_ns(k));
           }
           for (int64_t b = 0; b < nb2; ++b)
             if (gb[b] > 0) block_groups[b] = gb[b];

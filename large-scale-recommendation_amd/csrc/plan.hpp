@@ -361,14 +361,18 @@ void lpt_assign(const std::vector<int64_t>& load, int32_t G, std::vector<int32_t
 // time is modelled as G cells x kSysCellNs + max(block ratings / G, ratings of the block's
 // most rated item) / 2 pairs x ns per pair (no group is lighter than one item's run).
 constexpr double kSysCellNs = 6000.0;     // per-cell start, drain, hand-off and waiting (swept on NFLX + ML20M)
+// With the round-5 rings the cell cost re-swept lower at k <= 128 (profiles/r05_group_model.txt:
+// ML20M 4.65 -> 4.49 ms, NFLX 20.03 -> 19.97 ms at 5 us); k = 256 keeps 6 us (its 5-us schedule moves
+// YAHOO@0.05's RMSE past the 0.5% gate).
+constexpr double sys_cell_ns(int k) { return k <= 128 ? 5000.0 : kSysCellNs; }
 constexpr double kSysPairNs = 300.0;      // mixed-cell pair step incl. no-op halves and group imbalance (tuned)
 constexpr double kSysRunPairNs = 186.0;   // single-item-run pair step (wave trace)
 // split_run > 0: an item's run counts at most split_run ratings (hot-item replicas).
 std::vector<int32_t> choose_block_groups(const RatingBlocks& rb, const SideLayout& I, int32_t c, int32_t shard,
-                                         int32_t waves, int32_t split_run = 0);
+                                         int32_t waves, int32_t split_run = 0, double cell_ns = kSysCellNs);
 // The same model on per-block rating counts and most-rated-item counts (size / top, n*n each,
 // shard blocks only; e.g. from device histograms, kernels_plan.hip device_block_tops).
 std::vector<int32_t> choose_block_groups(const std::vector<int64_t>& size, const std::vector<int64_t>& top, int32_t nb,
-                                         int32_t c, int32_t shard, int32_t waves);
+                                         int32_t c, int32_t shard, int32_t waves, double cell_ns = kSysCellNs);
 
 }  // namespace mfhip

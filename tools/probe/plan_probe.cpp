@@ -60,12 +60,12 @@ int main(int argc, char** argv) {
       const int c = nb / G;
       std::vector<int32_t> Gall(static_cast<size_t>(nb) * nb, 0);
       for (int g = 0; g < G; ++g) {
-        const auto gb = choose_block_groups(rb, I, c, g, waves);
+        const auto gb = choose_block_groups(rb, I, c, g, waves, 0, sys_cell_ns(k));
         for (size_t b = 0; b < gb.size(); ++b) if (gb[b] > 0) Gall[b] = gb[b];
       }
       FastPlan fp;
       build_fast_plan(fp, rb, U, I, 128, k, 1.0, 0 * 0x9E3779B97F4A7C15ULL + 1, static_cast<uint32_t>(U.rows()),
-                      nullptr, 2 * kPairRing, &Gall);
+                      nullptr, pair_window(k), &Gall);
       for (int g = 0; g < G; ++g) {
         PairPlan pp;
         build_pair_plan(pp, fp, nb, c, g, k, false);
@@ -89,11 +89,11 @@ int main(int argc, char** argv) {
     }
     return 0;
   }
-  const auto Gb = choose_block_groups(rb, I, nb, 0, waves);
+  const auto Gb = choose_block_groups(rb, I, nb, 0, waves, 0, sys_cell_ns(k));
   std::printf("block groups %.3f s\n", lap());
   FastPlan fp;
   build_fast_plan(fp, rb, U, I, 128, k, 1.0, 0 * 0x9E3779B97F4A7C15ULL + 1, static_cast<uint32_t>(U.rows()), nullptr,
-                  2 * kPairRing, &Gb);
+                  pair_window(k), &Gb);
   std::printf("fast plan %.3f s\n", lap());
   PairPlan pp;
   build_pair_plan(pp, fp, nb, nb, 0, k, false);
