@@ -187,7 +187,7 @@ __device__ __forceinline__ void det_wave(const DetWave d, const uint32_t* __rest
     P[x] = ldrow<KPL>(urs, voff, live && okP[x] ? u * rowb : kOOB);
     RU[x] = ld_reg(rus, live ? u : 0u);
     if (!SINGLE || x == 0) {
-      Q[x] = ldrow<KPL>(irs, voff, live && !(x > 0 && (q & kDetKeepQ)) ? i * rowb : kOOB);
+      Q[x] = ldrow<KPL>(irs, voff, live && !(x > 0 && i == fi(x - 1)) ? i * rowb : kOOB);
       RI[x] = ld_reg(ris, live ? i : 0u);
     }
   }
@@ -211,10 +211,15 @@ __device__ __forceinline__ void det_wave(const DetWave d, const uint32_t* __rest
 #else
   auto stamp = [](int) {};
 #endif
+  // keep / defer the item row (same item as the previous / the next entry of this wave): found
+  // here from the entry fields, so the host build does not scan the entries for it
+  uint32_t prev_i = 0xFFFFFFFFu;  // the previous entry's item (none before entry 0)
   auto entry = [&](const int s, const int32_t j) {
     const int slot = s & 1;
     const uint32_t u = fu(s), qf = fq(s);
     const uint32_t i = SINGLE ? item0 : fi(s);
+    const bool keepq = !SINGLE && i == prev_i;
+    const bool deferq = !SINGLE && j + 1 < cnt && fi(s + 1) == i;
     const double r = rld(s < CH ? C0.r : C1.r, s);
     const int32_t useq = static_cast<int32_t>(qf & kDetUseqMask);
     const uint32_t u2 = fu(s + 2), q2 = fq(s + 2), u4 = fu(s + 4);
@@ -231,7 +236,7 @@ __device__ __forceinline__ void det_wave(const DetWave d, const uint32_t* __rest
       __builtin_amdgcn_s_waitcnt(0x0F70);
     }
     // 2. compute entry j (DSGDforMF.scala:405-410, the reference's rounding, no FMA)
-    if (!SINGLE && !(qf & kDetKeepQ)) {
+    if (!SINGLE && !keepq) {
 #pragma unroll
       for (int c = 0; c < KPL; ++c) q[c] = Q[slot].v[c];
     }
@@ -259,7 +264,7 @@ __device__ __forceinline__ void det_wave(const DetWave d, const uint32_t* __rest
     pv1 = useq + 1;
     // 4. entry j's stores
     strow<KPL>(urs, voff, u * rowb, pn);
-    if (!SINGLE) strow<KPL>(irs, voff, (qf & kDetDeferQ) ? kOOB : i * rowb, q);
+    if (!SINGLE) strow<KPL>(irs, voff, deferq ? kOOB : i * rowb, q);
     stamp(2);
     // 5. prefetch entry j+2 into this slot (after the stores: a reload of an item row this wave
     //    just stored sees it); its user row only if its ticket (polled at entry j-2) was ready
@@ -268,12 +273,13 @@ __device__ __forceinline__ void det_wave(const DetWave d, const uint32_t* __rest
     P[slot] = ldrow<KPL>(urs, voff, live2 && okN ? u2 * rowb : kOOB);
     RU[slot] = ld_reg(rus, live2 ? u2 : 0u);
     if (!SINGLE) {
-      Q[slot] = ldrow<KPL>(irs, voff, live2 && !(q2 & kDetKeepQ) ? i2 * rowb : kOOB);
+      Q[slot] = ldrow<KPL>(irs, voff, live2 && !(i2 == fi(s + 1)) ? i2 * rowb : kOOB);
       RI[slot] = ld_reg(ris, live2 ? i2 : 0u);
     }
     okP[slot] = okN;
     // 6. poll entry j+4's ticket (read at entry j+2)
     tk[slot] = poll_issue(trs, j + 4 < cnt ? u4 * 4u : kOOB);
+    prev_i = i;
     stamp(3);
   };
   // Full chunks run their CH entries with no exit test in between: a per-entry "j >= cnt" exit

@@ -64,7 +64,7 @@ struct DetBuf {
   hipEvent_t copied = nullptr;  // the H2D from `pin` finished (pin may be rewritten)
   hipEvent_t swept = nullptr;   // the sweep that read `dev` finished (dev may be rewritten)
   bool pending = false;         // `copied` was recorded and not yet waited for
-  int64_t n = 0, nw = 0, keeps = 0, defers = 0;
+  int64_t n = 0, nw = 0;
   DetStepScratch scratch;  // build_det_step's gathers for this slot (kept: no page faults per superstep)
 };
 
@@ -1015,7 +1015,7 @@ void det_build(mf_ctx* ctx, int64_t superstep, int slot) {
   for (auto& s : ctx->shards) {
     DetBuf& db = s.det_buf[slot];
     det_blocks(ctx, s, superstep, blocks, seeds);
-    db.n = db.nw = db.keeps = db.defers = 0;
+    db.n = db.nw = 0;
     for (int64_t b : blocks) {
       db.n += ctx->rb.size(b);
       db.nw += s.det_layout.block_waves[b];
@@ -1027,10 +1027,6 @@ void det_build(mf_ctx* ctx, int64_t superstep, int slot) {
                    reinterpret_cast<uint32_t*>(base + o.i), reinterpret_cast<uint32_t*>(base + o.qf),
                    reinterpret_cast<double*>(base + o.r)};
     build_det_step(ctx->rb, ctx->U, ctx->I, s.det_layout, blocks, seeds, ctx->P.has_seed != 0, out, &db.scratch);
-    for (int64_t x = 0; x < db.n; ++x) {
-      db.keeps += (out.qf[x] & kDetKeepQ) != 0;
-      db.defers += (out.qf[x] & kDetDeferQ) != 0;
-    }
     if (ctx->det_split) db.nw = det_slot_table(out.waves, db.nw, ctx->det_split_blocks, ctx->det_alone);
   }
 }
@@ -1129,9 +1125,10 @@ void det_run(mf_ctx* ctx, int64_t count) {
       MF_HIP(hipEventRecord(db.swept, sh.stream));
       ctx->stats.updates += db.n;
       ctx->stats.kernel_launches += 1;
-      // rows: user in + out per update, item in / out where not kept in registers; per update
-      // the 20-B entry, two lambda/omega doubles and the ticket poll + store
-      ctx->stats.moved_bytes += 8.0 * k * static_cast<double>(4 * db.n - db.keeps - db.defers) + 44.0 * db.n;
+      // rows: user in + out and item in + out per update (an upper bound: an item row kept in
+      // registers across consecutive entries of its item moves once); per update the 20-B entry,
+      // two lambda/omega doubles and the ticket poll + store
+      ctx->stats.moved_bytes += 8.0 * k * static_cast<double>(4 * db.n) + 44.0 * db.n;
     }
     ring_shift(ctx, s);
     ctx->superstep_done = s;

@@ -287,6 +287,7 @@ void build_det_layout(DetSweepLayout& L, const RatingBlocks& rb, const SideLayou
   const int64_t nb2 = static_cast<int64_t>(nb) * nb;
   L.block_waves.assign(nb2, 0);
   L.item_wave.assign(nb2, {});
+  L.wave_single.assign(nb2, {});
   // per superstep sm: the shard's blocks (p, (p+sm) mod n) share the wave budget by size
   for (int32_t sm = 0; sm < nb; ++sm) {
     int64_t total = 0;
@@ -322,13 +323,18 @@ void build_det_layout(DetSweepLayout& L, const RatingBlocks& rb, const SideLayou
     for (int32_t w = 0; w < W; ++w) heap.emplace(0, w);
     auto& iw = L.item_wave[b];
     iw.assign(ni, -1);
+    std::vector<int32_t> nitems(W, 0);
     for (int32_t it : items) {
       Load top = heap.top();
       heap.pop();
       iw[it] = top.second;
+      nitems[top.second]++;
       top.first += cnt[it];
       heap.push(top);
     }
+    auto& ws = L.wave_single[b];
+    ws.assign(W, 0);
+    for (int32_t w = 0; w < W; ++w) ws[w] = nitems[w] == 1;
   });
 }
 
@@ -495,22 +501,12 @@ void build_det_step(const RatingBlocks& rb, const SideLayout& U, const SideLayou
     }
   });
   lap(3);
-  // 5. items repeated back to back stay in registers (over all waves of the step, 64 at a time:
-  // eight blocks alone left half of the host threads idle)
-  constexpr int64_t kWaveTask = 64;
-  parallel_tasks((w0[nbk] + kWaveTask - 1) / kWaveTask, [&](int64_t task) {
-    for (int64_t wg = task * kWaveTask; wg < std::min(w0[nbk], (task + 1) * kWaveTask); ++wg) {
-      DetWave& dw = out.waves[wg];
-      const int64_t a = dw.begin, z = dw.begin + dw.count;
-      bool single = z > a;
-      for (int64_t y = a; y < z; ++y) {
-        if (y > a && out.i[y - 1] == out.i[y]) out.qf[y] |= kDetKeepQ;
-        if (y + 1 < z && out.i[y + 1] == out.i[y]) out.qf[y] |= kDetDeferQ;
-        single = single && out.i[y] == out.i[a];
-      }
-      dw.flags = single ? kDetWaveSingleItem : 0;  // the sweep's lean path (one item row, loaded and stored once)
-    }
-  });
+  // 5. a wave that holds one item of its block is a single-item wave (the layout's, static)
+  for (int64_t x = 0; x < nbk; ++x) {
+    const auto& ws = L.wave_single[blocks[x]];
+    for (int32_t w = 0; w < L.block_waves[blocks[x]]; ++w)
+      out.waves[w0[x] + w].flags = ws[w] ? kDetWaveSingleItem : 0;  // the sweep's lean / split path
+  }
   lap(4);
 }
 

@@ -127,8 +127,8 @@ void build_level_plan(const std::vector<OrderedSeq>& seqs, LevelPlan& out, std::
 // wave's entries are in increasing shuffle position, so the unfinished entry with the smallest
 // position can always run: with all waves resident the sweep cannot deadlock.
 constexpr uint32_t kDetUseqMask = (1u << 30) - 1;
-constexpr uint32_t kDetKeepQ = 1u << 30;   // same item as the wave's previous entry: row in registers
-constexpr uint32_t kDetDeferQ = 1u << 31;  // same item as the wave's next entry: no store yet
+// (round 4 also carried "same item as the previous / next entry" bits here, found by a host pass over
+// every entry; the sweep now compares the entries' items itself)
 struct DetWave {
   int64_t begin;  // first entry
   int32_t count;
@@ -141,6 +141,7 @@ static_assert(sizeof(DetWave) == 16, "DetWave is one 16-B word");
 struct DetSweepLayout {
   std::vector<int32_t> block_waves;             // n*n: waves of each rating block of this shard (0: none)
   std::vector<std::vector<int32_t>> item_wave;  // n*n: local item row of the block's item block -> wave
+  std::vector<std::vector<uint8_t>> wave_single;  // n*n: per wave of the block, 1 = it holds one item
 };
 // waves_per_superstep: budget of resident waves for one superstep of this shard; every block of a
 // superstep gets a share proportional to its ratings (>= 1, <= its distinct items).
@@ -162,7 +163,7 @@ struct DetStepOut {
   DetWave* waves;
   uint32_t* u;   // global user row
   uint32_t* i;   // global item row
-  uint32_t* qf;  // useq | kDetKeepQ | kDetDeferQ
+  uint32_t* qf;  // useq
   double* r;
 };
 int64_t det_build_phase_ns(int phase);  // MFHIP_TIMING diagnostics of build_det_step (0..4)
