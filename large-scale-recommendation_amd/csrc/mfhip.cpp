@@ -915,6 +915,13 @@ void ring_shift(mf_ctx* ctx, int64_t superstep) {
 struct DetOffsets {
   size_t waves, u, i, qf, r, total;
 };
+// The pair sweep's plan window for k (plan.hpp pair_window); MFHIP_TEST pair_window=N overrides
+// it for the window sweeps (clamped to the ring's minimum 2 * pair_ring).
+int32_t plan_window(int32_t k) {
+  if (const std::string v = test_knob("pair_window"); !v.empty())
+    return std::max<int32_t>(2 * pair_ring(pair_kpl(k)), std::atoi(v.c_str()));
+  return pair_window(k);
+}
 int64_t det_slot_room(int64_t nw);
 DetOffsets det_offsets(int64_t n, int64_t nw) {
   auto up = [](size_t x) { return (x + 255) & ~static_cast<size_t>(255); };
@@ -1428,7 +1435,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
       DeviceGuard g(s0.device);
       device_fast_schedule(s0.stream, dev_rb, ctx->rb, ctx->U, ctx->I, Gb, ctx->P.lambda,
                            static_cast<uint64_t>(ctx->P.seed) * 0x9E3779B97F4A7C15ULL + 1, fp, ctx->c, s0.index, k,
-                           dummy, pair_window(k), dev_pp, dev_pairs);
+                           dummy, plan_window(k), dev_pp, dev_pairs);
       dev_rb = DevRatingBlocks();
     } else {
       if (ctx->rb.urow.empty() && dev_rb.urow.get()) {  // a host-built plan after all
@@ -1438,7 +1445,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
       }
       build_fast_plan(fp, ctx->rb, ctx->U, ctx->I, ctx->G_fast, k, ctx->P.lambda,
                       static_cast<uint64_t>(ctx->P.seed) * 0x9E3779B97F4A7C15ULL + 1, dummy, nullptr,
-                      ctx->fast_pair ? pair_window(k) : kHazardWindow, block_groups.empty() ? nullptr : &block_groups,
+                      ctx->fast_pair ? plan_window(k) : kHazardWindow, block_groups.empty() ? nullptr : &block_groups,
                       ctx->item_split, static_cast<uint32_t>(ctx->I.rows() + 1), dev_plan ? &entries : nullptr);
     }
     MF_REQUIRE(static_cast<uint64_t>(ctx->I.rows() + 1 + fp.scratch_rows) * k * 4 < (1ull << 32),
@@ -1447,7 +1454,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
       Shard& s0 = ctx->shards[0];
       DeviceGuard g(s0.device);
       clk.lap("cell order (host)");
-      device_pair_schedule(s0.stream, entries, fp, ctx->nb, ctx->c, s0.index, k, dummy, pair_window(k), false, dev_pp,
+      device_pair_schedule(s0.stream, entries, fp, ctx->nb, ctx->c, s0.index, k, dummy, plan_window(k), false, dev_pp,
                            dev_pairs);
       ctx->reaper.drop(entries);
     }
@@ -2664,7 +2671,7 @@ int mf_fast_plan_window(int32_t k, int32_t* window_out) {
   return guarded([&] {
     MF_REQUIRE(window_out, "null");
     const FastKernel fk = choose_fast_kernel(k);
-    *window_out = fk == FastKernel::kPair ? pair_window(k) : kHazardWindow;
+    *window_out = fk == FastKernel::kPair ? plan_window(k) : kHazardWindow;
   });
 }
 

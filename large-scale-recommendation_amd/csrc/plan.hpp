@@ -275,11 +275,11 @@ constexpr int pair_ring(int kpl) { return kpl == 2 ? 6 : 4; }
 constexpr int pair_chunk(int kpl) { return kpl == 2 ? 60 : 56; }
 #endif
 constexpr int pair_kpl(int k) { return k <= 64 ? 1 : k <= 128 ? 2 : 4; }
-// The plan window for k (>= 2 * pair_ring): the smallest one at k = 64 (fewer padding records:
-// ML20M 4.82 -> 4.65 ms), 2 * kPairPlanRing above (NFLX 20.3 vs 20.8 ms at 12, YAHOO 215 vs 232 ms
-// at 8: the wider window orders the cells better than the padding it adds costs;
-// profiles/r05_pair_ring.txt)
-constexpr int pair_window(int k) { return k <= 64 ? 2 * pair_ring(1) : 2 * kPairPlanRing; }
+// The plan window for k (>= 2 * pair_ring; MFHIP_TEST pair_window=N overrides it): 10 records at
+// k = 64 (ML20M 4.82 / 4.49 / 4.45 / 4.64 ms at 14 / 8 / 10 / 12), 2 * kPairPlanRing = 14 above (NFLX
+// 20.8 / 20.05 / 20.25 / 20.5 ms at 12 / 14 / 16 / 18, YAHOO 232 vs 215 ms at 8 vs 14; a wider window
+// pads more, a narrower one orders the cells worse; profiles/r05_pair_ring.txt)
+constexpr int pair_window(int k) { return k <= 64 ? 10 : 2 * kPairPlanRing; }
 static_assert(pair_chunk(1) % pair_ring(1) == 0 && pair_chunk(2) % pair_ring(2) == 0 &&
                   pair_chunk(4) % pair_ring(4) == 0, "ring slots must repeat every chunk");
 static_assert(pair_ring(1) <= kPairPlanRing && pair_ring(2) <= kPairPlanRing && pair_ring(4) <= kPairPlanRing &&
