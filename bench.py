@@ -325,7 +325,8 @@ def online_leg(ctx, stream, a, batch=ONLINE_BATCH):
     ctx.set_profiling(False)
     dtype = "f64" if ctx.params.mode == L.MODE_DETERMINISTIC_F64 else "f32"
     k = ctx.params.num_factors
-    kernel = "k_online_f32" if dtype == "f32" and k <= 256 else "k_online_sweep"
+    kernel = ("k_online_f32" if k <= 256 else "k_online_sweep") if dtype == "f32" else \
+        ("k_det_sweep_split" if k in (64, 128, 256) else "k_online_sweep")
     kms_med = float(np.median(kms))
     return {"metric": "online ratings/s (1M-rating micro-batches on the fitted model)",
             "value": round(float(np.median(rates)), 1), "unit": "ratings/s", "min": round(float(min(rates)), 1),

@@ -44,6 +44,12 @@ struct OnlineSweepScratch;
 void online_sweep_plan(hipStream_t st, OnlineSweepScratch& sc, const uint32_t* eu, const uint32_t* ei,
                        const double* er, int64_t n, uint32_t W, uint32_t user_rows, uint32_t item_rows,
                        DetEntry* ent, uint32_t* useq, int64_t* wbeg, int32_t* touched);
+// The f64 online batch on the deterministic sweep (kernels_detsweep.hip): the plan's entries as
+// SoA arrays in sc.soa (eu / ei / eq / er, padded by kDetPad) and one DetWave per wave (single-item
+// flag from the entries) into waves[0 .. W).  Call after online_sweep_plan on the same scratch.
+void online_det_entries(hipStream_t st, OnlineSweepScratch& sc, const DetEntry* ent, const uint32_t* useq,
+                        const int64_t* wbeg, int64_t n, uint32_t W, uint32_t*& eu, uint32_t*& ei, uint32_t*& eq,
+                        double*& er, struct DetWave* waves);
 // Per-rating records of the online operators (mf_online_update_out), f64 rows of k at
 // [src[entry] * k]: kOutNext = (user', item') (FlinkOnlineMF.scala:131-135), kOutDelta =
 // (user + deltaItem, deltaItem) with user before the update (PSOfflineOnlineMF.scala:174-176).
@@ -121,6 +127,12 @@ void launch_det_sweep(hipStream_t st, const DetWave* waves, int nw, const uint32
 // slot 0 is a single-item wave runs it as a chain wave plus a helper wave (slot 1 ignored, by
 // convention kDetWaveHelper); any other slot is an ordinary k_det_sweep2 wave (count 0: none).
 int det_split_capacity(int k);
+// The same split sweep with SGDUpdater.nextFactors' update (the online f64 batch, no lambda /
+// omega); k = 64, 128, 256 (capacity 0 otherwise).
+int online_det_capacity(int k);
+void launch_online_det(hipStream_t st, const DetWave* slots, int nslots, const uint32_t* eu, const uint32_t* ei,
+                       const uint32_t* eq, const double* er, double* U, double* I, uint64_t u_bytes, uint64_t i_bytes,
+                       int k, double eta, int32_t* ticket, int32_t* err, hipEvent_t ev0, hipEvent_t ev1);
 void launch_det_sweep_split(hipStream_t st, const DetWave* slots, int nslots, const uint32_t* eu, const uint32_t* ei,
                             const uint32_t* eq, const double* er, double* U, double* I, uint64_t u_bytes,
                             uint64_t i_bytes, const double* regU, const double* regI, int k, double eta,

@@ -139,6 +139,31 @@ __device__ __forceinline__ void wait_vmcnt() {
 //     DPP broadcasts, ~6.6 instead of ~11-13 cycles per f64 add), else through LDS (seq_fold).
 constexpr int kDetChunk = 16;
 
+// The update rule (AR) of an entry, both in the reference's rounding (no FMA):
+//   kArDsgd: DSGDforMF.scala:405-410, lambda / omega per row (regU / regI);
+//   kArNext: SGDUpdater.nextFactors (core/FactorUpdater.scala:37-45), the online micro-batch:
+//            le = lr * e, p' = p + le * q, q' = q + le * p (old rows), no regularisation.  Its
+//            lambda / omega buffers are empty ranges: the loads still issue (so every vmcnt the
+//            hand-off counts is the same instruction count) but return 0 and touch no memory.
+constexpr int kArDsgd = 0, kArNext = 1;
+template <int AR>
+constexpr uint64_t reg_bytes() {
+  return AR == kArDsgd ? 0xFFFFF000ull : 0ull;
+}
+// (p', q') from the rows before the update, e = r - p.q
+template <int AR>
+__device__ __forceinline__ void update_pair(double p, double q, double e, double eta, double ru, double ri,
+                                            double& pn, double& qn) {
+  if constexpr (AR == kArDsgd) {
+    pn = p - eta * (ru * p - e * q);  // :407-408
+    qn = q - eta * (ri * q - e * p);  // :409-410 (old p)
+  } else {
+    const double le = eta * e;  // learningRate * e * i == (learningRate * e) * i
+    pn = p + le * q;
+    qn = q + le * p;
+  }
+}
+
 
 // One wave's entries.  SINGLE (DetWave::flags & kDetWaveSingleItem): every entry updates the same
 // item, so its row and lambda / omega are loaded once and stored once at the end, and an entry moves
@@ -148,7 +173,7 @@ constexpr int kDetChunk = 16;
 //   SINGLE:  publish 1 | user store KPL                 | user load KPL,                ru 1,       poll 1
 // NW = the operations issued after entry j-2's stores up to entry j's publish: entry j-2's loads plus
 // all of entry j-1's: generic (2 KPL + 3) + (4 KPL + 4) = 6 KPL + 7, SINGLE (KPL + 2) + (2 KPL + 3) = 3 KPL + 5.
-template <int KPL, bool FULL, bool SINGLE>
+template <int KPL, bool FULL, bool SINGLE, int AR = kArDsgd>
 __device__ __forceinline__ void det_wave(const DetWave d, const uint32_t* __restrict__ eu, const uint32_t* __restrict__ ei,
                                          const uint32_t* __restrict__ eq, const double* __restrict__ er, double* U,
                                          double* I, uint64_t u_bytes, uint64_t i_bytes, const double* __restrict__ regU,
@@ -160,7 +185,7 @@ __device__ __forceinline__ void det_wave(const DetWave d, const uint32_t* __rest
   const int32_t cnt = d.count;  // 32-bit: the entry tests are scalar compares, not 64-bit VALU ones
   const __amdgpu_buffer_rsrc_t urs = raw_rsrc(U, u_bytes), irs = raw_rsrc(I, i_bytes);
   const __amdgpu_buffer_rsrc_t trs = raw_rsrc(ticket, 0xFFFFF000ull);  // offsets are user rows * 4
-  const __amdgpu_buffer_rsrc_t rus = raw_rsrc(regU, 0xFFFFF000ull), ris = raw_rsrc(regI, 0xFFFFF000ull);
+  const __amdgpu_buffer_rsrc_t rus = raw_rsrc(regU, reg_bytes<AR>()), ris = raw_rsrc(regI, reg_bytes<AR>());
   uint32_t voff[KPL];
 #pragma unroll
   for (int c = 0; c < KPL; ++c) voff[c] = lane + 64 * c < k ? static_cast<uint32_t>(lane + 64 * c) * 8u : 0x80000000u;
@@ -251,10 +276,7 @@ __device__ __forceinline__ void det_wave(const DetWave d, const uint32_t* __rest
     const double e = r - dot;  // :405
     stamp(1);
 #pragma unroll
-    for (int c = 0; c < KPL; ++c) {
-      pn[c] = P[slot].v[c] - eta * (ru * P[slot].v[c] - e * q[c]);  // :407-408
-      q[c] = q[c] - eta * (ri * q[c] - e * P[slot].v[c]);           // :409-410 (old p)
-    }
+    for (int c = 0; c < KPL; ++c) update_pair<AR>(P[slot].v[c], q[c], e, eta, ru, ri, pn[c], q[c]);
     // 3. entry j-2's stores have landed (NW younger operations may still fly): publish its ticket
     wait_vmcnt<NW>();
     publish(trs, pend0, pv0);
@@ -399,13 +421,13 @@ __device__ __forceinline__ void link_wait(F v, int32_t want, int32_t* err, int l
   }
 }
 
-template <int KPL>
+template <int KPL, int AR>
 __device__ __forceinline__ void det_chain(const DetWave d, const uint32_t* __restrict__ ei, const double* I,
                                           uint64_t i_bytes, const double* __restrict__ regI, double eta,
                                           DetLink<KPL>& L, int32_t* err, int lane) {
   const int32_t cnt = d.count;
   const __amdgpu_buffer_rsrc_t irs = raw_rsrc(I, i_bytes);
-  const __amdgpu_buffer_rsrc_t ris = raw_rsrc(regI, 0xFFFFF000ull);
+  const __amdgpu_buffer_rsrc_t ris = raw_rsrc(regI, reg_bytes<AR>());
   uint32_t voff[KPL];
 #pragma unroll
   for (int c = 0; c < KPL; ++c) voff[c] = static_cast<uint32_t>(lane + 64 * c) * 8u;
@@ -454,7 +476,10 @@ __device__ __forceinline__ void det_chain(const DetWave d, const uint32_t* __res
     const double dot = seq_fold_dpp<double, KPL>(pr);
     const double e = R[s] - dot;  // :405
 #pragma unroll
-    for (int c = 0; c < KPL; ++c) q[c] = q[c] - eta * (ri * q[c] - e * P[s][c]);  // :409-410
+    for (int c = 0; c < KPL; ++c) {
+      if constexpr (AR == kArDsgd) q[c] = q[c] - eta * (ri * q[c] - e * P[s][c]);  // :409-410
+      else q[c] = q[c] + (eta * e) * P[s][c];  // nextFactors (update_pair's le * p)
+    }
     le[(j % kLinkR) * 64 + lane] = e;
     ldone[lane] = j + 1;
     // entry j + 2's operands into this register slot
@@ -476,7 +501,7 @@ __device__ __forceinline__ void det_chain(const DetWave d, const uint32_t* __res
   }
 }
 
-template <int KPL>
+template <int KPL, int AR>
 __device__ __forceinline__ void det_helper(const DetWave d, const uint32_t* __restrict__ eu, const uint32_t* __restrict__ ei,
                                            const uint32_t* __restrict__ eq, const double* __restrict__ er, double* U,
                                            double* I, uint64_t u_bytes, uint64_t i_bytes,
@@ -493,7 +518,7 @@ __device__ __forceinline__ void det_helper(const DetWave d, const uint32_t* __re
   const int32_t cnt = d.count;
   const __amdgpu_buffer_rsrc_t urs = raw_rsrc(U, u_bytes), irs = raw_rsrc(I, i_bytes);
   const __amdgpu_buffer_rsrc_t trs = raw_rsrc(ticket, 0xFFFFF000ull);
-  const __amdgpu_buffer_rsrc_t rus = raw_rsrc(regU, 0xFFFFF000ull), ris = raw_rsrc(regI, 0xFFFFF000ull);
+  const __amdgpu_buffer_rsrc_t rus = raw_rsrc(regU, reg_bytes<AR>()), ris = raw_rsrc(regI, reg_bytes<AR>());
   uint32_t voff[KPL];
 #pragma unroll
   for (int c = 0; c < KPL; ++c) voff[c] = static_cast<uint32_t>(lane + 64 * c) * 8u;
@@ -574,10 +599,7 @@ __device__ __forceinline__ void det_helper(const DetWave d, const uint32_t* __re
     link_get_row<KPL>(lp + (sl * 64 + lane) * KPL, p);
     // c. the user row (:407-408) and this wave's copy of the item row (:409-410, old p)
 #pragma unroll
-    for (int c = 0; c < KPL; ++c) {
-      pn[c] = p[c] - eta * (ru * p[c] - e * q[c]);
-      q[c] = q[c] - eta * (ri * q[c] - e * p[c]);
-    }
+    for (int c = 0; c < KPL; ++c) update_pair<AR>(p[c], q[c], e, eta, ru, ri, pn[c], q[c]);
     // d. entry j-2's stores have landed: publish its ticket; entry j's stores
     wait_vmcnt<NW>();
     publish(trs, pend0, pv0);
@@ -637,7 +659,7 @@ done:
 
 // Blocks of two wave slots: slots[2b + w] is wave w's descriptor.  A single-item wave's slot 1 is
 // its helper (kDetWaveHelper: the same entries); any other slot runs det_wave (count 0: nothing).
-template <int KPL>
+template <int KPL, int AR = kArDsgd>
 __global__ __launch_bounds__(128) void k_det_sweep_split(const DetWave* __restrict__ slots, const uint32_t* __restrict__ eu,
                                                          const uint32_t* __restrict__ ei, const uint32_t* __restrict__ eq,
                                                          const double* __restrict__ er, double* U, double* I,
@@ -657,13 +679,13 @@ __global__ __launch_bounds__(128) void k_det_sweep_split(const DetWave* __restri
       link.done[lane] = 0;
     }
     __syncthreads();
-    if (w == 0) det_chain<KPL>(d0, ei, I, i_bytes, regI, eta, link, err, lane);
-    else det_helper<KPL>(d0, eu, ei, eq, er, U, I, u_bytes, i_bytes, regU, regI, eta, ticket, link, err, lane);
+    if (w == 0) det_chain<KPL, AR>(d0, ei, I, i_bytes, regI, eta, link, err, lane);
+    else det_helper<KPL, AR>(d0, eu, ei, eq, er, U, I, u_bytes, i_bytes, regU, regI, eta, ticket, link, err, lane);
     return;
   }
   if (d.count == 0) return;
-  det_wave<KPL, true, false>(d, eu, ei, eq, er, U, I, u_bytes, i_bytes, regU, regI, 64 * KPL, eta, ticket, nullptr, err,
-                             nullptr, lane);
+  det_wave<KPL, true, false, AR>(d, eu, ei, eq, er, U, I, u_bytes, i_bytes, regU, regI, 64 * KPL, eta, ticket, nullptr,
+                                 err, nullptr, lane);
 }
 
 template <int KPL, bool FULL>
@@ -695,12 +717,12 @@ int det_capacity(bool full) {
   return st == hipSuccess ? cus * per_cu : 0;
 }
 
-template <int KPL>
+template <int KPL, int AR = kArDsgd>
 int det_split_cap() {
   int dev = 0, cus = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_det_sweep_split<KPL>, 128, 0) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_det_sweep_split<KPL, AR>, 128, 0) != hipSuccess) return 0;
   return 2 * cus * per_cu;
 }
 
@@ -726,6 +748,31 @@ void launch_det_sweep_split(hipStream_t st, const DetWave* slots, int nslots, co
   else if (k == 128) MF_DETS(2);
   else if (k == 256) MF_DETS(4);
 #undef MF_DETS
+}
+
+// The online f64 micro-batch (SGDUpdater.nextFactors in sequence order, core/FactorUpdater.scala:37-45)
+// on the deterministic sweep: the same per-item waves, per-user tickets and hand-off, kArNext's
+// update rule.  Slots as launch_det_sweep_split's; k = 64, 128, 256 only (0: not supported).
+int online_det_capacity(int k) {
+  if (k == 64) return det_split_cap<1, kArNext>();
+  if (k == 128) return det_split_cap<2, kArNext>();
+  if (k == 256) return det_split_cap<4, kArNext>();
+  return 0;
+}
+
+void launch_online_det(hipStream_t st, const DetWave* slots, int nslots, const uint32_t* eu, const uint32_t* ei,
+                       const uint32_t* eq, const double* er, double* U, double* I, uint64_t u_bytes, uint64_t i_bytes,
+                       int k, double eta, int32_t* ticket, int32_t* err, hipEvent_t ev0, hipEvent_t ev1) {
+  if (nslots <= 0) return;
+  const dim3 g(static_cast<unsigned>(nslots / 2)), b(128);
+  const double* none = nullptr;  // kArNext: no lambda / omega (empty buffer ranges)
+#define MF_ONDET(KPL)                                                                                                 \
+  hipExtLaunchKernelGGL((k_det_sweep_split<KPL, kArNext>), g, b, 0, st, ev0, ev1, 0, slots, eu, ei, eq, er, U, I,     \
+                        u_bytes, i_bytes, none, none, eta, ticket, err)
+  if (k == 64) MF_ONDET(1);
+  else if (k == 128) MF_ONDET(2);
+  else if (k == 256) MF_ONDET(4);
+#undef MF_ONDET
 }
 
 // the co-resident wave count of the instance launch_det_sweep picks for k

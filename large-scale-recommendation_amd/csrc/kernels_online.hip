@@ -6,8 +6,12 @@
 //   tickets : stable sort of (user row, x) -> an update's ticket value is its rank inside its
 //             user's run = the number of earlier updates of that user (the kernel waits until
 //             the user's ticket word reaches it)
-//   waves   : stable sort of (item row mod W, x) -> wave w's updates in sequence order; every
-//             update of an item lands in one wave, so the item's order is the sequence order
+//   waves   : stable sort of (wave of the item row, x) -> wave w's updates in sequence order; every
+//             update of an item lands in one wave, so the item's order is the sequence order.  An
+//             item with at least twice the mean wave load gets a wave of its own (waves 0 .. H-1,
+//             in whatever order the atomics hand them out: any item -> wave map gives the same
+//             factors), the others go to H + row mod (W - H).  The hottest items' chains bound the
+//             launch, so they should not share their wave with other items' updates.
 //   wbeg[w] : first position of wave w (lower bound in the sorted wave keys), wbeg[W] = n
 //   touched : distinct user rows (run heads of the user sort) and item rows (run heads of a
 //             key-only item sort) of the batch (UpdateSeparatedHashMap.updates,
@@ -34,11 +38,34 @@ unsigned grid_for(int64_t n) {
   return static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((n + kThreads - 1) / kThreads, 1 << 16)));
 }
 
+__global__ void k_item_count(const uint32_t* __restrict__ ei, int64_t n, uint32_t* __restrict__ cnt) {
+  for (int64_t x = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; x < n;
+       x += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    atomicAdd(cnt + ei[x], 1u);
+}
+
+// iwave[i] = the own wave of a heavy item row (count >= T, the first H to claim one), else -1
+__global__ void k_heavy(const uint32_t* __restrict__ cnt, uint32_t rows, uint32_t T, uint32_t H,
+                        uint32_t* __restrict__ nheavy, int32_t* __restrict__ iwave) {
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < rows;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    int32_t w = -1;
+    if (cnt[i] >= T) {
+      const uint32_t h = atomicAdd(nheavy, 1u);
+      if (h < H) w = static_cast<int32_t>(h);
+    }
+    iwave[i] = w;
+  }
+}
+
 __global__ void k_keys(const uint32_t* __restrict__ eu, const uint32_t* __restrict__ ei, int64_t n, uint32_t W,
-                       uint32_t* __restrict__ wkey, int32_t* __restrict__ iota) {
+                       uint32_t H, const int32_t* __restrict__ iwave, uint32_t* __restrict__ wkey,
+                       int32_t* __restrict__ iota) {
   for (int64_t x = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; x < n;
        x += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    wkey[x] = ei[x] % W;
+    const uint32_t i = ei[x];
+    const int32_t w = H > 0 ? iwave[i] : -1;
+    wkey[x] = w >= 0 ? static_cast<uint32_t>(w) : H + i % (W - H);
     iota[x] = static_cast<int32_t>(x);
   }
 }
@@ -95,7 +122,57 @@ int bits_for(uint64_t v) {  // radix bits that hold every key < v
   return b;
 }
 
+// The deterministic sweep's entry arrays (SoA, padded with kDetPad zero entries: the sweep reads
+// whole chunks past a wave's end) from the plan's wave-ordered entries
+__global__ void k_det_soa(const DetEntry* __restrict__ ent, const uint32_t* __restrict__ useq, int64_t n,
+                          int64_t total, uint32_t* __restrict__ eu, uint32_t* __restrict__ ei, uint32_t* __restrict__ eq,
+                          double* __restrict__ er) {
+  for (int64_t y = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; y < total;
+       y += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const bool live = y < n;
+    eu[y] = live ? ent[y].u : 0u;
+    ei[y] = live ? ent[y].i : 0u;
+    eq[y] = live ? useq[y] : 0u;
+    er[y] = live ? ent[y].r : 0.0;
+  }
+}
+
+// multi[w] = 1 when wave w holds more than one item (wkey = the sorted wave keys: wave of position y)
+__global__ void k_multi(const DetEntry* __restrict__ ent, const uint32_t* __restrict__ wkey,
+                        const int64_t* __restrict__ wbeg, int64_t n, int32_t* __restrict__ multi) {
+  for (int64_t y = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; y < n;
+       y += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const uint32_t w = wkey[y];
+    if (ent[y].i != ent[wbeg[w]].i) multi[w] = 1;
+  }
+}
+
+__global__ void k_det_waves(const int64_t* __restrict__ wbeg, const int32_t* __restrict__ multi, uint32_t W,
+                            DetWave* __restrict__ waves) {
+  for (int64_t w = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; w < W;
+       w += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    waves[w] = DetWave{wbeg[w], static_cast<int32_t>(wbeg[w + 1] - wbeg[w]), multi[w] ? 0 : kDetWaveSingleItem};
+}
+
 }  // namespace
+
+void online_det_entries(hipStream_t st, OnlineSweepScratch& sc, const DetEntry* ent, const uint32_t* useq,
+                        const int64_t* wbeg, int64_t n, uint32_t W, uint32_t*& eu, uint32_t*& ei, uint32_t*& eq,
+                        double*& er, DetWave* waves) {
+  const int64_t total = n + kDetPad;
+  sc.soa.alloc(static_cast<size_t>(total) * 20);
+  er = sc.soa.as<double>();
+  eu = reinterpret_cast<uint32_t*>(er + total);
+  ei = eu + total;
+  eq = ei + total;
+  hipLaunchKernelGGL(k_det_soa, dim3(grid_for(total)), dim3(kThreads), 0, st, ent, useq, n, total, eu, ei, eq, er);
+  sc.multi.alloc(static_cast<size_t>(W) * 4);
+  MF_HIP(hipMemsetAsync(sc.multi.get(), 0, static_cast<size_t>(W) * 4, st));
+  hipLaunchKernelGGL(k_multi, dim3(grid_for(n)), dim3(kThreads), 0, st, ent, sc.wkey2.as<uint32_t>(), wbeg, n,
+                     sc.multi.as<int32_t>());
+  hipLaunchKernelGGL(k_det_waves, dim3(grid_for(W)), dim3(kThreads), 0, st, wbeg, sc.multi.as<int32_t>(), W, waves);
+  MF_HIP(hipGetLastError());
+}
 
 void online_sweep_plan(hipStream_t st, OnlineSweepScratch& sc, const uint32_t* eu, const uint32_t* ei,
                        const double* er, int64_t n, uint32_t W, uint32_t user_rows, uint32_t item_rows,
@@ -111,8 +188,21 @@ void online_sweep_plan(hipStream_t st, OnlineSweepScratch& sc, const uint32_t* e
   sc.head.alloc(n * 4);
   sc.start.alloc(n * 4);
   sc.ticket.alloc(n * 4);
-  hipLaunchKernelGGL(k_keys, dim3(grid_for(n)), dim3(kThreads), 0, st, eu, ei, n, W, sc.wkey.as<uint32_t>(),
-                     sc.iota.as<int32_t>());
+  // heavy items: at least twice the mean wave load, at most a quarter of the waves
+  const uint32_t H = W >= 8 ? W / 4 : 0;
+  const uint32_t T = static_cast<uint32_t>(std::max<int64_t>(2, (2 * n + W - 1) / W));
+  if (H > 0) {
+    sc.icnt.alloc(static_cast<size_t>(std::max<uint32_t>(item_rows, 1)) * 4);
+    sc.iwave.alloc(static_cast<size_t>(std::max<uint32_t>(item_rows, 1)) * 4);
+    sc.nheavy.alloc(4);
+    MF_HIP(hipMemsetAsync(sc.icnt.get(), 0, static_cast<size_t>(item_rows) * 4, st));
+    MF_HIP(hipMemsetAsync(sc.nheavy.get(), 0, 4, st));
+    hipLaunchKernelGGL(k_item_count, dim3(grid_for(n)), dim3(kThreads), 0, st, ei, n, sc.icnt.as<uint32_t>());
+    hipLaunchKernelGGL(k_heavy, dim3(grid_for(item_rows)), dim3(kThreads), 0, st, sc.icnt.as<uint32_t>(), item_rows, T,
+                       H, sc.nheavy.as<uint32_t>(), sc.iwave.as<int32_t>());
+  }
+  hipLaunchKernelGGL(k_keys, dim3(grid_for(n)), dim3(kThreads), 0, st, eu, ei, n, W, H,
+                     H > 0 ? sc.iwave.as<int32_t>() : nullptr, sc.wkey.as<uint32_t>(), sc.iota.as<int32_t>());
   size_t tb = 0;
   const int ub = bits_for(user_rows), wb = bits_for(W);
   // tickets

@@ -1820,10 +1820,20 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
   // 0.5e8 ratings/s end to end
   const bool outs = uout || iout;
   int cap = 0;
+  // f64 at k = 64 / 128 / 256: the deterministic sweep's kernel with nextFactors' update (split
+  // hot-item chains, kernels_detsweep.hip), while every row offset fits its 32-bit buffer offsets
+  // (rows after this batch's new ids at most rows + n); MFHIP_TEST online_kernel=ticket keeps
+  // k_online_sweep
+  bool det_online = false;
   if (n > 0 && !outs && test_knob("online_kernel") != "level") {
     DeviceGuard g(s.device);
+    const auto fits = [&](int64_t rows) { return static_cast<double>(rows + n) * k * 8.0 <= 4294963200.0; };
+    det_online = ctx->f64 && test_knob("online_kernel") != "ticket" && online_det_capacity(k) > 0 &&
+                 fits(ctx->U.rows()) && fits(ctx->I.rows());
     // 0 (occupancy query failed): the level replay
-    cap = !ctx->f64 && online_f32_supports(k) ? online_f32_capacity(k) : online_sweep_capacity(k, ctx->f64);
+    cap = det_online ? online_det_capacity(k)
+          : !ctx->f64 && online_f32_supports(k) ? online_f32_capacity(k) : online_sweep_capacity(k, ctx->f64);
+    if (cap == 0) det_online = false;
   }
   // the sweep in arrival order takes the rows straight into its pinned upload buffer (user rows,
   // item rows, ratings: 16 B per rating), with no staging pass; otherwise they go to on_ur / on_ir
@@ -1934,6 +1944,7 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
         order.insert(order.end(), c.begin(), c.end());
       }
   }
+  std::vector<DetWave> det_slots;  // the f64 sweep's slot table (alive until the sync below)
   if (cap > 0) {
     // one persistent launch (k_online_sweep): items spread over the waves, each wave's updates in
     // sequence order, and per update the number of earlier updates of its user (its ticket value)
@@ -1985,6 +1996,27 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
                         reinterpret_cast<const uint32_t*>(s.det_dev.as<char>() + ebytes), s.uf.as<float>(),
                         s.itf.as<float>(), s.uf.bytes(), s.itf.bytes(), k, ctx->P.online_learning_rate,
                         sc.uticket.as<int32_t>(), sc.dummy.as<int32_t>(), sc.err.as<int32_t>(), t.start(), t.stop());
+    } else if (det_online) {
+      // the wave table goes through the host once (W descriptors): det_slot_table pairs each
+      // single-item wave with its helper and gives the longest chains a CU each
+      uint32_t *eu = nullptr, *ei = nullptr, *eq = nullptr;
+      double* er = nullptr;
+      sc.waves.alloc(static_cast<size_t>(det_slot_room(W)) * sizeof(DetWave));
+      online_det_entries(s.stream, sc, s.det_dev.as<DetEntry>(),
+                         reinterpret_cast<const uint32_t*>(s.det_dev.as<char>() + ebytes), sc.wbeg.as<int64_t>(), n,
+                         W32, eu, ei, eq, er, sc.waves.as<DetWave>());
+      det_slots.resize(static_cast<size_t>(det_slot_room(W)));
+      MF_HIP(hipMemcpyAsync(det_slots.data(), sc.waves.get(), static_cast<size_t>(W) * sizeof(DetWave),
+                            hipMemcpyDeviceToHost, s.stream));
+      MF_HIP(hipStreamSynchronize(s.stream));
+      const int64_t nslots = det_slot_table(det_slots.data(), W, cap / 2, true);
+      MF_HIP(hipMemcpyAsync(sc.waves.get(), det_slots.data(), static_cast<size_t>(nslots) * sizeof(DetWave),
+                            hipMemcpyHostToDevice, s.stream));
+      LaunchTimer t(s, ctx->profiling, true);
+      launch_online_det(s.stream, det_slots.empty() ? nullptr : sc.waves.as<DetWave>(), static_cast<int>(nslots), eu, ei,
+                        eq, er, s.uf.as<double>(), s.itf.as<double>(), s.uf.bytes(), s.itf.bytes(), k,
+                        ctx->P.online_learning_rate, sc.uticket.as<int32_t>(), sc.err.as<int32_t>(), t.start(),
+                        t.stop());
     } else {
       LaunchTimer t(s, ctx->profiling);
       launch_online_sweep(s.stream, static_cast<int>(W), sc.wbeg.as<int64_t>(), s.det_dev.as<DetEntry>(),

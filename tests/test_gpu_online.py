@@ -176,12 +176,15 @@ def test_per_rating_outputs_bit_exact(flavour, name):
 
 
 @pytest.mark.parametrize("mode,k", [(L.MODE_FAST_F32, 128), (L.MODE_DETERMINISTIC_F64, 200), (L.MODE_FAST_F32, 40),
-                                    (L.MODE_DETERMINISTIC_F64, 128), (L.MODE_DETERMINISTIC_F64, 64)])
+                                    (L.MODE_DETERMINISTIC_F64, 128), (L.MODE_DETERMINISTIC_F64, 64),
+                                    (L.MODE_DETERMINISTIC_F64, 256)])
 def test_online_sweep_equals_level_replay(monkeypatch, mode, k):
-    """The one-launch online sweep (the default: per-item waves, per-user tickets, k_online_sweep,
-    its wave lists and tickets built on the device by kernels_online.hip) gives the factors of the
-    level-by-level replay (MFHIP_TEST online_kernel=level) bit for bit, including a hot item, repeated
-    (user, item) pairs and ids first seen in a later batch."""
+    """The one-launch online sweep (the default: per-item waves, heavy items on waves of their own,
+    per-user tickets, its wave lists and tickets built on the device by kernels_online.hip) gives the
+    factors of the level-by-level replay (MFHIP_TEST online_kernel=level) bit for bit, including a
+    hot item, repeated (user, item) pairs and ids first seen in a later batch.  f64 at k = 64 / 128 /
+    256 runs on the deterministic split sweep (k_det_sweep_split with nextFactors' update); its
+    predecessor k_online_sweep (online_kernel=ticket) is checked as well."""
     rng = np.random.default_rng(7)
     n = 120000
     u = rng.integers(0, 5000, n).astype(np.int32)
@@ -189,7 +192,8 @@ def test_online_sweep_equals_level_replay(monkeypatch, mode, k):
     i[::37] = 3  # a hot item
     r = rng.integers(1, 6, n).astype(np.float64)
     res = {}
-    for kern in ("level", "sweep"):
+    kerns = ("level", "sweep", "ticket") if mode == L.MODE_DETERMINISTIC_F64 else ("level", "sweep")
+    for kern in kerns:
         set_knob(monkeypatch, "online_kernel", kern)
         p = L.default_params()
         p.num_factors, p.mode, p.online_learning_rate = k, mode, 0.01
@@ -197,14 +201,16 @@ def test_online_sweep_equals_level_replay(monkeypatch, mode, k):
             for s in range(0, n, 40000):
                 ctx.online_update(u[s:s + 40000], i[s:s + 40000], r[s:s + 40000], L.ONLINE_NEXT_FACTORS)
             res[kern] = (ctx.factors(0), ctx.factors(1))
-    for side in (0, 1):
-        assert np.array_equal(res["level"][side][0], res["sweep"][side][0])
-        assert np.array_equal(res["level"][side][1], res["sweep"][side][1])
+    for kern in kerns[1:]:
+        for side in (0, 1):
+            assert np.array_equal(res["level"][side][0], res[kern][side][0])
+            assert np.array_equal(res["level"][side][1], res[kern][side][1])
 
 
-@pytest.mark.parametrize("k", [32, 64])  # 64: every lane in use, the deferred-ticket instance
+# (f32, 64): every lane in use, the deferred-ticket instance; (f64, 64): the deterministic split sweep
+@pytest.mark.parametrize("mode,k", [(L.MODE_FAST_F32, 32), (L.MODE_FAST_F32, 64), (L.MODE_DETERMINISTIC_F64, 64)])
 @pytest.mark.parametrize("shape", ["one", "few", "one_user", "one_item", "spark"])
-def test_online_sweep_edge_batches(monkeypatch, shape, k):
+def test_online_sweep_edge_batches(monkeypatch, shape, mode, k):
     """Edge batches of the device-built sweep plan (kernels_online.hip) against the level replay,
     bit for bit: a single rating, fewer ratings than waves, one user across every wave (a ticket
     chain through all of them), one item (one wave holds the whole batch), and the Spark-sweep
@@ -223,7 +229,7 @@ def test_online_sweep_edge_batches(monkeypatch, shape, k):
     for kern in ("level", "sweep"):
         set_knob(monkeypatch, "online_kernel", kern)
         p = L.default_params()
-        p.num_factors, p.mode, p.online_learning_rate = k, L.MODE_FAST_F32, 0.01
+        p.num_factors, p.mode, p.online_learning_rate = k, mode, 0.01
         with mfhip.Context(p) as ctx:
             for s in range(0, n, 10000):
                 bu, bi = u[s:s + 10000], i[s:s + 10000]
