@@ -178,7 +178,7 @@ def det_kernel_name(k):
     MFHIP_TEST det_split=0."""
     knobs = dict(x.split("=", 1) for x in os.environ.get("MFHIP_TEST", "").split(",") if "=" in x)
     if k in (64, 128, 256) and knobs.get("det_split") != "0":
-        return "k_det_sweep_split"
+        return f"k_det_sweep_split<{k // 64}, 0>"  # <KPL, 0>: the DSGD instance (<KPL, 1>: online f64)
     return "k_det_sweep2"
 
 
@@ -326,7 +326,7 @@ def online_leg(ctx, stream, a, batch=ONLINE_BATCH):
     dtype = "f64" if ctx.params.mode == L.MODE_DETERMINISTIC_F64 else "f32"
     k = ctx.params.num_factors
     kernel = ("k_online_f32" if k <= 256 else "k_online_sweep") if dtype == "f32" else \
-        ("k_det_sweep_split" if k in (64, 128, 256) else "k_online_sweep")
+        (f"k_det_sweep_split<{k // 64}, 1>" if k in (64, 128, 256) else "k_online_sweep")
     kms_med = float(np.median(kms))
     return {"metric": "online ratings/s (1M-rating micro-batches on the fitted model)",
             "value": round(float(np.median(rates)), 1), "unit": "ratings/s", "min": round(float(min(rates)), 1),

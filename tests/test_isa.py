@@ -9,7 +9,7 @@ each kernel's control-flow graph:
 * every progress / ticket word of the persistent sweeps is stored only after the row stores it
   publishes have landed: the hand-counted `s_waitcnt vmcnt(N)` in front of it must cover them on
   every path of the BUILT code (k_sweep_pair_sys: every earlier store; k_det_sweep2 and the f64
-  k_online_sweep, which publish a ticket one or two entries late: every store older than the
+  k_online_sweep and the split sweep k_det_sweep_split (DSGD and online instances), which publish a ticket one or two entries late: every store older than the
   previous ticket store).
 
 A fixture library (tests/isa_fixtures.hip) with one known-bad and one known-good instance of
@@ -56,7 +56,8 @@ def _one(kern, part):
 
 
 def test_library_holds_the_sweep_kernels(kern):
-    for part in ("k_sweep_pair_sys", "k_det_sweep2", "k_online_sweep", "k_sweep_pair", "k_predict"):
+    for part in ("k_sweep_pair_sys", "k_det_sweep2", "k_det_sweep_splitILi2ELi0E", "k_det_sweep_splitILi2ELi1E", "k_online_sweep",
+                 "k_sweep_pair", "k_predict"):
         assert any(part in n for n in kern), part
 
 

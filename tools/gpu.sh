@@ -11,7 +11,7 @@
 #   bench:<tag>:<bench.py args>            one bench line -> <tag>.json, summary printed
 #   ab:<tag>:<reps>:<envA>|<envB>[|...]:<bench.py args>
 #                                          alternating A/B of environment settings on the bench line
-#   prof:<tag>:<kernel>:<cfg>:<mode>:<rank>:<bench.py args>   (<kernel> may be k1=sfx1,k2=sfx2,...:
+#   prof:<tag>:<kernel>:<cfg>:<mode>:<rank>:<bench.py args>   (<kernel> may be k1=sfx1;k2=sfx2;...:
 #                                          one traffic_<cfg>_<sfx>.json per kernel of the same run)
 #                                          rocprofv3 --kernel-trace --stats, then separate --pmc FETCH_SIZE
 #                                          and --pmc WRITE_SIZE passes, summarised per launch of <kernel>
@@ -91,9 +91,10 @@ for step in "$@"; do
       cd "$R"
       stats=$(ls "$O"/kt_$tag/*kernel_stats.csv | head -1)
       cp "$stats" "$O/stats_$tag.csv"
-      # <kernel> may list several kernels of the same run, kernel=suffix,...: each is summarised to
-      # traffic_<cfg>_<suffix>.json (mode = suffix); a bare kernel name writes traffic_<tag>.json
-      IFS=',' read -ra KS <<< "$kern"
+      # <kernel> may list several kernels of the same run, kernel=suffix;...: each is summarised to
+      # traffic_<cfg>_<suffix>.json (mode = suffix); a bare kernel name writes traffic_<tag>.json.  A
+      # kernel may carry its template arguments (k_det_sweep_split<2, 1>: that instance only)
+      IFS=';' read -ra KS <<< "$kern"
       for ks in "${KS[@]}"; do
         kn=${ks%%=*}; sfx=${ks#*=}
         if [ "$sfx" = "$ks" ]; then out="$O/traffic_$tag.json"; md=$mode; else out="$O/traffic_${cfg}_$sfx.json"; md=$sfx; fi
