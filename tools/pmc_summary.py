@@ -20,7 +20,7 @@ def kernel_match(name, kernel):
     """rocprof kernel names are demangled signatures: match the template name exactly, or, for a
     kernel given with its template arguments ("k_det_sweep_split<2, 1>"), that instance only."""
     if "<" in kernel:
-        return name.split("(")[0].replace(" ", "").endswith(kernel.replace(" ", ""))
+        return kernel.replace(" ", "") + "(" in name.replace(" ", "")
     return f"{kernel}<" in name or name.split("(")[0].endswith(kernel)
 
 
