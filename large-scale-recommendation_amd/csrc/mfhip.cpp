@@ -2009,7 +2009,7 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
       MF_HIP(hipMemcpyAsync(det_slots.data(), sc.waves.get(), static_cast<size_t>(W) * sizeof(DetWave),
                             hipMemcpyDeviceToHost, s.stream));
       MF_HIP(hipStreamSynchronize(s.stream));
-      const int64_t nslots = det_slot_table(det_slots.data(), W, cap / 2, true);
+      const int64_t nslots = det_slot_table(det_slots.data(), W, cap / 2, test_knob("det_alone") != "0");
       MF_HIP(hipMemcpyAsync(sc.waves.get(), det_slots.data(), static_cast<size_t>(nslots) * sizeof(DetWave),
                             hipMemcpyHostToDevice, s.stream));
       LaunchTimer t(s, ctx->profiling, true);
