@@ -8,9 +8,9 @@
 //             the user's ticket word reaches it)
 //   waves   : stable sort of (wave of the item row, x) -> wave w's updates in sequence order; every
 //             update of an item lands in one wave, so the item's order is the sequence order.  An
-//             item with at least twice the mean wave load gets a wave of its own (waves 0 .. H-1,
-//             in whatever order the atomics hand them out: any item -> wave map gives the same
-//             factors), the others go to H + row mod (W - H).  The hottest items' chains bound the
+//             item with at least the mean wave load gets a wave of its own (waves 0 .. H-1 in
+//             count-descending order, so the hottest always get one; any item -> wave map gives
+//             the same factors), the others go to H + row mod (W - H).  The hottest items' chains bound the
 //             launch, so they should not share their wave with other items' updates.
 //   wbeg[w] : first position of wave w (lower bound in the sorted wave keys), wbeg[W] = n
 //   touched : distinct user rows (run heads of the user sort) and item rows (run heads of a
@@ -26,6 +26,9 @@
 #include <hipcub/device/device_scan.hpp>
 
 #include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <string>
 
 #include "common.hpp"
 #include "kernels.hpp"
@@ -44,18 +47,20 @@ __global__ void k_item_count(const uint32_t* __restrict__ ei, int64_t n, uint32_
     atomicAdd(cnt + ei[x], 1u);
 }
 
-// iwave[i] = the own wave of a heavy item row (count >= T, the first H to claim one), else -1
-__global__ void k_heavy(const uint32_t* __restrict__ cnt, uint32_t rows, uint32_t T, uint32_t H,
-                        uint32_t* __restrict__ nheavy, int32_t* __restrict__ iwave) {
+__global__ void k_iota_rows(uint32_t rows, int32_t* __restrict__ iota, int32_t* __restrict__ iwave) {
   for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < rows;
        i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    int32_t w = -1;
-    if (cnt[i] >= T) {
-      const uint32_t h = atomicAdd(nheavy, 1u);
-      if (h < H) w = static_cast<int32_t>(h);
-    }
-    iwave[i] = w;
+    iota[i] = static_cast<int32_t>(i);
+    iwave[i] = -1;
   }
+}
+
+// iwave[item] = rank r of a heavy item row in count-descending order (count >= T, r < H)
+__global__ void k_heavy(const uint32_t* __restrict__ cnt_sorted, const int32_t* __restrict__ item_sorted, uint32_t H,
+                        uint32_t T, int32_t* __restrict__ iwave) {
+  for (int64_t r = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; r < H;
+       r += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    if (cnt_sorted[r] >= T) iwave[item_sorted[r]] = static_cast<int32_t>(r);
 }
 
 __global__ void k_keys(const uint32_t* __restrict__ eu, const uint32_t* __restrict__ ei, int64_t n, uint32_t W,
@@ -64,7 +69,7 @@ __global__ void k_keys(const uint32_t* __restrict__ eu, const uint32_t* __restri
   for (int64_t x = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; x < n;
        x += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     const uint32_t i = ei[x];
-    const int32_t w = H > 0 ? iwave[i] : -1;
+    const int32_t w = iwave ? iwave[i] : -1;
     wkey[x] = w >= 0 ? static_cast<uint32_t>(w) : H + i % (W - H);
     iota[x] = static_cast<int32_t>(x);
   }
@@ -188,22 +193,41 @@ void online_sweep_plan(hipStream_t st, OnlineSweepScratch& sc, const uint32_t* e
   sc.head.alloc(n * 4);
   sc.start.alloc(n * 4);
   sc.ticket.alloc(n * 4);
-  // heavy items: at least twice the mean wave load, at most a quarter of the waves
-  const uint32_t H = W >= 8 ? W / 4 : 0;
-  const uint32_t T = static_cast<uint32_t>(std::max<int64_t>(2, (2 * n + W - 1) / W));
-  if (H > 0) {
-    sc.icnt.alloc(static_cast<size_t>(std::max<uint32_t>(item_rows, 1)) * 4);
-    sc.iwave.alloc(static_cast<size_t>(std::max<uint32_t>(item_rows, 1)) * 4);
-    sc.nheavy.alloc(4);
-    MF_HIP(hipMemsetAsync(sc.icnt.get(), 0, static_cast<size_t>(item_rows) * 4, st));
-    MF_HIP(hipMemsetAsync(sc.nheavy.get(), 0, 4, st));
-    hipLaunchKernelGGL(k_item_count, dim3(grid_for(n)), dim3(kThreads), 0, st, ei, n, sc.icnt.as<uint32_t>());
-    hipLaunchKernelGGL(k_heavy, dim3(grid_for(item_rows)), dim3(kThreads), 0, st, sc.icnt.as<uint32_t>(), item_rows, T,
-                       H, sc.nheavy.as<uint32_t>(), sc.iwave.as<int32_t>());
+  // heavy items: at least the mean wave load, at most a quarter of the waves (MFHIP_TEST
+  // online_heavy=m: m times the mean instead, 0: none; online_heavy_cap=d: at most W/d -- the A/B
+  // switches, profiles/r05_online_heavy_ab.txt)
+  double mult = 1.0;
+  if (const std::string v = test_knob("online_heavy"); !v.empty()) mult = std::atof(v.c_str());
+  uint32_t cap_div = 4;
+  if (const std::string v = test_knob("online_heavy_cap"); !v.empty()) cap_div = std::max(2, std::atoi(v.c_str()));
+  const uint32_t H = W >= 8 && mult > 0.0 ? W / cap_div : 0;
+  const uint32_t T = static_cast<uint32_t>(std::max<double>(2.0, std::ceil(mult * static_cast<double>(n) / W)));
+  size_t tb = 0;
+  if (H > 0 && item_rows > 0) {
+    // the H most-rated items (ties by row) that reach T, by a descending radix sort of the counts
+    const size_t ib = static_cast<size_t>(item_rows) * 4;
+    sc.icnt.alloc(2 * ib);  // counts, then the sorted counts
+    sc.iwave.alloc(ib);
+    sc.nheavy.alloc(2 * ib);  // row iota, then the rows in count order
+    uint32_t* cnt = sc.icnt.as<uint32_t>();
+    int32_t* rows = sc.nheavy.as<int32_t>();
+    MF_HIP(hipMemsetAsync(cnt, 0, ib, st));
+    hipLaunchKernelGGL(k_item_count, dim3(grid_for(n)), dim3(kThreads), 0, st, ei, n, cnt);
+    hipLaunchKernelGGL(k_iota_rows, dim3(grid_for(item_rows)), dim3(kThreads), 0, st, item_rows, rows,
+                       sc.iwave.as<int32_t>());
+    const int ni = static_cast<int>(item_rows), cb = bits_for(static_cast<uint64_t>(n) + 1);
+    MF_HIP(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tb, cnt, cnt + item_rows, rows, rows + item_rows, ni, 0,
+                                                        cb, st));
+    sc.tmp.alloc(std::max<size_t>(tb, 256));
+    MF_HIP(hipcub::DeviceRadixSort::SortPairsDescending(sc.tmp.get(), tb, cnt, cnt + item_rows, rows, rows + item_rows,
+                                                        ni, 0, cb, st));
+    const uint32_t Hn = std::min<uint32_t>(H, item_rows);
+    hipLaunchKernelGGL(k_heavy, dim3(grid_for(Hn)), dim3(kThreads), 0, st, cnt + item_rows, rows + item_rows, Hn, T,
+                       sc.iwave.as<int32_t>());
   }
   hipLaunchKernelGGL(k_keys, dim3(grid_for(n)), dim3(kThreads), 0, st, eu, ei, n, W, H,
-                     H > 0 ? sc.iwave.as<int32_t>() : nullptr, sc.wkey.as<uint32_t>(), sc.iota.as<int32_t>());
-  size_t tb = 0;
+                     H > 0 && item_rows > 0 ? sc.iwave.as<int32_t>() : nullptr, sc.wkey.as<uint32_t>(),
+                     sc.iota.as<int32_t>());
   const int ub = bits_for(user_rows), wb = bits_for(W);
   // tickets
   MF_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, eu, sc.ukey.as<uint32_t>(), sc.iota.as<int32_t>(),
