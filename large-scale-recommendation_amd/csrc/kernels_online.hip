@@ -208,9 +208,9 @@ void online_sweep_plan(hipStream_t st, OnlineSweepScratch& sc, const uint32_t* e
     const size_t ib = static_cast<size_t>(item_rows) * 4;
     sc.icnt.alloc(2 * ib);  // counts, then the sorted counts
     sc.iwave.alloc(ib);
-    sc.nheavy.alloc(2 * ib);  // row iota, then the rows in count order
+    sc.irows.alloc(2 * ib);  // row iota, then the rows in count order
     uint32_t* cnt = sc.icnt.as<uint32_t>();
-    int32_t* rows = sc.nheavy.as<int32_t>();
+    int32_t* rows = sc.irows.as<int32_t>();
     MF_HIP(hipMemsetAsync(cnt, 0, ib, st));
     hipLaunchKernelGGL(k_item_count, dim3(grid_for(n)), dim3(kThreads), 0, st, ei, n, cnt);
     hipLaunchKernelGGL(k_iota_rows, dim3(grid_for(item_rows)), dim3(kThreads), 0, st, item_rows, rows,
