@@ -48,6 +48,9 @@ def parse():
                     help="ONLINE leg (BASELINE config 5): 1M-rating micro-batches applied to the fitted model (0 = off)")
     ap.add_argument("--det-epochs", type=int, default=2,
                     help="deterministic-f64 leg (the reference's exact order) on the same data: timed epochs (0 = off)")
+    ap.add_argument("--ml20m-epochs", type=int, default=9,
+                    help="ML20M leg (BASELINE config 2, full size, fast f32, k=64) beside the NFLX line: timed "
+                         "epochs (0 = off; only with --config NFLX on one GPU)")
     ap.add_argument("--item-split", type=int, default=0,
                     help="fast mode experiment: hot-item replicas (MFHIP_ITEM_SPLIT), max ratings per item chain "
                          "per rating block (0 = off)")
@@ -125,6 +128,86 @@ def pmc_traffic(a, k, groups, kernel, launch_us, tag=None):
             return None, None
         return rec["bytes_per_launch"], os.path.relpath(path, ROOT)
     return None, None
+
+
+MALL_BYTES = 256 * 2**20  # MI355X_MICROARCH.md: 256-MiB Infinity Cache (MALL) on the die
+
+
+def fetch_calibration():
+    """The committed FETCH_SIZE / WRITE_SIZE calibration of the sweeps' access shape (512-B rows as
+    64 lanes x 8 B, random rows of a slab past the MALL, sc1; tools/micro/fetch_calib.hip,
+    tools/pmc_calib.py): {read_ratio, write_ratio, source} or None.  The ratio is raw counter bytes
+    over known bytes, so the true bytes are counter / ratio."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_fetch_calib.json")))
+    if not paths:
+        return None
+    rec = json.load(open(paths[-1]))
+    cases = {c["case"]: c for c in rec.get("cases", [])}
+    rd, wr = cases.get("read_sc1_3GiB"), cases.get("write_sc1_3GiB")
+    if not rd or not wr or not rd.get("fetch_ratio_raw") or not wr.get("write_ratio_raw"):
+        return None
+    return {"read_ratio": rd["fetch_ratio_raw"], "write_ratio": wr["write_ratio_raw"],
+            "source": os.path.relpath(paths[-1], ROOT)}
+
+
+def traffic_level(k, users, dtype_bytes=4):
+    """What the PMC bytes measure: FETCH_SIZE / WRITE_SIZE are the L2's memory-side (fabric)
+    requests, Infinity-Cache (MALL) hits included (MI355X_MICROARCH.md, HBM section), so when the
+    user slab fits the MALL the fraction is a fabric-traffic fraction, not an HBM one."""
+    slab = (users + 2) * k * dtype_bytes
+    return {"traffic_level": "l2-fabric (MALL hits included)", "user_slab_bytes": slab, "mall_bytes": MALL_BYTES,
+            "user_slab_fits_mall": slab <= MALL_BYTES}
+
+
+def fast_roofline(a, k, groups, st_p, prof_epochs, world, users):
+    """Roofline of the fast sweep: a replay of prof_epochs epochs with a start/stop event pair on
+    every sweep launch (on the library's stream; for the pair kernel recorded by the dispatch packet
+    itself).  Headline: the committed PMC traffic of the same kernel (FETCH_SIZE x2 + WRITE_SIZE per
+    launch) over the event-timed launch; beside it the bytes the kernel requests (mf_stats.moved_bytes,
+    counted from the device plan), SURVEY 8d's per-update model (16k+20 B, which charges an item row
+    per update the kernel keeps in registers through a run, so it can exceed 1) and the PMC bytes
+    re-corrected with the measured calibration of this access shape (fetch_calibration)."""
+    from mfhip import _lib as L
+    if st_p["kernel_ms"] <= 0:
+        return None
+    bpu = 16 * k + 20 if a.mode == "fast" else 32 * k + 24
+    launches = st_p["kernel_launches"]
+    ksec = st_p["kernel_ms"] / 1e3
+    achieved = st_p["moved_bytes"] / ksec / 1e9  # GB/s, this rank's sweep kernel
+    kname = L.lib().mf_fast_kernel_name(k).decode() if a.mode == "fast" else det_kernel_name(k)
+    launch_us = round(st_p["kernel_ms"] * 1e3 / max(launches, 1), 2)
+    # the committed PMC summaries are one-GPU runs: a rank of an N-GPU ring runs other launches
+    traffic, traffic_src = pmc_traffic(a, k, groups, kname, launch_us) if world == 1 else (None, None)
+    launch_s = st_p["kernel_ms"] / max(launches, 1) / 1e3
+    tr_gbs = traffic / launch_s / 1e9 if traffic else None
+    alg_gbs = st_p["algorithmic_bytes"] / ksec / 1e9
+    head = tr_gbs if tr_gbs is not None else achieved
+    roof = {"bound": "hbm", "achieved": round(head, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(head / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kname,
+            "achieved_source": "PMC traffic (FETCH_SIZE x2 + WRITE_SIZE) per launch / event-timed launch"
+            if tr_gbs is not None else "requested bytes per launch / event-timed launch (no current PMC summary)",
+            "bytes_per_launch": round(st_p["moved_bytes"] / max(launches, 1)),
+            "bytes_source": "mf_stats.moved_bytes: in-range row loads/stores + schedule records of the device plan",
+            "requested_achieved": round(achieved, 1), "requested_frac": round(achieved / HBM_PEAK_GBS, 4),
+            "avg_launch_us": launch_us, "launches": launches, "profiled_epochs": prof_epochs,
+            "traffic_source": traffic_src, "algorithmic_bytes_per_update": bpu,
+            "algorithmic_achieved": round(alg_gbs, 1), "algorithmic_frac": round(alg_gbs / HBM_PEAK_GBS, 4),
+            "algorithmic_note": "SURVEY 8d charges an item row read+write per update; the sweep keeps the item "
+                                "row in registers through a run, so this can exceed 1 (not an HBM fraction)",
+            "traffic_frac": round(tr_gbs / HBM_PEAK_GBS, 4) if tr_gbs is not None else None,
+            "kernel_ms_per_epoch": round(st_p["kernel_ms"] / max(prof_epochs, 1), 3)}
+    roof.update(traffic_level(k, users, 4 if a.mode == "fast" else 8))
+    cal = fetch_calibration()
+    if traffic and cal:
+        # the summary's bytes are FETCH_SIZE x2 + WRITE_SIZE; undo the x2 and divide each side by the
+        # ratio measured for 8-B/lane random-row accesses
+        rec = json.load(open(os.path.join(ROOT, traffic_src)))
+        fetch_raw = rec["fetch_bytes_per_launch"] / 2.0
+        corr = fetch_raw / cal["read_ratio"] + rec["write_bytes_per_launch"] / cal["write_ratio"]
+        roof.update({"traffic_calibrated": round(corr), "calibrated_frac": round(corr / launch_s / 1e9 / HBM_PEAK_GBS, 4),
+                     "calibration": cal})
+    return roof
 
 
 def cpu_model() -> str:
@@ -206,6 +289,51 @@ def det_roofline(a, k, sp):
             "traffic_frac": round(tr_gbs / HBM_PEAK_GBS, 4) if tr_gbs is not None else None}
 
 
+def block_update_bench(train, k, nb, det_launch_us, reps=3):
+    """mf_block_update on one NFLX rating block (the Flink-resident updateLocalFactors,
+    DSGDforMF.scala:378-418): the training ratings of users u % nb == 0 and items i % nb == 0 (a
+    1/nb x 1/nb cell of the matrix, the size of one rating block), local indices, omegas counted over
+    the whole training split, random factors.  Timed end to end (host shuffle + gather, H2D of the
+    block's factor rows, one persistent split-sweep launch, D2H) and the launch alone (events);
+    beside them the block's longest item chain, which bounds the launch, and the det superstep's
+    per-block share (its launch over the nb blocks it runs at once)."""
+    import numpy as np
+    import mfhip
+    from mfhip import _lib as L
+    tu, ti, tr = train
+    sel = (tu % nb == 0) & (ti % nb == 0)
+    uu, uidx = np.unique(tu[sel], return_inverse=True)
+    ii, iidx = np.unique(ti[sel], return_inverse=True)
+    r = tr[sel]
+    uom = np.bincount(tu)[uu].astype(np.int32)
+    iom = np.bincount(ti)[ii].astype(np.int32)
+    rng = np.random.default_rng(5)
+    users, items = rng.random((len(uu), k)) * 0.1, rng.random((len(ii), k)) * 0.1
+    p = L.default_params()
+    p.num_factors = k
+    walls, kms = [], []
+    with mfhip.Context(p) as ctx:
+        for rep in range(reps + 1):
+            ctx.reset_stats()
+            ctx.set_profiling(True)
+            t0 = time.perf_counter()
+            mfhip.block_update(r, uidx.astype(np.int32), iidx.astype(np.int32), users, uom, items, iom, k, rep, 0, 0,
+                               0.001, 0, 0.0, 1.0, ctx=ctx)
+            dt = time.perf_counter() - t0
+            ctx.set_profiling(False)
+            if rep:
+                walls.append(dt)
+                kms.append(ctx.stats()["kernel_ms"])
+    chain = int(np.bincount(iidx).max())
+    return {"ratings": int(len(r)), "users": int(len(uu)), "items": int(len(ii)), "k": k,
+            "wall_ms_median": round(1e3 * float(np.median(walls)), 3),
+            "kernel_ms_median": round(float(np.median(kms)), 3), "longest_item_chain": chain,
+            "det_superstep_block_share_ms": round(det_launch_us / 1e3 / nb, 3) if det_launch_us else None,
+            "note": "one persistent k_det_sweep_split launch per call, bitwise the oracle "
+                    "(tests/test_gpu_dsgd.py test_block_update_1m_hot_block_bit_exact); the launch is bounded by "
+                    "the block's longest item chain (its updates are sequential, DSGDforMF.scala:395-415)"}
+
+
 def det_leg(a, k, nb, train, test, ref, stream):
     """The deterministic f64 mode on the same data: DSGDforMF.scala:378-418's exact update order
     (JVM shuffle, F2J ddot fold, no FMA), one persistent sweep per superstep.  Timed epochs after
@@ -249,6 +377,8 @@ def det_leg(a, k, nb, train, test, ref, stream):
         cold_updates = ctx.stats()["updates"]
         rmse, _ = ctx.rmse(*test)
         online = online_leg(ctx, stream, a) if stream is not None else None
+    launch_us = sp["kernel_ms"] * 1e3 / max(sp["kernel_launches"], 1)
+    blk = block_update_bench(train, k, nb, launch_us)
     return {"metric": "SGD rating updates/sec, deterministic f64 (the reference's exact update order)",
             "value": round(st["updates"] / el, 1), "unit": "updates/s", "dtype": "f64", "epochs": a.det_epochs,
             "ms_per_step": round(el * 1e3 / a.det_epochs, 3), "kernel": det_kernel_name(k),
@@ -260,7 +390,59 @@ def det_leg(a, k, nb, train, test, ref, stream):
             "cold_note": "restart + 10 epochs + sync from a cold host pipeline (no superstep built ahead)",
             "rmse": round(rmse, 9), "rmse_ref": round(ref["oracle_rmse"], 9) if ref else None,
             "rmse_equal_to_ref": (abs(rmse - ref["oracle_rmse"]) <= 1e-12 * ref["oracle_rmse"]) if ref else None,
-            "online": online}  # moved to the top-level "online" block by main()
+            "block_update": blk, "online": online}  # online: moved to the top-level "online" block by main()
+
+
+def ml20m_leg(a):
+    """BASELINE config 2 at full size beside the headline: ML20M-shaped synthetic (138k x 27k x 20M),
+    fast f32, k = 64, numBlocks 8 (mfhip.synth.CONFIGS) on the same GPU, after the NFLX context is
+    closed.  Timed epochs after one warmup epoch, the same profiled replay and roofline as the
+    headline (PMC summary profiles/r*_traffic_ML20M_fast.json), and the held-out RMSE after exactly
+    10 epochs against the f64 oracle's on the same data (tests/golden/rmse_ref.json)."""
+    import mfhip
+    from mfhip import _lib as L
+    from mfhip import synth
+    ma = argparse.Namespace(**{**vars(a), "config": "ML20M", "mode": "fast", "traffic_json": None})
+    nu, ni, nr, k, nb = synth.CONFIGS["ML20M"]
+    nu, ni, nr = max(1, int(nu * a.scale)), max(1, int(ni * a.scale)), max(1, int(nr * a.scale))
+    (tu, ti, tr), (eu, ei, er) = synth.generate(nu, ni, nr).split()
+    p = L.default_params()
+    p.num_factors, p.num_blocks, p.seed, p.has_seed = k, nb, 0, 1
+    p.iterations = 10
+    p.mode = L.MODE_FAST_F32
+    with mfhip.Context(p) as ctx:
+        t0 = time.time()
+        ctx.prepare(tu, ti, tr)
+        ctx.sync()
+        t_prep = time.time() - t0
+        ctx.run(nb)
+        ctx.sync()
+        ctx.reset_stats()
+        t0 = time.perf_counter()
+        ctx.run(a.ml20m_epochs * nb)
+        ctx.sync()
+        el = time.perf_counter() - t0
+        st = ctx.stats()
+        prof_epochs = min(a.ml20m_epochs, 2)
+        ctx.reset_stats()
+        ctx.set_profiling(True)
+        ctx.run(prof_epochs * nb)
+        ctx.sync()
+        ctx.set_profiling(False)
+        st_p = ctx.stats()
+        ctx.restart()
+        ctx.run(10 * nb)
+        rmse, _ = ctx.rmse(eu, ei, er)
+    ref = rmse_reference(ma, (tu, ti, tr, eu, ei, er))
+    return {"metric": "SGD rating updates/sec, ML20M-shaped (BASELINE config 2), fast f32, rank 64, 1 GPU",
+            "value": round(st["updates"] / el, 1), "unit": "updates/s", "dtype": "f32", "epochs": a.ml20m_epochs,
+            "ms_per_step": round(el * 1e3 / a.ml20m_epochs, 3), "groups": st["groups"], "pad_records": st["pads"],
+            "config": {"users": nu, "items": ni, "ratings": nr, "train_ratings": int(len(tr)), "rank": k,
+                       "num_blocks": nb},
+            "roofline": fast_roofline(ma, k, st["groups"], st_p, prof_epochs, 1, nu),
+            "rmse": round(rmse, 6), "rmse_epochs": 10, "rmse_ref": round(ref["oracle_rmse"], 6) if ref else None,
+            "rmse_rel": round((rmse - ref["oracle_rmse"]) / ref["oracle_rmse"], 5) if ref else None,
+            "prepare_s": round(t_prep, 2)}
 
 
 ONLINE_BATCH = 1_000_000
@@ -426,37 +608,7 @@ def main():
     ref = rmse_reference(a, (tu, ti, tr, eu, ei, er)) if D.rank == 0 else None
 
     value = updates / elapsed
-    bpu = 16 * k + 20 if a.mode == "fast" else 32 * k + 24
-    roof = None
-    if st_p["kernel_ms"] > 0:
-        launches = st_p["kernel_launches"]
-        ksec = st_p["kernel_ms"] / 1e3
-        achieved = st_p["moved_bytes"] / ksec / 1e9  # GB/s, this rank's sweep kernel
-        kname = L.lib().mf_fast_kernel_name(k).decode() if a.mode == "fast" else det_kernel_name(k)
-        launch_us = round(st_p["kernel_ms"] * 1e3 / max(launches, 1), 2)
-        # the committed PMC summaries are one-GPU runs: a rank of an N-GPU ring runs other launches
-        traffic, traffic_src = pmc_traffic(a, k, st["groups"], kname, launch_us) if D.world == 1 else (None, None)
-        tr_gbs = traffic / (st_p["kernel_ms"] / max(launches, 1) / 1e3) / 1e9 if traffic else None
-        alg_gbs = st_p["algorithmic_bytes"] / ksec / 1e9
-        # headline: the HBM bytes the counters measured (PMC) over the launch time; beside it the
-        # bytes the kernel requests (moved_bytes) and SURVEY 8d's per-update model, labelled
-        head = tr_gbs if tr_gbs is not None else achieved
-        roof = {"bound": "hbm", "achieved": round(head, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(head / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kname,
-                "achieved_source": "PMC traffic (FETCH_SIZE x2 + WRITE_SIZE) per launch / event-timed launch"
-                if tr_gbs is not None else "requested bytes per launch / event-timed launch (no current PMC summary)",
-                "bytes_per_launch": round(st_p["moved_bytes"] / max(launches, 1)),
-                "bytes_source": "mf_stats.moved_bytes: in-range row loads/stores + schedule records of the device plan",
-                "requested_achieved": round(achieved, 1), "requested_frac": round(achieved / HBM_PEAK_GBS, 4),
-                "avg_launch_us": round(st_p["kernel_ms"] * 1e3 / max(launches, 1), 2),
-                "launches": launches, "profiled_epochs": prof_epochs, "traffic_source": traffic_src,
-                "algorithmic_bytes_per_update": bpu,
-                "algorithmic_achieved": round(alg_gbs, 1),
-                "algorithmic_frac": round(alg_gbs / HBM_PEAK_GBS, 4),
-                "algorithmic_note": "SURVEY 8d charges an item row read+write per update; the sweep keeps the item "
-                                    "row in registers through a run, so this can exceed 1 (not an HBM fraction)",
-                "traffic_frac": round(tr_gbs / HBM_PEAK_GBS, 4) if tr_gbs is not None else None,
-                "kernel_ms_per_epoch": round(st_p["kernel_ms"] / prof_epochs, 3)}
+    roof = fast_roofline(a, k, st["groups"], st_p, prof_epochs, D.world, int(nu * a.scale))
 
     online = None
     stream = online_stream(a, synth, nu, ni) if D.world == 1 and a.online_batches > 0 else None
@@ -468,6 +620,11 @@ def main():
         det = det_leg(a, k, nb, (tu, ti, tr), (eu, ei, er), ref, stream)
         if online is not None and det.get("online"):
             online["f64"] = det.pop("online")
+
+    ml20m = None
+    if D.world == 1 and a.config == "NFLX" and a.mode == "fast" and a.ml20m_epochs > 0:
+        ctx.close()  # (closed already when the det leg ran)
+        ml20m = ml20m_leg(a)
 
     cpu = None
     if D.rank == 0 and D.world == 1 and not a.no_cpu_baseline:
@@ -490,7 +647,7 @@ def main():
             "rmse_rel": round((rmse - ref["oracle_rmse"]) / ref["oracle_rmse"], 5) if ref else None,
             "rmse_ref_source": "tests/golden/rmse_ref.json (tools/rmse_parity.py, oracle f64, same data sha256)"
                                if ref else None,
-            "roofline": roof, "cpu_baseline": cpu, "online": online, "deterministic": det,
+            "roofline": roof, "cpu_baseline": cpu, "online": online, "deterministic": det, "ml20m": ml20m,
             "setup_s": {"generate": round(t_gen, 2), "prepare": round(t_prep, 2), "rmse_eval": round(t_eval, 3)},
         }
         print(json.dumps(out), flush=True)

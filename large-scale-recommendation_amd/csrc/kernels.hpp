@@ -81,7 +81,7 @@ void launch_fast_superstep(hipStream_t st, const FastBlk* blks, int nblk, int G,
 
 // Fast-mode sweep, pair schedule (kernels_pair.hip): one launch per sub-step, one wave per
 // cell, two updates of one item per step (build_pair_plan).  k in {64, 128, 256}; the plan
-// window must be >= 2 * kPairPlanRing.
+// window must be >= 2 * pair_ring(pair_kpl(k)) (plan.hpp pair_window).
 bool pair_kernel_supports(int k);
 // ev0 / ev1 (may be null): start / stop events recorded by the dispatch itself.
 void launch_sweep_pair(hipStream_t st, const WaveDesc* waves, int nwaves, const PairRec* recs, float* U, float* I,

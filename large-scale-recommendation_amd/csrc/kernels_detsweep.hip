@@ -408,12 +408,16 @@ __device__ __forceinline__ void link_get_row(MFHIP_LDS(double) * at, double (&v)
   }
 }
 
+// The chain wave waits here whenever its helper is blocked on a user ticket, legitimately, for up
+// to the ticket wait's own bound (poll_until: ~2^20 polls, 1-2 s).  So this bound is a clock, and
+// longer (~4 s on the 100 MHz s_memrealtime): a helper that times out sets err itself, and the
+// chain must not be the one to fail the launch first (its message would name the wrong wait).
 template <typename F>
 __device__ __forceinline__ void link_wait(F v, int32_t want, int32_t* err, int lane) {
-  uint32_t n = 0;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   while (__builtin_amdgcn_readfirstlane(v()) < want) {
     __builtin_amdgcn_s_sleep(1);
-    if (++n > (1u << 22)) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {
       if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __builtin_amdgcn_s_waitcnt(0x0F70);  // the flag store is not a row store a ticket publishes
       break;

@@ -149,6 +149,7 @@ struct mf_ctx {
   bool det_split = false;         // ... with single-item chains split over two waves (k_det_sweep_split)
   bool det_alone = true;          // ... the longest chains on CUs of their own (det_slot_table)
   int64_t det_split_blocks = 0;   // resident blocks of k_det_sweep_split (per device share)
+  int64_t det_cu_period = 256;    // CUs of the device: blocks b and b + period share a CU
   bool ring_overlap = false;      // fast systolic sweep, >1 shard, c >= 2: the ring step overlaps the sweep
   // fast-mode hot-item replicas (plan.hpp SplitItem), an experiment outside the product surface:
   // MFHIP_ITEM_SPLIT=m sweeps an item with more than m ratings in one rating block as ceil(r / m)
@@ -966,12 +967,21 @@ const bool g_det_timing = std::getenv("MFHIP_TIMING") != nullptr;
 // build_det_step (the buffer holds det_slot_room(nw)): each single-item wave with its helper slot,
 // longest first (block 0 is the hottest chain), then the other waves two per block; empty waves
 // dropped.  The chains within half of the longest (at most kDetAlone) bound the superstep, so they
-// get a CU each: the dispatcher deals block b to XCD b % 8 and, inside it, CU (b / 8) % 32, so
-// blocks b + 256 m share block b's CU -- those positions stay empty (both waves leave at once)
-// while the table has at most max_blocks blocks.  Returns the slot count (even).
+// get a CU each: the dispatcher deals block b to XCD b % 8 and, inside it, CU (b / 8) % (cus / 8),
+// so blocks b + cus m share block b's CU (period = the device's CU count, 256 on MI355X) -- those
+// positions stay empty (both waves leave at once) while the table has at most max_blocks blocks
+// (the co-resident limit: a block past it would never start and the ticket sweep would hang).
+// Returns the slot count (even).
+int64_t device_cu_count(int dev) {
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) return 256;
+  return cus;
+}
 constexpr int64_t kDetAlone = 64;
-int64_t det_slot_room(int64_t nw) { return 2 * nw + 2 * kDetAlone * (2 * nw / 256 + 2) + 2; }
-int64_t det_slot_table(DetWave* waves, int64_t nw, int64_t max_blocks, bool alone) {
+// H <= period / 2 chains keep their CU, so at most half of the positions are empty: <= 4 nw slots
+int64_t det_slot_room(int64_t nw) { return 4 * nw + 4; }
+int64_t det_slot_table(DetWave* waves, int64_t nw, int64_t max_blocks, bool alone, int64_t period) {
+  period = std::max<int64_t>(period, 8);
   std::vector<DetWave> single, multi;
   for (int64_t w = 0; w < nw; ++w) {
     if (waves[w].count == 0) continue;
@@ -989,11 +999,13 @@ int64_t det_slot_table(DetWave* waves, int64_t nw, int64_t max_blocks, bool alon
       ++H;
   const int64_t nb = static_cast<int64_t>(blocks.size());
   int64_t empties = 0;
-  for (int64_t b = 256; b < nb + empties; ++b) empties += (b % 256) < H;
+  H = std::min(H, period / 2);
+  for (int64_t b = period; b < nb + empties; ++b) empties += (b % period) < H;
   if (nb + empties > max_blocks) empties = 0, H = 0;  // no room: the plain order
+  MF_REQUIRE(nb <= max_blocks, "det slot table: more blocks than can be resident at once");
   int64_t n = 0, next = 0;
   for (int64_t b = 0; next < nb; ++b) {
-    if (b >= 256 && (b % 256) < H) {
+    if (b >= period && (b % period) < H) {
       waves[n++] = DetWave{0, 0, 0};
       waves[n++] = DetWave{0, 0, 0};
     } else {
@@ -1034,7 +1046,8 @@ void det_build(mf_ctx* ctx, int64_t superstep, int slot) {
                    reinterpret_cast<uint32_t*>(base + o.i), reinterpret_cast<uint32_t*>(base + o.qf),
                    reinterpret_cast<double*>(base + o.r)};
     build_det_step(ctx->rb, ctx->U, ctx->I, s.det_layout, blocks, seeds, ctx->P.has_seed != 0, out, &db.scratch);
-    if (ctx->det_split) db.nw = det_slot_table(out.waves, db.nw, ctx->det_split_blocks, ctx->det_alone);
+    if (ctx->det_split)
+      db.nw = det_slot_table(out.waves, db.nw, ctx->det_split_blocks, ctx->det_alone, ctx->det_cu_period);
   }
 }
 
@@ -1253,7 +1266,10 @@ void prepare_det_sweep(mf_ctx* ctx) {
       (static_cast<uint64_t>(ctx->U.rows()) * k8 >= 0x7FFFF000ull || static_cast<uint64_t>(ctx->I.rows()) * k8 >= 0x7FFFF000ull))
     return;
   int32_t waves = std::max(1, cap / 2);
-  if (const std::string v = test_knob("det_waves"); !v.empty()) waves = std::clamp(std::atoi(v.c_str()), 1, cap);
+  // the split sweep's slot table holds at most one block (two slots) per wave of the layout, and
+  // at most cap / 2 blocks are resident: so at most cap / 2 waves there
+  if (const std::string v = test_knob("det_waves"); !v.empty())
+    waves = std::clamp(std::atoi(v.c_str()), 1, split ? std::max(1, cap / 2) : cap);
   const int32_t n = ctx->nb;
   {  // the build's shuffle-order gather reads one 16-B record per rating
     const int64_t total = ctx->rb.start.empty() ? 0 : ctx->rb.start.back();
@@ -1299,6 +1315,7 @@ void prepare_det_sweep(mf_ctx* ctx) {
   ctx->det_split = split;
   ctx->det_split_blocks = cap / 2;
   ctx->det_alone = test_knob("det_alone") != "0";
+  ctx->det_cu_period = device_cu_count(ctx->shards[0].device);
 }
 
 void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, int64_t n) {
@@ -1824,16 +1841,22 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
   // hot-item chains, kernels_detsweep.hip), while every row offset fits its 32-bit buffer offsets
   // (rows after this batch's new ids at most rows + n); MFHIP_TEST online_kernel=ticket keeps
   // k_online_sweep
-  bool det_online = false;
+  // f32 at k <= 256: k_online_f32, whose row offsets are 32-bit as well (u * k * 4 bytes); a slab
+  // that would pass 4 GiB with this batch's new rows takes k_online_sweep (size_t addressing).
+  // MFHIP_TEST offset_limit=<bytes> lowers the limit so the tests reach that fallback.
+  bool det_online = false, f32_online = false;
   if (n > 0 && !outs && test_knob("online_kernel") != "level") {
     DeviceGuard g(s.device);
-    const auto fits = [&](int64_t rows) { return static_cast<double>(rows + n) * k * 8.0 <= 4294963200.0; };
+    double limit = 4294963200.0;  // raw_rsrc's clamp (pair_device.hpp)
+    if (const std::string v = test_knob("offset_limit"); !v.empty()) limit = std::stod(v);
+    const auto fits = [&](int64_t rows, int eb) { return static_cast<double>(rows + n) * k * eb <= limit; };
     det_online = ctx->f64 && test_knob("online_kernel") != "ticket" && online_det_capacity(k) > 0 &&
-                 fits(ctx->U.rows()) && fits(ctx->I.rows());
+                 fits(ctx->U.rows(), 8) && fits(ctx->I.rows(), 8);
+    f32_online = !ctx->f64 && online_f32_supports(k) && fits(ctx->U.rows(), 4) && fits(ctx->I.rows(), 4);
     // 0 (occupancy query failed): the level replay
     cap = det_online ? online_det_capacity(k)
-          : !ctx->f64 && online_f32_supports(k) ? online_f32_capacity(k) : online_sweep_capacity(k, ctx->f64);
-    if (cap == 0) det_online = false;
+          : f32_online ? online_f32_capacity(k) : online_sweep_capacity(k, ctx->f64);
+    if (cap == 0) det_online = f32_online = false;
   }
   // the sweep in arrival order takes the rows straight into its pinned upload buffer (user rows,
   // item rows, ratings: 16 B per rating), with no staging pass; otherwise they go to on_ur / on_ir
@@ -1989,7 +2012,7 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
     MF_HIP(hipMemsetAsync(sc.uticket.get(), 0, static_cast<size_t>(std::max<int64_t>(ctx->U.rows(), 1)) * 4, s.stream));
     sc.err.alloc(4);
     MF_HIP(hipMemsetAsync(sc.err.get(), 0, 4, s.stream));
-    if (!ctx->f64 && online_f32_supports(k)) {
+    if (f32_online) {
       sc.dummy.alloc(static_cast<size_t>(W) * 64);
       LaunchTimer t(s, ctx->profiling, true);
       launch_online_f32(s.stream, static_cast<int>(W), sc.wbeg.as<int64_t>(), s.det_dev.as<DetEntry>(),
@@ -2009,7 +2032,8 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
       MF_HIP(hipMemcpyAsync(det_slots.data(), sc.waves.get(), static_cast<size_t>(W) * sizeof(DetWave),
                             hipMemcpyDeviceToHost, s.stream));
       MF_HIP(hipStreamSynchronize(s.stream));
-      const int64_t nslots = det_slot_table(det_slots.data(), W, cap / 2, test_knob("det_alone") != "0");
+      const int64_t nslots =
+          det_slot_table(det_slots.data(), W, cap / 2, test_knob("det_alone") != "0", device_cu_count(s.device));
       MF_HIP(hipMemcpyAsync(sc.waves.get(), det_slots.data(), static_cast<size_t>(nslots) * sizeof(DetWave),
                             hipMemcpyHostToDevice, s.stream));
       LaunchTimer t(s, ctx->profiling, true);
@@ -2408,6 +2432,40 @@ int mf_empirical_risk(mf_ctx* ctx, const int32_t* u, const int32_t* i, const dou
   });
 }
 
+// mf_block_update: one rating block's updateLocalFactors (DSGDforMF.scala:378-418) on caller
+// buffers, as a Flink-resident task would call it.  The block's shuffle (new Random(iteration ^
+// ratingBlockId ^ seed), :392-393) runs on the host; the block then runs as ONE persistent launch of
+// the deterministic split sweep (k_det_sweep_split, kernels_detsweep.hip) -- the superstep's kernel
+// with a one-block superstep: every item's updates in shuffle order inside one wave (the hottest
+// items as chain + helper pairs on CUs of their own), every user's through per-user tickets -- with
+// its wave lists and tickets built on the device by the online plan (kernels_online.hip
+// online_sweep_plan / online_det_entries: any item -> wave map gives the same factors).  Bitwise the
+// sequential reference order (tests/test_gpu_dsgd.py test_block_update_*).  k outside 64 / 128 /
+// 256, slabs past the 32-bit row offsets, or MFHIP_TEST det_kernel=level: one launch per dependency
+// level (k_level), the same factors.
+namespace {
+void block_update_levels(Shard& s, const std::vector<int32_t>& order, const double* r, const int32_t* uidx,
+                         const int32_t* iidx, int64_t len, DevBuf& du, DevBuf& di, DevBuf& dru, DevBuf& dri, int64_t nu,
+                         int64_t ni, int k, double eta, int64_t& levels) {
+  std::vector<uint32_t> uu(uidx, uidx + len), ii(iidx, iidx + len);
+  OrderedSeq sq{uu.data(), ii.data(), r, order.data(), len, 0, static_cast<uint32_t>(nu), 0, static_cast<uint32_t>(ni)};
+  LevelPlan lp;
+  build_level_plan({sq}, lp);
+  DevBuf de;
+  de.alloc(lp.entries.size() * sizeof(DetEntry));
+  MF_HIP(hipMemcpyAsync(de.get(), lp.entries.data(), lp.entries.size() * sizeof(DetEntry), hipMemcpyHostToDevice,
+                        s.stream));
+  for (int64_t l = 0; l < lp.levels(); ++l) {
+    const int64_t b0 = lp.level_start[l], cnt = lp.level_start[l + 1] - b0;
+    launch_level(s.stream, de.as<DetEntry>() + b0, cnt, du.get(), di.get(), dru.get(), dri.get(), k, eta, Arith::kDsgd,
+                 true);
+  }
+  MF_HIP(hipGetLastError());
+  MF_HIP(hipStreamSynchronize(s.stream));  // lp and de are released on return
+  levels = lp.levels();
+}
+}  // namespace
+
 int mf_block_update(mf_ctx* ctx, const double* r, const int32_t* uidx, const int32_t* iidx, int64_t len,
                     double* users, const int32_t* uomega, int64_t nu, double* items, const int32_t* iomega,
                     int64_t ni, int k, int iteration, int rating_block_id, int64_t seed, double lr,
@@ -2416,45 +2474,116 @@ int mf_block_update(mf_ctx* ctx, const double* r, const int32_t* uidx, const int
     MF_REQUIRE(ctx, "null context");
     MF_REQUIRE(len >= 0 && nu >= 0 && ni >= 0 && k >= 1 && k <= 512, "bad sizes");
     MF_REQUIRE(len == 0 || (r && uidx && iidx && users && items && uomega && iomega), "null argument");
-    for (int64_t j = 0; j < len; ++j)
-      MF_REQUIRE(uidx[j] >= 0 && uidx[j] < nu && iidx[j] >= 0 && iidx[j] < ni, "rating index out of block range");
+    MF_REQUIRE(len < (int64_t{1} << 31), "a rating block holds fewer than 2^31 ratings");
+    std::atomic<int64_t> bad{0};
+    parallel_for(len, [&](int64_t b, int64_t e, int) {
+      int64_t m = 0;
+      for (int64_t j = b; j < e; ++j) m += !(uidx[j] >= 0 && uidx[j] < nu && iidx[j] >= 0 && iidx[j] < ni);
+      bad += m;
+    });
+    MF_REQUIRE(bad == 0, "rating index out of block range");
     if (len == 0) return;
+    require_healthy(ctx);
     Shard& s = ctx->shards[0];
     DeviceGuard g(s.device);
+    PhaseClock clk;
     std::vector<int32_t> order(len);
     JavaRandom rng(static_cast<int64_t>(iteration ^ rating_block_id) ^ seed);  // DSGDforMF.scala:392
     scala_shuffle(rng, order.data(), len);
-    std::vector<uint32_t> uu(uidx, uidx + len), ii(iidx, iidx + len);
-    OrderedSeq sq{uu.data(), ii.data(), r, order.data(), len, 0, static_cast<uint32_t>(nu), 0,
-                  static_cast<uint32_t>(ni)};
-    LevelPlan lp;
-    build_level_plan({sq}, lp);
-    std::vector<double> ru(nu), ri(ni);
-    for (int64_t x = 0; x < nu; ++x) ru[x] = lambda / static_cast<double>(uomega[x]);
-    for (int64_t x = 0; x < ni; ++x) ri[x] = lambda / static_cast<double>(iomega[x]);
+    clk.lap("block_update: shuffle");
     const double eta = learning_rate(lr_method, lr, iteration + 1, lambda, lr_arg);  // :383-386
-    DevBuf du, di, dru, dri, de;
-    du.alloc(static_cast<size_t>(nu) * k * 8);
-    di.alloc(static_cast<size_t>(ni) * k * 8);
-    dru.alloc(static_cast<size_t>(nu) * 8);
-    dri.alloc(static_cast<size_t>(ni) * 8);
-    de.alloc(lp.entries.size() * sizeof(DetEntry));
-    MF_HIP(hipMemcpy(du.get(), users, static_cast<size_t>(nu) * k * 8, hipMemcpyHostToDevice));
-    MF_HIP(hipMemcpy(di.get(), items, static_cast<size_t>(ni) * k * 8, hipMemcpyHostToDevice));
-    MF_HIP(hipMemcpy(dru.get(), ru.data(), static_cast<size_t>(nu) * 8, hipMemcpyHostToDevice));
-    MF_HIP(hipMemcpy(dri.get(), ri.data(), static_cast<size_t>(ni) * 8, hipMemcpyHostToDevice));
-    MF_HIP(hipMemcpy(de.get(), lp.entries.data(), lp.entries.size() * sizeof(DetEntry), hipMemcpyHostToDevice));
-    for (int64_t l = 0; l < lp.levels(); ++l) {
-      const int64_t b0 = lp.level_start[l], cnt = lp.level_start[l + 1] - b0;
-      launch_level(s.stream, de.as<DetEntry>() + b0, cnt, du.get(), di.get(), dru.get(), dri.get(), k, eta,
-                   Arith::kDsgd, true);
+    const size_t ub = static_cast<size_t>(nu) * k * 8, ib = static_cast<size_t>(ni) * k * 8;
+    DevBuf du, di, dru, dri;
+    du.alloc(std::max<size_t>(ub, 8));
+    di.alloc(std::max<size_t>(ib, 8));
+    dru.alloc(static_cast<size_t>(std::max<int64_t>(nu, 1)) * 8);
+    dri.alloc(static_cast<size_t>(std::max<int64_t>(ni, 1)) * 8);
+    {
+      std::vector<double> ru(nu), ri(ni);
+      for (int64_t x = 0; x < nu; ++x) ru[x] = lambda / static_cast<double>(uomega[x]);
+      for (int64_t x = 0; x < ni; ++x) ri[x] = lambda / static_cast<double>(iomega[x]);
+      MF_HIP(hipMemcpyAsync(du.get(), users, ub, hipMemcpyHostToDevice, s.stream));
+      MF_HIP(hipMemcpyAsync(di.get(), items, ib, hipMemcpyHostToDevice, s.stream));
+      MF_HIP(hipMemcpyAsync(dru.get(), ru.data(), static_cast<size_t>(nu) * 8, hipMemcpyHostToDevice, s.stream));
+      MF_HIP(hipMemcpyAsync(dri.get(), ri.data(), static_cast<size_t>(ni) * 8, hipMemcpyHostToDevice, s.stream));
+      MF_HIP(hipStreamSynchronize(s.stream));  // ru / ri are released here
     }
-    MF_HIP(hipGetLastError());
+    const int cap = det_split_capacity(k);
+    const bool sweep = cap >= 2 && test_knob("det_kernel") != "level" && ub < 0xFFFFF000ull && ib < 0xFFFFF000ull;
+    int64_t levels = 0;
+    if (!sweep) {
+      block_update_levels(s, order, r, uidx, iidx, len, du, di, dru, dri, nu, ni, k, eta, levels);
+    } else {
+      // the block in shuffle order, as the online plan takes a batch: rows, rows, ratings (16 B each)
+      const size_t in_bytes = static_cast<size_t>(len) * 16;
+      s.det_pin.alloc(in_bytes);
+      uint32_t* pu = s.det_pin.as<uint32_t>();
+      uint32_t* pi = pu + len;
+      double* pr = reinterpret_cast<double*>(pi + len);
+      parallel_for(len, [&](int64_t b, int64_t e, int) {
+        for (int64_t x = b; x < e; ++x) {
+          const int32_t j = order[x];
+          pu[x] = static_cast<uint32_t>(uidx[j]);
+          pi[x] = static_cast<uint32_t>(iidx[j]);
+          pr[x] = r[j];
+        }
+      });
+      clk.lap("block_update: gather");
+      OnlineSweepScratch& sc = s.online_sc;
+      sc.in.alloc(in_bytes);
+      MF_HIP(hipMemcpyAsync(sc.in.get(), pu, in_bytes, hipMemcpyHostToDevice, s.stream));
+      const int64_t W = std::max<int64_t>(1, std::min<int64_t>({static_cast<int64_t>(cap / 2), 4096, len}));
+      const size_t ebytes = static_cast<size_t>(len) * sizeof(DetEntry), qbytes = static_cast<size_t>(len) * 4;
+      s.det_dev.alloc(ebytes + qbytes);
+      sc.wbeg.alloc(static_cast<size_t>(W + 1) * 8);
+      sc.touched.alloc(8);
+      const uint32_t* dpu = sc.in.as<uint32_t>();
+      online_sweep_plan(s.stream, sc, dpu, dpu + len, reinterpret_cast<const double*>(dpu + 2 * len), len,
+                        static_cast<uint32_t>(W), static_cast<uint32_t>(nu), static_cast<uint32_t>(ni),
+                        s.det_dev.as<DetEntry>(), reinterpret_cast<uint32_t*>(s.det_dev.as<char>() + ebytes),
+                        sc.wbeg.as<int64_t>(), sc.touched.as<int32_t>());
+      uint32_t *eu = nullptr, *ei = nullptr, *eq = nullptr;
+      double* er = nullptr;
+      sc.waves.alloc(static_cast<size_t>(det_slot_room(W)) * sizeof(DetWave));
+      online_det_entries(s.stream, sc, s.det_dev.as<DetEntry>(),
+                         reinterpret_cast<const uint32_t*>(s.det_dev.as<char>() + ebytes), sc.wbeg.as<int64_t>(), len,
+                         static_cast<uint32_t>(W), eu, ei, eq, er, sc.waves.as<DetWave>());
+      std::vector<DetWave> slots(static_cast<size_t>(det_slot_room(W)));
+      MF_HIP(hipMemcpyAsync(slots.data(), sc.waves.get(), static_cast<size_t>(W) * sizeof(DetWave),
+                            hipMemcpyDeviceToHost, s.stream));
+      MF_HIP(hipStreamSynchronize(s.stream));
+      const int64_t nslots =
+          det_slot_table(slots.data(), W, cap / 2, test_knob("det_alone") != "0", device_cu_count(s.device));
+      MF_HIP(hipMemcpyAsync(sc.waves.get(), slots.data(), static_cast<size_t>(nslots) * sizeof(DetWave),
+                            hipMemcpyHostToDevice, s.stream));
+      sc.uticket.alloc(static_cast<size_t>(std::max<int64_t>(nu, 1)) * 4);
+      MF_HIP(hipMemsetAsync(sc.uticket.get(), 0, static_cast<size_t>(std::max<int64_t>(nu, 1)) * 4, s.stream));
+      sc.err.alloc(4);
+      MF_HIP(hipMemsetAsync(sc.err.get(), 0, 4, s.stream));
+      {
+        LaunchTimer t(s, ctx->profiling, true);
+        launch_det_sweep_split(s.stream, sc.waves.as<DetWave>(), static_cast<int>(nslots), eu, ei, eq, er,
+                               du.as<double>(), di.as<double>(), ub, ib, dru.as<double>(), dri.as<double>(), k, eta,
+                               sc.uticket.as<int32_t>(), sc.err.as<int32_t>(), t.start(), t.stop());
+      }
+      MF_HIP(hipGetLastError());
+      int32_t err = 0;
+      MF_HIP(hipMemcpyAsync(&err, sc.err.get(), 4, hipMemcpyDeviceToHost, s.stream));
+      MF_HIP(hipStreamSynchronize(s.stream));
+      clk.lap("block_update: plan + sweep");
+      if (err) {
+        ctx->failed = "block update sweep: a wave waited > 1 s for a user ticket (waves not co-resident?); "
+                      "set MFHIP_TEST=det_kernel=level (INTEGRATION.md section 5)";
+        fail(MF_ERR_TIMEOUT, ctx->failed);
+      }
+      ctx->stats.kernel_launches += 1;
+    }
+    MF_HIP(hipMemcpyAsync(users, du.get(), ub, hipMemcpyDeviceToHost, s.stream));
+    MF_HIP(hipMemcpyAsync(items, di.get(), ib, hipMemcpyDeviceToHost, s.stream));
     MF_HIP(hipStreamSynchronize(s.stream));
-    MF_HIP(hipMemcpy(users, du.get(), static_cast<size_t>(nu) * k * 8, hipMemcpyDeviceToHost));
-    MF_HIP(hipMemcpy(items, di.get(), static_cast<size_t>(ni) * k * 8, hipMemcpyDeviceToHost));
+    clk.lap("block_update: download");
     ctx->stats.updates += len;
-    ctx->stats.levels += lp.levels();
+    ctx->stats.levels += levels;
   });
 }
 

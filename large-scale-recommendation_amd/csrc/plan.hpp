@@ -280,6 +280,9 @@ constexpr int pair_kpl(int k) { return k <= 64 ? 1 : k <= 128 ? 2 : 4; }
 // 20.8 / 20.05 / 20.25 / 20.5 ms at 12 / 14 / 16 / 18, YAHOO 232 vs 215 ms at 8 vs 14; a wider window
 // pads more, a narrower one orders the cells worse; profiles/r05_pair_ring.txt)
 constexpr int pair_window(int k) { return k <= 64 ? 10 : 2 * kPairPlanRing; }
+static_assert(pair_window(64) >= 2 * pair_ring(pair_kpl(64)) && pair_window(128) >= 2 * pair_ring(pair_kpl(128)) &&
+                  pair_window(256) >= 2 * pair_ring(pair_kpl(256)),
+              "the hazard window covers the ring at every supported k");
 static_assert(pair_chunk(1) % pair_ring(1) == 0 && pair_chunk(2) % pair_ring(2) == 0 &&
                   pair_chunk(4) % pair_ring(4) == 0, "ring slots must repeat every chunk");
 static_assert(pair_ring(1) <= kPairPlanRing && pair_ring(2) <= kPairPlanRing && pair_ring(4) <= kPairPlanRing &&
@@ -327,7 +330,8 @@ struct PairPlan {
   int64_t noop_halves = 0;       // pair halves that are no-ops (planner padding, repeated users)
   std::vector<double> sm_bytes;  // per superstep index: bytes the sweep requests (records + in-range rows)
 };
-// The plan window must be >= 2 * kPairPlanRing records.  substep_waves: order the cells (and
+// The plan window must be >= 2 * pair_ring(pair_kpl(k)) records (pair_window(k) is; the knob
+// MFHIP_TEST pair_window=N is clamped to it, mfhip.cpp plan_window).  substep_waves: order the cells (and
 // pp.waves / sub_off) per sub-step (sm, t), longest first, for the per-sub-step launches (needs a
 // uniform G); otherwise per superstep, and only the systolic tables are meaningful.
 // cell_pairs (tables only): the pair count of every cell, indexed like fp.cell_off; the records

@@ -23,7 +23,7 @@ import pytest
 
 import coracle
 import mfhip
-from conftest import GOLDEN
+from conftest import GOLDEN, set_knob
 from mfhip import _lib as L
 from mfhip import synth
 
@@ -126,12 +126,14 @@ def _row_rel_err(a, b):
     return float((np.linalg.norm(a - b, axis=1) / den).max())
 
 
-def test_online_1m_batch_fast_f32_within_tolerance_of_f64_oracle():
+def test_online_1m_batch_fast_f32_within_tolerance_of_f64_oracle(monkeypatch):
     """The ONLINE line's precision: the same 1M-rating micro-batch applied in FAST f32 mode on a
-    fast-mode DSGD fit, (a) through the one-launch sweep bench.py times (k_online_sweep) and (b)
-    with per-rating records (the level replay), against coracle.online_apply in f64 from exactly
-    the fitted f32 factors (widened): every factor row and every per-rating (user', item') record
-    within ONLINE_F32_TOL relative (FlinkOnlineMF.scala:52-137, core/FactorUpdater.scala:37-45)."""
+    fast-mode DSGD fit, (a) through the one-launch sweep bench.py times (k_online_f32), (b) with
+    per-rating records (the level replay) and (c) through the wide-offset fallback k_online_sweep
+    (taken when a slab would pass the 32-bit row offsets of k_online_f32, forced here with
+    MFHIP_TEST offset_limit=1), against coracle.online_apply in f64 from exactly the fitted f32
+    factors (widened): every factor row and every per-rating (user', item') record within
+    ONLINE_F32_TOL relative (FlinkOnlineMF.scala:52-137, core/FactorUpdater.scala:37-45)."""
     config, scale = "NFLX", 0.05
     nu, ni, nr, k, nb = synth.CONFIGS[config]
     nu, ni, nr = int(nu * scale), int(ni * scale), int(nr * scale)
@@ -142,11 +144,12 @@ def test_online_1m_batch_fast_f32_within_tolerance_of_f64_oracle():
     p.num_factors, p.num_blocks, p.iterations, p.seed, p.mode = k, nb, 1, 0, L.MODE_FAST_F32
     p.online_learning_rate = lr
     res = {}
-    for path in ("sweep", "records"):
+    for path in ("sweep", "records", "wide"):
+        set_knob(monkeypatch, "offset_limit", 1 if path == "wide" else 4294963200)
         with mfhip.Context(p) as ctx:
             ctx.fit(tu, ti, tr)
             start = (ctx.factors(0), ctx.factors(1))
-            if path == "sweep":
+            if path in ("sweep", "wide"):
                 ctx.online_update(batch.u, batch.i, batch.r, L.ONLINE_NEXT_FACTORS)
                 recs = None
             else:
@@ -164,7 +167,10 @@ def test_online_1m_batch_fast_f32_within_tolerance_of_f64_oracle():
     # per-rating reference records: replay in f64 keeping (user', item') after every rating
     Ur, Ir = Uo.copy(), Io.copy()
     coracle.online_apply(urow, irow, batch.r, Ur, Ir, k, lr)
-    for path in ("sweep", "records"):
+    # the fallback's dot product is a sequential fold, k_online_f32's a fixed tree: a different
+    # kernel ran (identical factors would mean the offset check did not route the batch)
+    assert not np.array_equal(res["wide"][2][1], res["sweep"][2][1])
+    for path in ("sweep", "records", "wide"):
         _, (fu_ids, fu), (fi_ids, fi), _ = res[path]
         assert np.array_equal(fu_ids, np.sort(uall)) and np.array_equal(fi_ids, np.sort(iall))
         eu, ei = _row_rel_err(fu, Ur[uorder]), _row_rel_err(fi, Ir[iorder])

@@ -195,9 +195,14 @@ def test_snapshot_file_resume_bit_exact(tmp_path):
             bad.load(snap)
 
 
-def test_block_update_exact():
+@pytest.mark.parametrize("k,kern", [(12, "sweep"), (64, "sweep"), (64, "level"), (128, "sweep")])
+def test_block_update_exact(monkeypatch, k, kern):
+    """mf_block_update (the Flink-resident updateLocalFactors, DSGDforMF.scala:378-418) == the C
+    oracle's sequential order, bitwise: on the persistent split sweep at k = 64 / 128 (the one-block
+    superstep), and one launch per dependency level at k = 12 and with MFHIP_TEST det_kernel=level."""
+    set_knob(monkeypatch, "det_kernel", kern)
     rng = np.random.default_rng(8)
-    nu, ni, k, n = 30, 20, 12, 400
+    nu, ni, n = 30, 20, 400
     uidx = rng.integers(0, nu, n).astype(np.int32)
     iidx = rng.integers(0, ni, n).astype(np.int32)
     r = rng.random(n) * 5
@@ -207,6 +212,31 @@ def test_block_update_exact():
     a = mfhip.block_update(r, uidx, iidx, users, uom, items, iom, k, 2, 7, 5, 0.01, 0, 0.0, 1.0)
     b = coracle.block_update(r, uidx, iidx, users, uom, items, iom, k, 2, 7, 5, 0.01, 0, 0.0, 1.0)
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+def test_block_update_1m_hot_block_bit_exact():
+    """One NFLX-shaped rating block of 1.2M ratings (Zipf users and items, one item in ~4% of the
+    ratings, heavy users) through mf_block_update at k = 128: one persistent split-sweep launch,
+    bitwise the C oracle's block update (new Random(iteration ^ ratingBlockId ^ seed) shuffle, F2J
+    fold, no FMA)."""
+    k = 128
+    d = synth.generate(60000, 2200, 1_200_000, seed=17, test_fraction=0.0)
+    rng = np.random.default_rng(17)
+    uidx, iidx, r = d.u.copy(), d.i.copy(), d.r.copy()
+    iidx[rng.random(len(iidx)) < 0.04] = 5  # a hot item: a ~48k-update chain
+    nu, ni = int(uidx.max()) + 1, int(iidx.max()) + 1
+    users, items = rng.random((nu, k)) * 0.3, rng.random((ni, k)) * 0.3
+    uom = np.bincount(uidx, minlength=nu).astype(np.int32) + 1
+    iom = np.bincount(iidx, minlength=ni).astype(np.int32) + 1
+    p = L.default_params()
+    p.num_factors = k
+    with mfhip.Context(p) as ctx:
+        a = mfhip.block_update(r, uidx, iidx, users, uom, items, iom, k, 3, 9, 42, 0.001, 0, 0.0, 1.0, ctx=ctx)
+        st = ctx.stats()
+    assert st["kernel_launches"] == 1 and st["levels"] == 0  # the persistent sweep ran
+    b = coracle.block_update(r, uidx, iidx, users, uom, items, iom, k, 3, 9, 42, 0.001, 0, 0.0, 1.0)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
 
 
 def test_edge_cases():
@@ -538,6 +568,30 @@ def test_deterministic_persistent_sweep_bit_exact_hot_items(monkeypatch, k, nb, 
             ids, vecs = ctx.factors(side)
             rids, rvecs = m.factors(side)
             assert np.array_equal(ids, rids) and np.array_equal(vecs, rvecs)
+
+
+def test_det_split_many_blocks_cu_isolation_bitwise(monkeypatch):
+    """The split sweep's slot table past one CU period (det_slot_table): with ~1000 waves a superstep
+    has several hundred blocks, so the longest chains' CU-sharing positions b + cus*m are left empty
+    (det_alone=1, the default) -- factors bitwise the C oracle's with and without that isolation."""
+    k, nb = 64, 1
+    d = synth.generate(6000, 3000, 150000, seed=21)
+    rng = np.random.default_rng(21)
+    hot = np.repeat(np.arange(12, dtype=np.int32), 900)  # a dozen long single-item chains
+    d.u = np.concatenate([d.u, rng.integers(0, 6000, len(hot)).astype(np.int32)])
+    d.i = np.concatenate([d.i, hot])
+    d.r = np.concatenate([d.r, rng.integers(1, 6, len(hot)).astype(np.float64)])
+    m = coracle.dsgd_fit(d.u, d.i, d.r, k=k, iterations=2, n_blocks=nb, seed=3, threads=4)
+    set_knob(monkeypatch, "det_waves", 1000)
+    for alone in ("1", "0"):
+        set_knob(monkeypatch, "det_alone", alone)
+        with mfhip.Context(params(k, 2, nb, 3)) as ctx:
+            ctx.fit(d.u, d.i, d.r)
+            assert ctx.stats()["kernel_launches"] <= 2 * nb  # the persistent sweep ran
+            for side in (0, 1):
+                ids, vecs = ctx.factors(side)
+                rids, rvecs = m.factors(side)
+                assert np.array_equal(ids, rids) and np.array_equal(vecs, rvecs), (alone, side)
 
 
 @pytest.mark.parametrize("shards,nb", [(2, 4), (2, 8), (4, 8)])

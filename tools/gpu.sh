@@ -22,6 +22,8 @@
 #                                          device 0 with distinct RCCL host ids (MFHIP_FAKE_HOSTS), checked
 #                                          against a single-process context (tools/rank_check.py)
 #   micro:<src.hip>[:<hipcc flags>]        build a tools/micro benchmark and run it
+#   calib                                  FETCH_SIZE / WRITE_SIZE vs known bytes of 512-B row gathers and
+#                                          scatters (tools/micro/fetch_calib.hip) -> fetch_calib.json
 #   cmd:<shell command>                    anything else (300 s limit)
 set -o pipefail
 export TMPDIR=/tmp
@@ -130,6 +132,19 @@ for step in "$@"; do
         || { echo "micro build failed"; tail -5 "$O/$b.build.log"; exit 1; }
       timeout -k 10 120 "$O/$b" > "$O/$b.txt" 2>&1 || { echo "micro $b failed"; tail -5 "$O/$b.txt"; exit 1; }
       cat "$O/$b.txt" ;;
+    calib)  # FETCH_SIZE / WRITE_SIZE against known bytes (tools/micro/fetch_calib.hip, tools/pmc_calib.py)
+      hipcc -O3 --offload-arch=gfx950 -o "$O/fetch_calib" tools/micro/fetch_calib.hip > "$O/fetch_calib.build.log" 2>&1 \
+        || { echo "calib build failed"; tail -5 "$O/fetch_calib.build.log"; exit 1; }
+      timeout -k 10 120 "$O/fetch_calib" > "$O/fetch_calib.txt" 2>&1 || { echo "calib run failed"; tail -5 "$O/fetch_calib.txt"; exit 1; }
+      cd /tmp
+      timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$O/calib_fetch" -o f --output-format csv -- "$O/fetch_calib" \
+        > "$O/calib_fetch.log" 2>&1 || { echo "calib fetch pass failed"; tail -5 "$O/calib_fetch.log"; exit 1; }
+      timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$O/calib_write" -o w --output-format csv -- "$O/fetch_calib" \
+        > "$O/calib_write.log" 2>&1 || { echo "calib write pass failed"; tail -5 "$O/calib_write.log"; exit 1; }
+      cd "$R"
+      python3 tools/pmc_calib.py --cases "$O/fetch_calib.txt" --fetch $(ls "$O"/calib_fetch/*counter_collection.csv | head -1) \
+        --write $(ls "$O"/calib_write/*counter_collection.csv | head -1) --out "$O/fetch_calib.json" || { echo "calib summary failed"; exit 1; }
+      rm -rf "$O/calib_fetch" "$O/calib_write" ;;
     cmd)
       timeout -k 10 300 bash -c "$rest" > "$O/cmd_$n.log" 2>&1 || { echo "cmd failed"; tail -10 "$O/cmd_$n.log"; exit 1; }
       tail -20 "$O/cmd_$n.log" ;;
