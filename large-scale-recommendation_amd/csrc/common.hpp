@@ -116,6 +116,7 @@ struct OnlineSweepScratch {
   DevBuf dummy;                            // k_online_f32: a scratch ticket line per wave
   DevBuf icnt, iwave, irows;               // per item row: update counts (+ sorted), own wave (-1: none), rows by count
   DevBuf soa, multi, waves;                // the f64 sweep's entry arrays, multi-item flags, wave table
+  DevBuf miss;                             // the device id lookup's miss count
 };
 
 // Pinned host staging buffer.

@@ -44,6 +44,14 @@ struct OnlineSweepScratch;
 void online_sweep_plan(hipStream_t st, OnlineSweepScratch& sc, const uint32_t* eu, const uint32_t* ei,
                        const double* er, int64_t n, uint32_t W, uint32_t user_rows, uint32_t item_rows,
                        DetEntry* ent, uint32_t* useq, int64_t* wbeg, int32_t* touched);
+// The online batch's id -> row lookup on the device, over a mirror of the host IdIndex (same
+// hash, same slots; id_index.hpp): in[0, n) user ids and in[n, 2n) item ids (the batch as
+// uploaded) are replaced by their rows, 0xFFFFFFFF where the table has no such id; *misses counts
+// those (the host then gives the unseen ids rows in first-touch order).  A null table: all misses.
+void launch_id_lookup(hipStream_t st, uint32_t* in, int64_t n, const void* uslots, uint64_t umask, const void* islots,
+                      uint64_t imask, int32_t* misses);
+// slots[pos[j]] = vals[j] (8-B slots): the mirror takes the host table's writes since its last sync
+void launch_id_scatter(hipStream_t st, void* slots, const uint32_t* pos, const void* vals, int64_t m);
 // The f64 online batch on the deterministic sweep (kernels_detsweep.hip): the plan's entries as
 // SoA arrays in sc.soa (eu / ei / eq / er, padded by kDetPad) and one DetWave per wave (single-item
 // flag from the entries) into waves[0 .. W).  Call after online_sweep_plan on the same scratch.

@@ -161,6 +161,63 @@ __global__ void k_det_waves(const int64_t* __restrict__ wbeg, const int32_t* __r
 
 }  // namespace
 
+namespace {
+// IdIndex::hash (id_index.hpp), the same bits on the device
+__device__ __forceinline__ uint64_t id_hash(int32_t id) {
+  uint64_t x = static_cast<uint32_t>(id);
+  x ^= x >> 16; x *= 0x7feb352dULL; x ^= x >> 15; x *= 0x846ca68bULL; x ^= x >> 16;
+  return x;
+}
+// linear probing over a mirror of the host table: the row, or 0xFFFFFFFF (absent / empty table)
+__device__ __forceinline__ uint32_t id_find(const int2* __restrict__ slots, uint64_t mask, int32_t id) {
+  if (!slots) return 0xFFFFFFFFu;
+  uint64_t h = id_hash(id) & mask;
+  for (;;) {
+    const int2 sl = slots[h];
+    if (sl.y < 0) return 0xFFFFFFFFu;
+    if (sl.x == id) return static_cast<uint32_t>(sl.y);
+    h = (h + 1) & mask;
+  }
+}
+__global__ __launch_bounds__(kThreads) void k_id_lookup(uint32_t* __restrict__ in, int64_t n,
+                                                       const int2* __restrict__ us, uint64_t um,
+                                                       const int2* __restrict__ is, uint64_t im,
+                                                       int32_t* __restrict__ misses) {
+  const int64_t j = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  int m = 0;
+  if (j < n) {
+    const uint32_t ur = id_find(us, um, static_cast<int32_t>(in[j]));
+    const uint32_t ir = id_find(is, im, static_cast<int32_t>(in[n + j]));
+    in[j] = ur;
+    in[n + j] = ir;
+    m = (ur == 0xFFFFFFFFu) + (ir == 0xFFFFFFFFu);
+  }
+  // one atomic per wave
+  const int tot = __popcll(__ballot(m >= 1)) + __popcll(__ballot(m == 2));
+  if ((threadIdx.x & 63) == 0 && tot) atomicAdd(misses, tot);
+}
+__global__ __launch_bounds__(kThreads) void k_id_scatter(int2* __restrict__ slots, const uint32_t* __restrict__ pos,
+                                                        const int2* __restrict__ vals, int64_t m) {
+  const int64_t j = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  if (j < m) slots[pos[j]] = vals[j];
+}
+}  // namespace
+
+void launch_id_lookup(hipStream_t st, uint32_t* in, int64_t n, const void* uslots, uint64_t umask, const void* islots,
+                      uint64_t imask, int32_t* misses) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_id_lookup, dim3(grid_for(n)), dim3(kThreads), 0, st, in, n, static_cast<const int2*>(uslots),
+                     umask, static_cast<const int2*>(islots), imask, misses);
+  MF_HIP(hipGetLastError());
+}
+
+void launch_id_scatter(hipStream_t st, void* slots, const uint32_t* pos, const void* vals, int64_t m) {
+  if (m <= 0) return;
+  hipLaunchKernelGGL(k_id_scatter, dim3(grid_for(m)), dim3(kThreads), 0, st, static_cast<int2*>(slots), pos,
+                     static_cast<const int2*>(vals), m);
+  MF_HIP(hipGetLastError());
+}
+
 void online_det_entries(hipStream_t st, OnlineSweepScratch& sc, const DetEntry* ent, const uint32_t* useq,
                         const int64_t* wbeg, int64_t n, uint32_t W, uint32_t*& eu, uint32_t*& ei, uint32_t*& eq,
                         double*& er, DetWave* waves) {

@@ -138,7 +138,10 @@ __device__ int64_t emit_cell(const EmitArgs& A, int64_t gc, int64_t& pads) {
     while (y >= 0 && igE[iorder[y]] - igB[iorder[y]] < sv) { iorder[y + 1] = iorder[y]; --y; }
     iorder[y + 1] = v;
   }
-  const int32_t W = A.window;
+  // (plan.hpp plan_window_pack) a single-item cell with a run window: no user within W records,
+  // not even the next one
+  const bool run_cell = plan_window_strict_runs(A.window) && nig == 1;
+  const int32_t W = nig == 1 ? plan_window_run(A.window) : plan_window_mixed(A.window);
   FastRec* out = A.recs ? A.recs + A.recbase[gc] : nullptr;
   int32_t iorder_head = 0, prev_ug = -1, prev_ig = -1, left = m;
   int32_t pos = 0;
@@ -162,7 +165,7 @@ __device__ int64_t emit_cell(const EmitArgs& A, int64_t gc, int64_t& pads) {
       for (int32_t y = head; y < end && seen < limit; ++y) {
         if (taken[y]) continue;
         ++seen;
-        if ((!any_user && ug[y] == prev_ug) || pos - lastu[ug[y]] >= W) return y;
+        if ((!any_user && !run_cell && ug[y] == prev_ug) || pos - lastu[ug[y]] >= W) return y;
       }
       return -1;
     };
@@ -171,7 +174,7 @@ __device__ int64_t emit_cell(const EmitArgs& A, int64_t gc, int64_t& pads) {
       return scan_item(prev_ig, false);
     };
     auto try_user = [&]() -> int32_t {
-      if (prev_ug < 0 || ugL[prev_ug] == 0) return -1;
+      if (run_cell || prev_ug < 0 || ugL[prev_ug] == 0) return -1;
       int32_t& head = ugH[prev_ug];
       const int32_t end = ugE[prev_ug];
       while (head < end && taken[ulist[head]]) ++head;

@@ -68,6 +68,13 @@ struct DetBuf {
   DetStepScratch scratch;  // build_det_step's gathers for this slot (kept: no page faults per superstep)
 };
 
+// A device mirror of one side's IdIndex (same slots), for the online batch's id lookup.
+struct DevIndex {
+  DevBuf slots, upd_pos, upd_val;
+  uint64_t gen = 0, cap = 0;
+  size_t applied = 0;  // entries of the table's write log already in the mirror
+};
+
 struct Shard {
   int device = 0;
   int index = 0;  // global shard index (== rank in rank mode)
@@ -88,6 +95,7 @@ struct Shard {
   DevBuf det_dev;
   PinnedBuf det_pin;
   OnlineSweepScratch online_sc;  // online micro-batches (k_online_sweep)
+  DevIndex didx[2];              // device mirrors of the user [0] / item [1] IdIndex (online id lookup)
   // fast mode
   DevBuf fast_recs, fast_cells, fast_blks;
   DevBuf fast_prog, fast_err;  // persistent sweep: progress words + timeout flag
@@ -916,12 +924,17 @@ void ring_shift(mf_ctx* ctx, int64_t superstep) {
 struct DetOffsets {
   size_t waves, u, i, qf, r, total;
 };
-// The pair sweep's plan window for k (plan.hpp pair_window); MFHIP_TEST pair_window=N overrides
-// it for the window sweeps (clamped to the ring's minimum 2 * pair_ring).
+// The pair sweep's plan window for k (plan.hpp pair_window, plan_window_pack): MFHIP_TEST
+// pair_window=N overrides the mixed cells' window for the window sweeps (clamped to the ring's
+// minimum 2 * pair_ring), run_window=N the single-item cells' (plan.hpp pair_run_window; 0 = the
+// same window, forwarded repeats allowed).
 int32_t plan_window(int32_t k) {
+  int32_t w = pair_window(k), rw = pair_run_window(k);
   if (const std::string v = test_knob("pair_window"); !v.empty())
-    return std::max<int32_t>(2 * pair_ring(pair_kpl(k)), std::atoi(v.c_str()));
-  return pair_window(k);
+    w = std::max<int32_t>(2 * pair_ring(pair_kpl(k)), std::atoi(v.c_str()));
+  if (const std::string v = test_knob("run_window"); !v.empty()) rw = std::atoi(v.c_str());
+  if (rw != 0) rw = std::clamp<int32_t>(rw, w, 0x7FFF);
+  return plan_window_pack(w, rw);
 }
 int64_t det_slot_room(int64_t nw);
 DetOffsets det_offsets(int64_t n, int64_t nw) {
@@ -1815,6 +1828,40 @@ int32_t online_row(mf_ctx* ctx, SideLayout& S, int32_t id, std::vector<int32_t>&
   return nr;
 }
 
+// Brings the device mirror d up to the host table ix: the whole table after a rehash / clear / a
+// table of its own (generation changed), else only the slots written since the last sync.
+void sync_dev_index(Shard& s, const IdIndex& ix, DevIndex& d) {
+  const uint64_t cap = ix.capacity();
+  const auto& log = ix.log();
+  if (cap == 0) {
+    d.gen = ix.gen();
+    d.cap = 0;
+    d.applied = log.size();
+    return;
+  }
+  if (d.gen != ix.gen() || d.cap != cap) {
+    d.slots.alloc(cap * sizeof(IdIndex::Slot));
+    MF_HIP(hipMemcpyAsync(d.slots.get(), ix.slots(), cap * sizeof(IdIndex::Slot), hipMemcpyHostToDevice, s.stream));
+    MF_HIP(hipStreamSynchronize(s.stream));  // pageable source
+    d.gen = ix.gen();
+    d.cap = cap;
+    d.applied = log.size();
+    return;
+  }
+  const size_t m = log.size() - d.applied;
+  if (m == 0) return;
+  std::vector<uint32_t> pos(log.begin() + static_cast<std::ptrdiff_t>(d.applied), log.end());
+  std::vector<IdIndex::Slot> val(m);
+  for (size_t j = 0; j < m; ++j) val[j] = ix.slots()[pos[j]];
+  d.upd_pos.alloc(m * 4);
+  d.upd_val.alloc(m * sizeof(IdIndex::Slot));
+  MF_HIP(hipMemcpyAsync(d.upd_pos.get(), pos.data(), m * 4, hipMemcpyHostToDevice, s.stream));
+  MF_HIP(hipMemcpyAsync(d.upd_val.get(), val.data(), m * sizeof(IdIndex::Slot), hipMemcpyHostToDevice, s.stream));
+  launch_id_scatter(s.stream, d.slots.get(), d.upd_pos.as<uint32_t>(), d.upd_val.get(), static_cast<int64_t>(m));
+  MF_HIP(hipStreamSynchronize(s.stream));  // pos / val are released on return
+  d.applied = log.size();
+}
+
 void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, int64_t n, int flavour,
                    int num_partitions, int64_t* tu, int64_t* ti, double* uout = nullptr, double* iout = nullptr) {
   MF_REQUIRE(ctx->shards.size() == 1 && !ctx->rank_mode, "online updates run on a single-device context");
@@ -1885,14 +1932,51 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
   // as one sequential scan would
   constexpr uint32_t kMiss = 0xFFFFFFFFu;
   std::atomic<int64_t> misses{0};
-  parallel_for(n, [&](int64_t lo2, int64_t hi2, int) {
-    ctx->U.index.find_many(u + lo2, hi2 - lo2, ur + lo2);
-    ctx->I.index.find_many(i + lo2, hi2 - lo2, ir + lo2);
-    if (direct) std::memcpy(reinterpret_cast<double*>(ir + n) + lo2, r + lo2, static_cast<size_t>(hi2 - lo2) * 8);
-    int64_t m = 0;
-    for (int64_t j = lo2; j < hi2; ++j) m += (ur[j] == kMiss) + (ir[j] == kMiss);
-    misses += m;
-  });
+  // the direct path looks the ids up on the device (a mirror of each side's IdIndex, kept in step
+  // by sync_dev_index): the host only copies the batch into the pinned upload, and resolves misses
+  // (ids first seen in this batch) itself, in rating order, when there are any.  MFHIP_TEST
+  // online_lookup=host keeps the host lookup (the tests compare the two bit for bit).
+  const bool dev_lookup = direct && test_knob("online_lookup") != "host";
+  bool uploaded = false;
+  if (dev_lookup) {
+    DeviceGuard g(s.device);
+    parallel_for(n, [&](int64_t lo2, int64_t hi2, int) {
+      const size_t c = static_cast<size_t>(hi2 - lo2);
+      std::memcpy(ur + lo2, u + lo2, c * 4);
+      std::memcpy(ir + lo2, i + lo2, c * 4);
+      std::memcpy(reinterpret_cast<double*>(ir + n) + lo2, r + lo2, c * 8);
+    });
+    clk.lap("online: staging");
+    OnlineSweepScratch& sc = s.online_sc;
+    sync_dev_index(s, ctx->U.index, s.didx[0]);
+    sync_dev_index(s, ctx->I.index, s.didx[1]);
+    const size_t ibytes = static_cast<size_t>(n) * 16;
+    sc.in.alloc(ibytes);
+    MF_HIP(hipMemcpyAsync(sc.in.get(), ur, ibytes, hipMemcpyHostToDevice, s.stream));
+    sc.miss.alloc(4);
+    MF_HIP(hipMemsetAsync(sc.miss.get(), 0, 4, s.stream));
+    const DevIndex &du = s.didx[0], &di = s.didx[1];
+    launch_id_lookup(s.stream, sc.in.as<uint32_t>(), n, du.cap ? du.slots.get() : nullptr, du.cap - 1,
+                     di.cap ? di.slots.get() : nullptr, di.cap - 1, sc.miss.as<int32_t>());
+    int32_t m = 0;
+    MF_HIP(hipMemcpyAsync(&m, sc.miss.get(), 4, hipMemcpyDeviceToHost, s.stream));
+    MF_HIP(hipStreamSynchronize(s.stream));
+    misses = m;
+    if (m > 0) {  // the rows as found (kMiss where absent) back into the pinned buffer
+      MF_HIP(hipMemcpyAsync(ur, sc.in.get(), static_cast<size_t>(n) * 8, hipMemcpyDeviceToHost, s.stream));
+      MF_HIP(hipStreamSynchronize(s.stream));
+    }
+    uploaded = m == 0;
+  } else {
+    parallel_for(n, [&](int64_t lo2, int64_t hi2, int) {
+      ctx->U.index.find_many(u + lo2, hi2 - lo2, ur + lo2);
+      ctx->I.index.find_many(i + lo2, hi2 - lo2, ir + lo2);
+      if (direct) std::memcpy(reinterpret_cast<double*>(ir + n) + lo2, r + lo2, static_cast<size_t>(hi2 - lo2) * 8);
+      int64_t m = 0;
+      for (int64_t j = lo2; j < hi2; ++j) m += (ur[j] == kMiss) + (ir[j] == kMiss);
+      misses += m;
+    });
+  }
   if (misses > 0)
     for (int64_t j = 0; j < n; ++j) {
       if (ur[j] == kMiss) ur[j] = static_cast<uint32_t>(online_row(ctx, ctx->U, u[j], fu));
@@ -1998,8 +2082,10 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
       clk.lap("online: sweep staging");
     }
     uint32_t* pu = s.det_pin.as<uint32_t>();
-    sc.in.alloc(ibytes);
-    MF_HIP(hipMemcpyAsync(sc.in.get(), pu, ibytes, hipMemcpyHostToDevice, s.stream));
+    if (!uploaded) {  // (the device lookup left the batch's rows in sc.in already)
+      sc.in.alloc(ibytes);
+      MF_HIP(hipMemcpyAsync(sc.in.get(), pu, ibytes, hipMemcpyHostToDevice, s.stream));
+    }
     s.det_dev.alloc(ebytes + qbytes);
     sc.wbeg.alloc(static_cast<size_t>(W + 1) * 8);
     const uint32_t* du = sc.in.as<uint32_t>();

@@ -588,7 +588,10 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
                      int32_t G0, int32_t k, double lambda, uint64_t order_seed, uint32_t dummy_row,
                      std::vector<int64_t>* rec_src, int32_t window, const std::vector<int32_t>* block_groups,
                      int32_t split_run, uint32_t scratch_base, std::vector<FastBlockWork>* entries_out) {
-  const int64_t kHazardWindow = window;  // shadows the default for this plan
+  // (plan.hpp plan_window_pack: mixed cells' window, single-item cells' window)
+  const int64_t kHazardWindow = plan_window_mixed(window);  // shadows the default for this plan
+  const int64_t kRunWindow = plan_window_run(window);
+  const bool strict_runs = plan_window_strict_runs(window);
   const uint32_t row_bytes = static_cast<uint32_t>(k) * 4u;
   const int32_t nb = rb.n_blocks;
   const int64_t nb2 = static_cast<int64_t>(nb) * nb;
@@ -885,16 +888,19 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
       size_t iorder_head = 0;
       int32_t prev_ug = -1, prev_ig = -1;
       int32_t left = m;
+      // a single-item cell with a run window: no user within win records, not even the next one
+      const bool run_cell = strict_runs && igs.size() == 1;
+      const int64_t win = igs.size() == 1 ? kRunWindow : kHazardWindow;
       while (left > 0) {
         const int32_t pos = static_cast<int32_t>(static_cast<int64_t>(out.size()) - stream_begin);
-        auto free_at = [&](const Last& L) { return L.sid != sid || pos - L.pos >= kHazardWindow; };
+        auto free_at = [&](const Last& L) { return L.sid != sid || pos - L.pos >= win; };
         auto ufree = [&](const Ent& en) { return free_at(last_u[en.ug]); };
         auto ifree = [&](int32_t ig) { return free_at(last_i[ig]); };
         // the first untaken entries of a group's list (at most 4 * window of them) that pass ok
         auto scan = [&](Grp& g2, const int32_t* list, auto ok) -> int32_t {
           while (g2.head < g2.end && taken[list ? list[g2.head] : g2.head]) ++g2.head;
           int seen = 0;
-          for (int32_t y = g2.head; y < g2.end && seen < 4 * kHazardWindow; ++y) {
+          for (int32_t y = g2.head; y < g2.end && seen < 4 * win; ++y) {
             const int32_t e = list ? list[y] : y;
             if (taken[e]) continue;
             ++seen;
@@ -904,10 +910,10 @@ void build_fast_plan(FastPlan& fp, const RatingBlocks& rb, const SideLayout& U, 
         };
         auto try_item = [&]() -> int32_t {  // continue the item run
           if (prev_ig < 0 || igs[prev_ig].left == 0) return -1;
-          return scan(igs[prev_ig], nullptr, [&](const Ent& en) { return en.ug == prev_ug || ufree(en); });
+          return scan(igs[prev_ig], nullptr, [&](const Ent& en) { return (!run_cell && en.ug == prev_ug) || ufree(en); });
         };
         auto try_user = [&]() -> int32_t {  // continue the user run
-          if (prev_ug < 0 || ugs[prev_ug].left == 0) return -1;
+          if (run_cell || prev_ug < 0 || ugs[prev_ug].left == 0) return -1;
           return scan(ugs[prev_ug], ulist.data(), [&](const Ent& en) { return en.ig == prev_ig || ifree(en.ig); });
         };
         const bool user_first = prev_ug >= 0 && prev_ig >= 0 && ugs[prev_ug].left > igs[prev_ig].left;

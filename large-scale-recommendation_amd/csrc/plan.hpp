@@ -274,12 +274,24 @@ constexpr int pair_chunk(int) { return MFHIP_EXP_PAIR_CHUNK; }
 constexpr int pair_ring(int kpl) { return kpl == 2 ? 6 : 4; }
 constexpr int pair_chunk(int kpl) { return kpl == 2 ? 60 : 56; }
 #endif
+// The window argument of build_fast_plan / device_fast_schedule: the low 16 bits are the hazard
+// window of cells with several item runs, the high 16 bits (0: the same) that of single-item
+// cells (one item run, the hot items' chains).  A run window also forbids a user at the next record
+// (no forwarded repeats): the single-run block step (kernels_pair.hip) solves whole blocks of
+// records at once and prefetches their rows two blocks ahead, so inside a cell no user may recur
+// within run-window records.
+constexpr int32_t plan_window_pack(int32_t w, int32_t run_w) { return (w & 0xFFFF) | (run_w << 16); }
+constexpr int32_t plan_window_mixed(int32_t p) { return p & 0xFFFF; }
+constexpr int32_t plan_window_run(int32_t p) { return (p >> 16) ? (p >> 16) : (p & 0xFFFF); }
+constexpr bool plan_window_strict_runs(int32_t p) { return (p >> 16) != 0; }
 constexpr int pair_kpl(int k) { return k <= 64 ? 1 : k <= 128 ? 2 : 4; }
 // The plan window for k (>= 2 * pair_ring; MFHIP_TEST pair_window=N overrides it): 10 records at
 // k = 64 (ML20M 4.82 / 4.49 / 4.45 / 4.64 ms at 14 / 8 / 10 / 12), 2 * kPairPlanRing = 14 above (NFLX
 // 20.8 / 20.05 / 20.25 / 20.5 ms at 12 / 14 / 16 / 18, YAHOO 232 vs 215 ms at 8 vs 14; a wider window
 // pads more, a narrower one orders the cells worse; profiles/r05_pair_ring.txt)
 constexpr int pair_window(int k) { return k <= 64 ? 10 : 2 * kPairPlanRing; }
+// The single-item cells' window for k (plan_window_pack; 0 = pair_window with forwarded repeats)
+constexpr int pair_run_window(int) { return 0; }
 static_assert(pair_window(64) >= 2 * pair_ring(pair_kpl(64)) && pair_window(128) >= 2 * pair_ring(pair_kpl(128)) &&
                   pair_window(256) >= 2 * pair_ring(pair_kpl(256)),
               "the hazard window covers the ring at every supported k");

@@ -243,3 +243,32 @@ def test_online_sweep_edge_batches(monkeypatch, shape, mode, k):
     for side in (0, 1):
         assert np.array_equal(res["level"][side][0], res["sweep"][side][0])
         assert np.array_equal(res["level"][side][1], res["sweep"][side][1])
+
+
+@pytest.mark.parametrize("mode", [L.MODE_FAST_F32, L.MODE_DETERMINISTIC_F64])
+def test_device_id_lookup_equals_host_lookup(monkeypatch, mode):
+    """The online batch's id -> row lookup on the device (a mirror of each side's IdIndex, kept in
+    step with the host table: whole after a rehash, else the slots written since) gives the rows of
+    the host lookup (MFHIP_TEST online_lookup=host), bit for bit in the factors and the id lists:
+    negative ids, an empty model at the start (every id new), new ids in every later batch (first
+    touch order), and enough of them that both tables rehash between batches."""
+    rng = np.random.default_rng(23)
+    res = {}
+    for where in ("host", "device"):
+        set_knob(monkeypatch, "online_lookup", where)
+        p = L.default_params()
+        p.num_factors, p.mode, p.online_learning_rate = 64, mode, 0.01
+        rng = np.random.default_rng(23)
+        with mfhip.Context(p) as ctx:
+            for b in range(6):
+                n = 20000
+                hi = 500 * 4 ** b  # the id ranges grow: each batch brings new ids, later batches force rehashes
+                u = (rng.integers(-hi, hi, n)).astype(np.int32)
+                i = (rng.integers(-hi // 4, hi // 4, n)).astype(np.int32)
+                r = rng.integers(1, 6, n).astype(np.float64)
+                tu, ti = ctx.online_update(u, i, r, L.ONLINE_NEXT_FACTORS)
+                assert (tu, ti) == (len(np.unique(u)), len(np.unique(i)))
+            res[where] = (ctx.factors(0), ctx.factors(1))
+    for side in (0, 1):
+        assert np.array_equal(res["host"][side][0], res["device"][side][0])
+        assert np.array_equal(res["host"][side][1], res["device"][side][1])

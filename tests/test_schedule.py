@@ -108,10 +108,18 @@ def test_hot_item_replicas_split_and_stay_conflict_free(nb, G, split):
 
 
 @pytest.mark.parametrize("nb,G,window", [(1, 4, 0), (3, 8, 0), (4, 16, 0), (3, 8, 32), (2, 4, 16), (3, -64, 14),
-                                         (2, -16, 14)])
+                                         (2, -16, 14), (2, -16, 14 | (48 << 16)), (1, 16, 10 | (40 << 16))])
 def test_fast_rotation_is_conflict_free(nb, G, window):
-    """G < 0: the systolic sweep's per-rating-block groups for a budget of -G waves per superstep."""
+    """G < 0: the systolic sweep's per-rating-block groups for a budget of -G waves per superstep.
+    window = w | (run_w << 16) (plan.hpp plan_window_pack): single-item cells keep every user
+    run_w records apart, without forwarded repeats."""
     d = synth.generate(500, 200, 20000, seed=1)
+    if window >> 16:  # a hot item, so that single-item cells exist
+        rng = np.random.default_rng(2)
+        hu = rng.integers(0, 500, 3000).astype(np.int32)
+        d.u = np.concatenate([d.u, hu])
+        d.i = np.concatenate([d.i, np.full(len(hu), 7, np.int32)])
+        d.r = np.concatenate([d.r, np.ones(len(hu))])
     b, t, g, p = fast_schedule(d.u, d.i, nb, 3, G, window=window)
     if G < 0:
         Gb = {int(x): int(t[b == x].max()) + 1 for x in np.unique(b)}  # per block: t, g in [0, G_j)
@@ -120,7 +128,8 @@ def test_fast_rotation_is_conflict_free(nb, G, window):
         for s in range(nb):  # the superstep's waves fit the budget
             assert sum(v for x, v in Gb.items() if (x // nb + s) % nb == x % nb) <= -G
         G = 1024
-    win = window or 8
+    win = (window & 0xFFFF) or 8
+    run_win = window >> 16
     # blocks follow DSGD blocking of the reference
     ub = np.array([mfhip.jvm.block_of(int(x), 3, nb) for x in d.u])
     ib = np.array([mfhip.jvm.block_of(int(x), 3, nb) for x in d.i])
@@ -141,17 +150,23 @@ def test_fast_rotation_is_conflict_free(nb, G, window):
     # distance: 8 for kernels_fast.hip, lean_ring_depth(k) for kernels_lean.hip); item runs keep the item row in registers.  Padding records (the gaps)
     # carry the zero user row and the preceding record's item, so they extend an item run.
     key = b.astype(np.int64) * G * G + t.astype(np.int64) * G + g
-    runs = 0
+    runs = single = 0
     for c in np.unique(key)[:300]:
         m = np.where(key == c)[0]
         pos = p[m]
         assert len(set(pos.tolist())) == len(m)  # distinct slots (gaps = no-op padding records)
+        one_item = run_win and len(np.unique(d.i[m])) == 1
+        single += bool(one_item)
         for side, ids in (("u", d.u[m]), ("i", d.i[m])):
             last, prev = {}, -1
             for x, y in sorted(zip(pos.tolist(), ids.tolist())):
                 run = side == "i" and last.get(y) == prev  # only padding since this item's last record
-                assert y not in last or x - last[y] == 1 or x - last[y] >= win or run, (side, y, last.get(y), x)
+                if one_item and side == "u":  # no repeat within run_win, not even adjacent
+                    assert y not in last or x - last[y] >= run_win, (y, last.get(y), x)
+                else:
+                    assert y not in last or x - last[y] == 1 or x - last[y] >= win or run, (side, y, last.get(y), x)
                 last[y] = prev = x
         items_in_order = d.i[m[np.argsort(pos)]]
         runs += int(np.sum(items_in_order[1:] == items_in_order[:-1]))
     assert runs > 0
+    assert single > 0 or not run_win
