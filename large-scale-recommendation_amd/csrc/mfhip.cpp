@@ -1940,19 +1940,30 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
   bool uploaded = false;
   if (dev_lookup) {
     DeviceGuard g(s.device);
-    parallel_for(n, [&](int64_t lo2, int64_t hi2, int) {
-      const size_t c = static_cast<size_t>(hi2 - lo2);
-      std::memcpy(ur + lo2, u + lo2, c * 4);
-      std::memcpy(ir + lo2, i + lo2, c * 4);
-      std::memcpy(reinterpret_cast<double*>(ir + n) + lo2, r + lo2, c * 8);
-    });
-    clk.lap("online: staging");
     OnlineSweepScratch& sc = s.online_sc;
     sync_dev_index(s, ctx->U.index, s.didx[0]);
     sync_dev_index(s, ctx->I.index, s.didx[1]);
     const size_t ibytes = static_cast<size_t>(n) * 16;
     sc.in.alloc(ibytes);
-    MF_HIP(hipMemcpyAsync(sc.in.get(), ur, ibytes, hipMemcpyHostToDevice, s.stream));
+    // the batch into the pinned buffer in pieces, each piece's upload queued as soon as it is
+    // staged: the DMA of piece c overlaps the host copy of piece c + 1
+    const int64_t piece = std::max<int64_t>(int64_t{1} << 17, (n + 7) / 8);
+    uint32_t* din = sc.in.as<uint32_t>();
+    for (int64_t p0 = 0; p0 < n; p0 += piece) {
+      const int64_t p1 = std::min(n, p0 + piece);
+      parallel_for(p1 - p0, [&](int64_t lo2, int64_t hi2, int) {
+        const int64_t a = p0 + lo2;
+        const size_t c = static_cast<size_t>(hi2 - lo2);
+        std::memcpy(ur + a, u + a, c * 4);
+        std::memcpy(ir + a, i + a, c * 4);
+        std::memcpy(reinterpret_cast<double*>(ir + n) + a, r + a, c * 8);
+      });
+      const size_t c = static_cast<size_t>(p1 - p0);
+      MF_HIP(hipMemcpyAsync(din + p0, ur + p0, c * 4, hipMemcpyHostToDevice, s.stream));
+      MF_HIP(hipMemcpyAsync(din + n + p0, ir + p0, c * 4, hipMemcpyHostToDevice, s.stream));
+      MF_HIP(hipMemcpyAsync(din + 2 * n + 2 * p0, ir + n + 2 * p0, c * 8, hipMemcpyHostToDevice, s.stream));
+    }
+    clk.lap("online: staging + upload");
     sc.miss.alloc(4);
     MF_HIP(hipMemsetAsync(sc.miss.get(), 0, 4, s.stream));
     const DevIndex &du = s.didx[0], &di = s.didx[1];
