@@ -117,6 +117,26 @@ struct OnlineSweepScratch {
   DevBuf icnt, iwave, irows;               // per item row: update counts (+ sorted), own wave (-1: none), rows by count
   DevBuf soa, multi, waves;                // the f64 sweep's entry arrays, multi-item flags, wave table
   DevBuf miss;                             // the device id lookup's miss count
+  // the plan's independent sorts run side by side: the tickets' user sort on s2, the touched-item
+  // sort on s3 (each with its own hipCUB scratch and keys), joined back into the caller's stream
+  DevBuf tmp2, tmp3, iota2, ikey, iflag;
+  hipStream_t s2 = nullptr, s3 = nullptr;
+  hipEvent_t ev_in = nullptr, ev2 = nullptr, ev3 = nullptr;
+  OnlineSweepScratch() = default;
+  OnlineSweepScratch(const OnlineSweepScratch&) = delete;
+  OnlineSweepScratch& operator=(const OnlineSweepScratch&) = delete;
+  ~OnlineSweepScratch() {
+    for (hipEvent_t e : {ev_in, ev2, ev3})
+      if (e) (void)hipEventDestroy(e);
+    for (hipStream_t q : {s2, s3})
+      if (q) (void)hipStreamDestroy(q);
+  }
+  void side_streams() {  // on the current device (the caller's DeviceGuard)
+    if (s2) return;
+    MF_HIP(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+    MF_HIP(hipStreamCreateWithFlags(&s3, hipStreamNonBlocking));
+    for (hipEvent_t* e : {&ev_in, &ev2, &ev3}) MF_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  }
 };
 
 // Pinned host staging buffer.

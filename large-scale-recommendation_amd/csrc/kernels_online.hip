@@ -47,6 +47,12 @@ __global__ void k_item_count(const uint32_t* __restrict__ ei, int64_t n, uint32_
     atomicAdd(cnt + ei[x], 1u);
 }
 
+__global__ void k_iota(int64_t n, int32_t* __restrict__ iota) {
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    iota[i] = static_cast<int32_t>(i);
+}
+
 __global__ void k_iota_rows(uint32_t rows, int32_t* __restrict__ iota, int32_t* __restrict__ iwave) {
   for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < rows;
        i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
@@ -286,45 +292,61 @@ void online_sweep_plan(hipStream_t st, OnlineSweepScratch& sc, const uint32_t* e
                      H > 0 && item_rows > 0 ? sc.iwave.as<int32_t>() : nullptr, sc.wkey.as<uint32_t>(),
                      sc.iota.as<int32_t>());
   const int ub = bits_for(user_rows), wb = bits_for(W);
-  // tickets
-  MF_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, eu, sc.ukey.as<uint32_t>(), sc.iota.as<int32_t>(),
-                                            sc.ux.as<int32_t>(), N, 0, ub, st));
-  sc.tmp.alloc(std::max<size_t>(tb, 256));
-  MF_HIP(hipcub::DeviceRadixSort::SortPairs(sc.tmp.get(), tb, eu, sc.ukey.as<uint32_t>(), sc.iota.as<int32_t>(),
-                                            sc.ux.as<int32_t>(), N, 0, ub, st));
-  hipLaunchKernelGGL(k_run_heads, dim3(grid_for(n)), dim3(kThreads), 0, st, sc.ukey.as<uint32_t>(), n,
+  // tickets on s2 (user sort, run starts, ranks) and the touched items on s3 (a key-only item sort)
+  // run beside the wave keys and the wave sort on st; both only read the uploaded batch
+  sc.side_streams();
+  sc.iota2.alloc(n * 4);
+  sc.ikey.alloc(n * 4);
+  sc.iflag.alloc(n * 4);
+  MF_HIP(hipEventRecord(sc.ev_in, st));
+  MF_HIP(hipStreamWaitEvent(sc.s2, sc.ev_in, 0));
+  MF_HIP(hipStreamWaitEvent(sc.s3, sc.ev_in, 0));
+  size_t tb2 = 0, tb3 = 0;
+  hipLaunchKernelGGL(k_iota, dim3(grid_for(n)), dim3(kThreads), 0, sc.s2, n, sc.iota2.as<int32_t>());
+  MF_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb2, eu, sc.ukey.as<uint32_t>(), sc.iota2.as<int32_t>(),
+                                            sc.ux.as<int32_t>(), N, 0, ub, sc.s2));
+  sc.tmp2.alloc(std::max<size_t>(tb2, 256));
+  MF_HIP(hipcub::DeviceRadixSort::SortPairs(sc.tmp2.get(), tb2, eu, sc.ukey.as<uint32_t>(), sc.iota2.as<int32_t>(),
+                                            sc.ux.as<int32_t>(), N, 0, ub, sc.s2));
+  hipLaunchKernelGGL(k_run_heads, dim3(grid_for(n)), dim3(kThreads), 0, sc.s2, sc.ukey.as<uint32_t>(), n,
                      sc.head.as<int32_t>());
-  MF_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb, sc.head.as<int32_t>(), sc.start.as<int32_t>(), hipcub::Max(),
-                                           N, st));
-  sc.tmp.alloc(std::max<size_t>(tb, 256));
-  MF_HIP(hipcub::DeviceScan::InclusiveScan(sc.tmp.get(), tb, sc.head.as<int32_t>(), sc.start.as<int32_t>(),
-                                           hipcub::Max(), N, st));
-  hipLaunchKernelGGL(k_tickets, dim3(grid_for(n)), dim3(kThreads), 0, st, sc.ux.as<int32_t>(), sc.start.as<int32_t>(),
+  MF_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb2, sc.head.as<int32_t>(), sc.start.as<int32_t>(), hipcub::Max(),
+                                           N, sc.s2));
+  sc.tmp2.alloc(std::max<size_t>(tb2, 256));
+  MF_HIP(hipcub::DeviceScan::InclusiveScan(sc.tmp2.get(), tb2, sc.head.as<int32_t>(), sc.start.as<int32_t>(),
+                                           hipcub::Max(), N, sc.s2));
+  hipLaunchKernelGGL(k_tickets, dim3(grid_for(n)), dim3(kThreads), 0, sc.s2, sc.ux.as<int32_t>(), sc.start.as<int32_t>(),
                      n, sc.ticket.as<uint32_t>());
-  // waves
+  // touched users: run heads of the user-sorted keys (s2)
+  hipLaunchKernelGGL(k_head_flags, dim3(grid_for(n)), dim3(kThreads), 0, sc.s2, sc.ukey.as<uint32_t>(), n,
+                     sc.head.as<int32_t>());
+  MF_HIP(hipcub::DeviceReduce::Sum(nullptr, tb2, sc.head.as<int32_t>(), touched, N, sc.s2));
+  sc.tmp2.alloc(std::max<size_t>(tb2, 256));
+  MF_HIP(hipcub::DeviceReduce::Sum(sc.tmp2.get(), tb2, sc.head.as<int32_t>(), touched, N, sc.s2));
+  MF_HIP(hipEventRecord(sc.ev2, sc.s2));
+  // touched items (s3)
+  MF_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb3, ei, sc.ikey.as<uint32_t>(), N, 0, bits_for(item_rows), sc.s3));
+  sc.tmp3.alloc(std::max<size_t>(tb3, 256));
+  MF_HIP(hipcub::DeviceRadixSort::SortKeys(sc.tmp3.get(), tb3, ei, sc.ikey.as<uint32_t>(), N, 0, bits_for(item_rows),
+                                           sc.s3));
+  hipLaunchKernelGGL(k_head_flags, dim3(grid_for(n)), dim3(kThreads), 0, sc.s3, sc.ikey.as<uint32_t>(), n,
+                     sc.iflag.as<int32_t>());
+  MF_HIP(hipcub::DeviceReduce::Sum(nullptr, tb3, sc.iflag.as<int32_t>(), touched + 1, N, sc.s3));
+  sc.tmp3.alloc(std::max<size_t>(tb3, 256));
+  MF_HIP(hipcub::DeviceReduce::Sum(sc.tmp3.get(), tb3, sc.iflag.as<int32_t>(), touched + 1, N, sc.s3));
+  MF_HIP(hipEventRecord(sc.ev3, sc.s3));
+  // waves (st): the wave sort, then the gather once the tickets are in
   MF_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, sc.wkey.as<uint32_t>(), sc.wkey2.as<uint32_t>(),
                                             sc.iota.as<int32_t>(), sc.wx.as<int32_t>(), N, 0, wb, st));
   sc.tmp.alloc(std::max<size_t>(tb, 256));
   MF_HIP(hipcub::DeviceRadixSort::SortPairs(sc.tmp.get(), tb, sc.wkey.as<uint32_t>(), sc.wkey2.as<uint32_t>(),
                                             sc.iota.as<int32_t>(), sc.wx.as<int32_t>(), N, 0, wb, st));
-  hipLaunchKernelGGL(k_gather, dim3(grid_for(n)), dim3(kThreads), 0, st, sc.wx.as<int32_t>(), eu, ei, er,
-                     sc.ticket.as<uint32_t>(), n, ent, useq);
   hipLaunchKernelGGL(k_wave_begin, dim3(grid_for(W + 1)), dim3(kThreads), 0, st, sc.wkey2.as<uint32_t>(), n, W,
                      wbeg);
-  // touched rows: run heads of the user-sorted keys, and of the item rows sorted (keys only)
-  hipLaunchKernelGGL(k_head_flags, dim3(grid_for(n)), dim3(kThreads), 0, st, sc.ukey.as<uint32_t>(), n,
-                     sc.head.as<int32_t>());
-  MF_HIP(hipcub::DeviceReduce::Sum(nullptr, tb, sc.head.as<int32_t>(), touched, N, st));
-  sc.tmp.alloc(std::max<size_t>(tb, 256));
-  MF_HIP(hipcub::DeviceReduce::Sum(sc.tmp.get(), tb, sc.head.as<int32_t>(), touched, N, st));
-  MF_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, ei, sc.wkey.as<uint32_t>(), N, 0, bits_for(item_rows), st));
-  sc.tmp.alloc(std::max<size_t>(tb, 256));
-  MF_HIP(hipcub::DeviceRadixSort::SortKeys(sc.tmp.get(), tb, ei, sc.wkey.as<uint32_t>(), N, 0, bits_for(item_rows), st));
-  hipLaunchKernelGGL(k_head_flags, dim3(grid_for(n)), dim3(kThreads), 0, st, sc.wkey.as<uint32_t>(), n,
-                     sc.start.as<int32_t>());
-  MF_HIP(hipcub::DeviceReduce::Sum(nullptr, tb, sc.start.as<int32_t>(), touched + 1, N, st));
-  sc.tmp.alloc(std::max<size_t>(tb, 256));
-  MF_HIP(hipcub::DeviceReduce::Sum(sc.tmp.get(), tb, sc.start.as<int32_t>(), touched + 1, N, st));
+  MF_HIP(hipStreamWaitEvent(st, sc.ev2, 0));
+  hipLaunchKernelGGL(k_gather, dim3(grid_for(n)), dim3(kThreads), 0, st, sc.wx.as<int32_t>(), eu, ei, er,
+                     sc.ticket.as<uint32_t>(), n, ent, useq);
+  MF_HIP(hipStreamWaitEvent(st, sc.ev3, 0));  // touched[1]; and nothing on s3 outlives the plan
   MF_HIP(hipGetLastError());
 }
 

@@ -15,11 +15,14 @@
 // loaded when the item changed, and the previous update's stores were drained every update):
 //   * updates in chunks of 16 with the update's index a compile-time constant (every field a
 //     constant-lane v_readlane), full chunks without exit tests;
-//   * user AND item rows prefetched two updates ahead, after the current update's stores (an item
-//     row is only ever written by this wave; an item that recurs after another one was stored at
-//     the switch, before the prefetch, so a prefetched item row is always current);
-//   * the ticket of update j + 4 polled at update j (read at j + 2, when j + 4's row is prefetched
-//     only if it is already due), and tickets published two updates late: update j waits only for
+//   * user rows prefetched kUD = 4 updates ahead and item rows two ahead, after the current
+//     update's stores (an item row is only ever written by this wave; an item that recurs after
+//     another one was stored at the switch, before the prefetch, so a prefetched item row is always
+//     current; a user row is prefetched only when its ticket is due, i.e. every earlier update of
+//     that user, this wave's included, has landed).  Two ahead the hot wave waited on its user rows
+//     (NFLX batch: 0.835 ms for a 2.3k-update chain);
+//   * the ticket of update j + kUD + 2 polled at update j (read at j + 2, when that update's row is
+//     prefetched only if it is already due), and tickets published two updates late: update j waits only for
 //     update j - 2's stores (vmcnt(NW): the operations issued after them), so a store's round trip
 //     overlaps two updates of compute.  A wave publishes every pending ticket before it blocks;
 //   * the dot product is online_f32.hpp's fixed tree (~10 dependent VALU operations, not a 128-add
@@ -43,6 +46,7 @@ namespace {
 constexpr int kSC1 = 16;                // buffer cache policy: sc1 (L1 bypass, write-through)
 constexpr uint32_t kOOB = 0xFFFFF000u;  // a row offset past the slab: the load returns 0, no store
 constexpr int kOnChunk = 16;            // updates per register chunk
+constexpr int kUD = 4;                  // user rows prefetched this many updates ahead
 
 __device__ __forceinline__ uint32_t rl(uint32_t v, int l) {
   return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), l));
@@ -165,20 +169,25 @@ __global__ __launch_bounds__(64) void k_online_f32(const int64_t* __restrict__ w
   auto fq = [&](int s) { return s < CH ? rl(C0.q, s) : rl(C1.q, s - CH); };
   auto fr = [&](int s) { return __uint_as_float(s < CH ? rl(__float_as_uint(C0.r), s) : rl(__float_as_uint(C1.r), s - CH)); };
 
-  float P[2][KPL], Q[2][KPL];
-  int32_t okP[2];  // the slot's user row was prefetched (its ticket was due)
-  int32_t tk[2];   // ticket polls, read two updates after they are issued
-  // prologue: updates 0 and 1 (their tickets read here), polls of updates 2 and 3
+  // user rows kUD updates ahead (a 4-deep ring), item rows two ahead (an item row is written by
+  // this wave alone, and one that recurs two updates on was stored at the switch, before the
+  // prefetch; four ahead it would not be)
+  float P[kUD][KPL], Q[2][KPL];
+  int32_t okP[kUD];  // the slot's user row was prefetched (its ticket was due)
+  int32_t tk[2];     // ticket polls, read two updates after they are issued
+  // prologue: the user rows of updates 0 .. kUD-1 and the item rows of 0 and 1 (their tickets read
+  // here), polls of updates kUD and kUD+1
 #pragma unroll
-  for (int x = 0; x < 2; ++x) {
+  for (int x = 0; x < kUD; ++x) {
     const bool live = x < cnt;
     const uint32_t u = fu(x);
     okP[x] = !live || __builtin_amdgcn_readfirstlane(poll_issue(ticket + u)) == static_cast<int32_t>(fq(x));
     rows.load(urs, live && okP[x] ? u * rowb : kOOB, P[x]);
-    rows.load(irs, live && (x == 0 || fi(1) != fi(0)) ? fi(x) * rowb : kOOB, Q[x]);
   }
 #pragma unroll
-  for (int x = 0; x < 2; ++x) tk[x] = poll_issue(x + 2 < cnt ? ticket + fu(x + 2) : dummy_ticket);
+  for (int x = 0; x < 2; ++x) rows.load(irs, x < cnt && (x == 0 || fi(1) != fi(0)) ? fi(x) * rowb : kOOB, Q[x]);
+#pragma unroll
+  for (int x = 0; x < 2; ++x) tk[x] = poll_issue(x + kUD < cnt ? ticket + fu(x + kUD) : dummy_ticket);
   __builtin_amdgcn_s_waitcnt(0x0F70);
   int32_t* pend0 = dummy_ticket;  // update j-2's ticket word and value
   int32_t pv0 = 0;
@@ -189,23 +198,23 @@ __global__ __launch_bounds__(64) void k_online_f32(const int64_t* __restrict__ w
   for (int c = 0; c < KPL; ++c) q[c] = 0.f;
   uint32_t cur_i = 0;
 
-  // update j (chunk-relative s, a compile-time constant once unrolled); s + 4 < 2 CH
+  // update j (chunk-relative s, a compile-time constant once unrolled); s + kUD + 2 < 2 CH
   auto update = [&](const int s, const int32_t j) {
-    const int slot = s & 1;
+    const int slot = s & 1, us = s % kUD;
     const uint32_t u = fu(s), i = fi(s);
     const int32_t qseq = static_cast<int32_t>(fq(s));
     const float r = fr(s);
-    const uint32_t u2 = fu(s + 2), q2 = fq(s + 2), u4 = fu(s + 4);
+    const uint32_t uD = fu(s + kUD), qD = fq(s + kUD), uT = fu(s + kUD + 2);
     const uint32_t i1 = fi(s + 1), i2 = fi(s + 2);
     // 1. the user row, when its ticket was not due at prefetch time: publish the pending tickets
     //    (after their stores), wait for ours, load now
-    if (!okP[slot]) {
+    if (!okP[us]) {
       __builtin_amdgcn_s_waitcnt(0x0F70);
       publish(pend0, pv0, lane);
       publish(pend1, pv1, lane);
       pend0 = pend1 = dummy_ticket;
       wait_ticket_or_fail(ticket + u, qseq, err, lane);  // no early return (ticket_wait.hpp)
-      rows.load(urs, u * rowb, P[slot]);
+      rows.load(urs, u * rowb, P[us]);
       __builtin_amdgcn_s_waitcnt(0x0F70);
     }
     // 2. the item row: prefetched when the item changed, else the one in registers
@@ -217,7 +226,7 @@ __global__ __launch_bounds__(64) void k_online_f32(const int64_t* __restrict__ w
     // 3. the update (online_f32.hpp)
     float p[KPL];
 #pragma unroll
-    for (int c = 0; c < KPL; ++c) p[c] = P[slot][c];
+    for (int c = 0; c < KPL; ++c) p[c] = P[us][c];
     const float le = f32_err(static_cast<double>(r), f32_wave_sum(f32_lane_dot<KPL>(p, q)), eta);
     f32_sgd_next<KPL>(p, q, le);
     // 4. update j-2's stores have landed (NW younger operations may still fly): publish its ticket
@@ -228,17 +237,18 @@ __global__ __launch_bounds__(64) void k_online_f32(const int64_t* __restrict__ w
     pend1 = ticket + u;
     pv1 = qseq + 1;
     // 5. stores: the user row, and the item row when the next update is on another item (or none)
-    const bool live1 = j + 1 < cnt, live2 = j + 2 < cnt;
+    const bool live1 = j + 1 < cnt, live2 = j + 2 < cnt, liveD = j + kUD < cnt;
     rows.store(urs, u * rowb, p);
     rows.store(irs, !live1 || i1 != i ? i * rowb : kOOB, q);
-    // 6. prefetch update j+2 into this slot: its user row if its ticket (polled at j-2) is due, its
+    // 6. prefetch: update j+kUD's user row into this user slot if its ticket (polled at j-2) is due
+    //    -- every earlier update of that user, this wave's included, has landed -- and update j+2's
     //    item row if it starts another item's run
-    const int32_t okN = !live2 || __builtin_amdgcn_readfirstlane(tk[slot]) == static_cast<int32_t>(q2);
-    rows.load(urs, live2 && okN ? u2 * rowb : kOOB, P[slot]);
+    const int32_t okN = !liveD || __builtin_amdgcn_readfirstlane(tk[slot]) == static_cast<int32_t>(qD);
+    rows.load(urs, liveD && okN ? uD * rowb : kOOB, P[us]);
     rows.load(irs, live2 && i2 != i1 ? i2 * rowb : kOOB, Q[slot]);
-    okP[slot] = okN;
-    // 7. poll update j+4's ticket (read at j+2)
-    tk[slot] = poll_issue(j + 4 < cnt ? ticket + u4 : dummy_ticket);
+    okP[us] = okN;
+    // 7. poll update j+kUD+2's ticket (read at j+2)
+    tk[slot] = poll_issue(j + kUD + 2 < cnt ? ticket + uT : dummy_ticket);
   };
   // full chunks run their updates with no exit test in between (ticket_wait.hpp, kernels_detsweep.hip)
   for (int32_t c0 = 0;; c0 += CH) {

@@ -2613,6 +2613,7 @@ int mf_block_update(mf_ctx* ctx, const double* r, const int32_t* uidx, const int
     } else {
       // the block in shuffle order, as the online plan takes a batch: rows, rows, ratings (16 B each)
       const size_t in_bytes = static_cast<size_t>(len) * 16;
+      MF_HIP(hipStreamSynchronize(s.stream));  // det_pin may still feed an earlier copy
       s.det_pin.alloc(in_bytes);
       uint32_t* pu = s.det_pin.as<uint32_t>();
       uint32_t* pi = pu + len;
