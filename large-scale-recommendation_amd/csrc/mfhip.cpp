@@ -96,6 +96,7 @@ struct Shard {
   PinnedBuf det_pin;
   OnlineSweepScratch online_sc;  // online micro-batches (k_online_sweep)
   DevIndex didx[2];              // device mirrors of the user [0] / item [1] IdIndex (online id lookup)
+  DevBuf blk_u, blk_i, blk_ru, blk_ri;  // mf_block_update: the block's factor rows and lambda / omega
   // fast mode
   DevBuf fast_recs, fast_cells, fast_blks;
   DevBuf fast_prog, fast_err;  // persistent sweep: progress words + timeout flag
@@ -1945,24 +1946,15 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
     sync_dev_index(s, ctx->I.index, s.didx[1]);
     const size_t ibytes = static_cast<size_t>(n) * 16;
     sc.in.alloc(ibytes);
-    // the batch into the pinned buffer in pieces, each piece's upload queued as soon as it is
-    // staged: the DMA of piece c overlaps the host copy of piece c + 1
-    const int64_t piece = std::max<int64_t>(int64_t{1} << 17, (n + 7) / 8);
-    uint32_t* din = sc.in.as<uint32_t>();
-    for (int64_t p0 = 0; p0 < n; p0 += piece) {
-      const int64_t p1 = std::min(n, p0 + piece);
-      parallel_for(p1 - p0, [&](int64_t lo2, int64_t hi2, int) {
-        const int64_t a = p0 + lo2;
-        const size_t c = static_cast<size_t>(hi2 - lo2);
-        std::memcpy(ur + a, u + a, c * 4);
-        std::memcpy(ir + a, i + a, c * 4);
-        std::memcpy(reinterpret_cast<double*>(ir + n) + a, r + a, c * 8);
-      });
-      const size_t c = static_cast<size_t>(p1 - p0);
-      MF_HIP(hipMemcpyAsync(din + p0, ur + p0, c * 4, hipMemcpyHostToDevice, s.stream));
-      MF_HIP(hipMemcpyAsync(din + n + p0, ir + p0, c * 4, hipMemcpyHostToDevice, s.stream));
-      MF_HIP(hipMemcpyAsync(din + 2 * n + 2 * p0, ir + n + 2 * p0, c * 8, hipMemcpyHostToDevice, s.stream));
-    }
+    // (staging in pieces with each piece's upload queued behind it was slower: 2-3 ms against ~1 ms
+    // per NFLX batch, gpurun_out/r6d)
+    parallel_for(n, [&](int64_t lo2, int64_t hi2, int) {
+      const size_t c = static_cast<size_t>(hi2 - lo2);
+      std::memcpy(ur + lo2, u + lo2, c * 4);
+      std::memcpy(ir + lo2, i + lo2, c * 4);
+      std::memcpy(reinterpret_cast<double*>(ir + n) + lo2, r + lo2, c * 8);
+    });
+    MF_HIP(hipMemcpyAsync(sc.in.get(), ur, ibytes, hipMemcpyHostToDevice, s.stream));
     clk.lap("online: staging + upload");
     sc.miss.alloc(4);
     MF_HIP(hipMemsetAsync(sc.miss.get(), 0, 4, s.stream));
@@ -2590,7 +2582,8 @@ int mf_block_update(mf_ctx* ctx, const double* r, const int32_t* uidx, const int
     clk.lap("block_update: shuffle");
     const double eta = learning_rate(lr_method, lr, iteration + 1, lambda, lr_arg);  // :383-386
     const size_t ub = static_cast<size_t>(nu) * k * 8, ib = static_cast<size_t>(ni) * k * 8;
-    DevBuf du, di, dru, dri;
+    // the block's rows and reg vectors live in the shard's scratch across calls (grow-only)
+    DevBuf &du = s.blk_u, &di = s.blk_i, &dru = s.blk_ru, &dri = s.blk_ri;
     du.alloc(std::max<size_t>(ub, 8));
     di.alloc(std::max<size_t>(ib, 8));
     dru.alloc(static_cast<size_t>(std::max<int64_t>(nu, 1)) * 8);
