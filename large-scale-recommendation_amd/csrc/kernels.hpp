@@ -34,16 +34,17 @@ bool online_f32_supports(int k);
 int online_f32_capacity(int k);
 void launch_online_f32(hipStream_t st, int nw, const int64_t* wbeg, const DetEntry* ent, const uint32_t* useq, float* U,
                        float* I, uint64_t u_bytes, uint64_t i_bytes, int k, double eta, int32_t* ticket,
-                       int32_t* dummy_ticket, int32_t* err, hipEvent_t ev0, hipEvent_t ev1);
+                       int32_t* dummy_ticket, int32_t* err, int nsingle, hipEvent_t ev0, hipEvent_t ev1);
 // k_online_sweep's inputs from one batch in sequence order (eu / ei / er: user row, item row,
 // rating of update x; device arrays), on the device (kernels_online.hip): ent / useq (n each,
 // grouped by wave = item row mod W, sequence order inside a wave, useq = the update's rank among
 // its user's updates) and wbeg (W + 1); touched[0..1] = distinct user / item rows of the batch.
 // user_rows / item_rows bound eu / ei.
 struct OnlineSweepScratch;
-void online_sweep_plan(hipStream_t st, OnlineSweepScratch& sc, const uint32_t* eu, const uint32_t* ei,
-                       const double* er, int64_t n, uint32_t W, uint32_t user_rows, uint32_t item_rows,
-                       DetEntry* ent, uint32_t* useq, int64_t* wbeg, int32_t* touched);
+// Returns H: waves [0, H) hold one item each (the heavy items), the others any number.
+uint32_t online_sweep_plan(hipStream_t st, OnlineSweepScratch& sc, const uint32_t* eu, const uint32_t* ei,
+                           const double* er, int64_t n, uint32_t W, uint32_t user_rows, uint32_t item_rows,
+                           DetEntry* ent, uint32_t* useq, int64_t* wbeg, int32_t* touched);
 // The online batch's id -> row lookup on the device, over a mirror of the host IdIndex (same
 // hash, same slots; id_index.hpp): in[0, n) user ids and in[n, 2n) item ids (the batch as
 // uploaded) are replaced by their rows, 0xFFFFFFFF where the table has no such id; *misses counts

@@ -242,9 +242,9 @@ void online_det_entries(hipStream_t st, OnlineSweepScratch& sc, const DetEntry* 
   MF_HIP(hipGetLastError());
 }
 
-void online_sweep_plan(hipStream_t st, OnlineSweepScratch& sc, const uint32_t* eu, const uint32_t* ei,
-                       const double* er, int64_t n, uint32_t W, uint32_t user_rows, uint32_t item_rows,
-                       DetEntry* ent, uint32_t* useq, int64_t* wbeg, int32_t* touched) {
+uint32_t online_sweep_plan(hipStream_t st, OnlineSweepScratch& sc, const uint32_t* eu, const uint32_t* ei,
+                           const double* er, int64_t n, uint32_t W, uint32_t user_rows, uint32_t item_rows,
+                           DetEntry* ent, uint32_t* useq, int64_t* wbeg, int32_t* touched) {
   MF_REQUIRE(n > 0 && n < (int64_t{1} << 31) && W >= 1, "online sweep plan: bad batch shape");
   const int N = static_cast<int>(n);
   sc.ukey.alloc(n * 4);
@@ -348,6 +348,7 @@ void online_sweep_plan(hipStream_t st, OnlineSweepScratch& sc, const uint32_t* e
                      sc.ticket.as<uint32_t>(), n, ent, useq);
   MF_HIP(hipStreamWaitEvent(st, sc.ev3, 0));  // touched[1]; and nothing on s3 outlives the plan
   MF_HIP(hipGetLastError());
+  return H > 0 && item_rows > 0 ? H : 0;
 }
 
 }  // namespace mfhip

@@ -22,9 +22,9 @@
 //     that user, this wave's included, has landed).  Two ahead the hot wave waited on its user rows
 //     (NFLX batch: 0.835 ms for a 2.3k-update chain);
 //   * the ticket of update j + kUD + 2 polled at update j (read at j + 2, when that update's row is
-//     prefetched only if it is already due), and tickets published two updates late: update j waits only for
-//     update j - 2's stores (vmcnt(NW): the operations issued after them), so a store's round trip
-//     overlaps two updates of compute.  A wave publishes every pending ticket before it blocks;
+//     prefetched only if it is already due), and tickets published kPD = 4 updates late: update j waits only for
+//     update j - 4's stores (vmcnt(NW): the operations issued after them), so a store's round trip
+//     overlaps four updates of compute.  A wave publishes every pending ticket before it blocks;
 //   * the dot product is online_f32.hpp's fixed tree (~10 dependent VALU operations, not a 128-add
 //     chain); the level replay uses the same arithmetic, so both give the same factors bit for bit.
 // Every update issues the same vector-memory operations (out-of-range offsets for rows it does not
@@ -46,7 +46,8 @@ namespace {
 constexpr int kSC1 = 16;                // buffer cache policy: sc1 (L1 bypass, write-through)
 constexpr uint32_t kOOB = 0xFFFFF000u;  // a row offset past the slab: the load returns 0, no store
 constexpr int kOnChunk = 16;            // updates per register chunk
-constexpr int kUD = 4;                  // user rows prefetched this many updates ahead
+constexpr int kSingleDepth = 4;         // single-item waves: user rows, polls and tickets this many updates apart
+constexpr int kPubLate = 4;             // every wave publishes a ticket this many updates late (tools/isa_check.py)
 
 __device__ __forceinline__ uint32_t rl(uint32_t v, int l) {
   return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), l));
@@ -136,22 +137,28 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70 & ~0xF);
 }
 
-template <int KPL, bool FULL>
-__global__ __launch_bounds__(64) void k_online_f32(const int64_t* __restrict__ wbeg, const DetEntry* __restrict__ ent,
-                                                   const uint32_t* __restrict__ useq, float* U, float* I,
-                                                   uint64_t u_bytes, uint64_t i_bytes, int k, float eta,
-                                                   int32_t* ticket, int32_t* dummy_ticket, int32_t* err) {
+// One wave's updates.  UD: user rows prefetched UD updates ahead (guarded by the user's ticket);
+// TD: a ticket poll is read TD updates after it is issued; PD: tickets published PD updates late.
+// vmcnt counts in issue order, so a wave waits, in effect, for the oldest of those distances --
+// and for its item rows, prefetched two updates ahead (an item that recurs after a switch must be
+// loaded after its store).  SINGLE: the wave holds one item (the plan's heavy-item waves), so the
+// item row is loaded once and stored once, and every distance can be deeper: the hot item's chain
+// -- the batch's critical path -- no longer waits for each update's row stores two updates later
+// (NFLX 1M batch: 0.835-0.863 ms with every distance 2, the chain ~360 ns per update).
+template <int KPL, bool FULL, int UD, int TD, int PD, bool SINGLE>
+__device__ __forceinline__ void online_wave(const int64_t jb, const int32_t cnt, const DetEntry* __restrict__ ent,
+                                            const uint32_t* __restrict__ useq, float* U, float* I, uint64_t u_bytes,
+                                            uint64_t i_bytes, int k, float eta, int32_t* ticket, int32_t* dummy_ticket,
+                                            int32_t* err) {
   using R = Rows<KPL, FULL>;
   constexpr int CH = kOnChunk;
-  // operations issued after update j-2's stores up to update j's publish: j-2's loads (user row,
-  // item row, ticket poll) and all of j-1's (publish, user + item row stores, its loads)
-  constexpr int NW = (2 * R::OPS + 1) + (1 + 2 * R::OPS + 2 * R::OPS + 1);
+  static_assert(UD + TD < 2 * CH - CH + 1 && 2 <= UD && 2 <= TD && 1 <= PD, "ring distances");
+  // operations issued after update j-PD's stores up to update j's publish: j-PD's loads and poll,
+  // then PD-1 whole updates (publish, stores, loads, poll); SINGLE moves no item row per update
+  constexpr int IO = SINGLE ? 0 : R::OPS;  // item-row operations per update (load, store)
+  constexpr int NW = (R::OPS + IO + 1) + (PD - 1) * (1 + R::OPS + IO + R::OPS + IO + 1);
   static_assert(NW < 64, "vmcnt range");
   const int lane = threadIdx.x;
-  const int64_t jb = wbeg[blockIdx.x];
-  const int32_t cnt = static_cast<int32_t>(wbeg[blockIdx.x + 1] - jb);
-  if (cnt <= 0) return;
-  dummy_ticket += 16 * static_cast<int64_t>(blockIdx.x);  // this wave's own scratch line
   const R rows(lane, k);
   const __amdgpu_buffer_rsrc_t urs = raw_rsrc(U, u_bytes), irs = raw_rsrc(I, i_bytes);
   const __amdgpu_buffer_rsrc_t ers = raw_rsrc(ent + jb, static_cast<uint64_t>(cnt) * sizeof(DetEntry));
@@ -169,86 +176,105 @@ __global__ __launch_bounds__(64) void k_online_f32(const int64_t* __restrict__ w
   auto fq = [&](int s) { return s < CH ? rl(C0.q, s) : rl(C1.q, s - CH); };
   auto fr = [&](int s) { return __uint_as_float(s < CH ? rl(__float_as_uint(C0.r), s) : rl(__float_as_uint(C1.r), s - CH)); };
 
-  // user rows kUD updates ahead (a 4-deep ring), item rows two ahead (an item row is written by
-  // this wave alone, and one that recurs two updates on was stored at the switch, before the
-  // prefetch; four ahead it would not be)
-  float P[kUD][KPL], Q[2][KPL];
-  int32_t okP[kUD];  // the slot's user row was prefetched (its ticket was due)
-  int32_t tk[2];     // ticket polls, read two updates after they are issued
-  // prologue: the user rows of updates 0 .. kUD-1 and the item rows of 0 and 1 (their tickets read
-  // here), polls of updates kUD and kUD+1
+  float P[UD][KPL], Q[2][KPL];
+  int32_t okP[UD];  // the slot's user row was prefetched (its ticket was due)
+  int32_t tk[TD];   // ticket polls, read TD updates after they are issued
+  // prologue: the user rows of updates 0 .. UD-1 (their tickets read here), the item rows of
+  // updates 0 and 1 (SINGLE: the one item row), polls of updates UD .. UD+TD-1
 #pragma unroll
-  for (int x = 0; x < kUD; ++x) {
+  for (int x = 0; x < UD; ++x) {
     const bool live = x < cnt;
     const uint32_t u = fu(x);
     okP[x] = !live || __builtin_amdgcn_readfirstlane(poll_issue(ticket + u)) == static_cast<int32_t>(fq(x));
     rows.load(urs, live && okP[x] ? u * rowb : kOOB, P[x]);
   }
+  if constexpr (SINGLE) {
+    rows.load(irs, fi(0) * rowb, Q[0]);
+  } else {
 #pragma unroll
-  for (int x = 0; x < 2; ++x) rows.load(irs, x < cnt && (x == 0 || fi(1) != fi(0)) ? fi(x) * rowb : kOOB, Q[x]);
+    for (int x = 0; x < 2; ++x) rows.load(irs, x < cnt && (x == 0 || fi(1) != fi(0)) ? fi(x) * rowb : kOOB, Q[x]);
+  }
 #pragma unroll
-  for (int x = 0; x < 2; ++x) tk[x] = poll_issue(x + kUD < cnt ? ticket + fu(x + kUD) : dummy_ticket);
+  for (int x = 0; x < TD; ++x) tk[x] = poll_issue(x + UD < cnt ? ticket + fu(x + UD) : dummy_ticket);
   __builtin_amdgcn_s_waitcnt(0x0F70);
-  int32_t* pend0 = dummy_ticket;  // update j-2's ticket word and value
-  int32_t pv0 = 0;
-  int32_t* pend1 = dummy_ticket;  // update j-1's
-  int32_t pv1 = 0;
+  int32_t* pend[PD];  // the tickets of updates j-PD .. j-1 (word, value), published PD updates late
+  int32_t pv[PD];
+#pragma unroll
+  for (int x = 0; x < PD; ++x) {
+    pend[x] = dummy_ticket;
+    pv[x] = 0;
+  }
+  auto publish_all = [&] {
+#pragma unroll
+    for (int x = 0; x < PD; ++x) {
+      publish(pend[x], pv[x], lane);
+      pend[x] = dummy_ticket;
+    }
+  };
   float q[KPL];  // the current item's row
 #pragma unroll
-  for (int c = 0; c < KPL; ++c) q[c] = 0.f;
+  for (int c = 0; c < KPL; ++c) q[c] = SINGLE ? Q[0][c] : 0.f;
   uint32_t cur_i = 0;
 
-  // update j (chunk-relative s, a compile-time constant once unrolled); s + kUD + 2 < 2 CH
+  // update j (chunk-relative s, a compile-time constant once unrolled); s + UD + TD < 2 CH
   auto update = [&](const int s, const int32_t j) {
-    const int slot = s & 1, us = s % kUD;
+    const int slot = s & 1, us = s % UD, ts = s % TD;
     const uint32_t u = fu(s), i = fi(s);
     const int32_t qseq = static_cast<int32_t>(fq(s));
     const float r = fr(s);
-    const uint32_t uD = fu(s + kUD), qD = fq(s + kUD), uT = fu(s + kUD + 2);
-    const uint32_t i1 = fi(s + 1), i2 = fi(s + 2);
+    const uint32_t uD = fu(s + UD), qD = fq(s + UD), uT = fu(s + UD + TD);
     // 1. the user row, when its ticket was not due at prefetch time: publish the pending tickets
     //    (after their stores), wait for ours, load now
     if (!okP[us]) {
       __builtin_amdgcn_s_waitcnt(0x0F70);
-      publish(pend0, pv0, lane);
-      publish(pend1, pv1, lane);
-      pend0 = pend1 = dummy_ticket;
+      publish_all();
       wait_ticket_or_fail(ticket + u, qseq, err, lane);  // no early return (ticket_wait.hpp)
       rows.load(urs, u * rowb, P[us]);
       __builtin_amdgcn_s_waitcnt(0x0F70);
     }
     // 2. the item row: prefetched when the item changed, else the one in registers
-    if (j == 0 || i != cur_i) {
+    if constexpr (!SINGLE) {
+      if (j == 0 || i != cur_i) {
 #pragma unroll
-      for (int c = 0; c < KPL; ++c) q[c] = Q[slot][c];
+        for (int c = 0; c < KPL; ++c) q[c] = Q[slot][c];
+      }
+      cur_i = i;
     }
-    cur_i = i;
     // 3. the update (online_f32.hpp)
     float p[KPL];
 #pragma unroll
     for (int c = 0; c < KPL; ++c) p[c] = P[us][c];
     const float le = f32_err(static_cast<double>(r), f32_wave_sum(f32_lane_dot<KPL>(p, q)), eta);
     f32_sgd_next<KPL>(p, q, le);
-    // 4. update j-2's stores have landed (NW younger operations may still fly): publish its ticket
+    // 4. update j-PD's stores have landed (NW younger operations may still fly): publish its ticket
     wait_vmcnt<NW>();
-    publish(pend0, pv0, lane);
-    pend0 = pend1;
-    pv0 = pv1;
-    pend1 = ticket + u;
-    pv1 = qseq + 1;
+    publish(pend[0], pv[0], lane);
+#pragma unroll
+    for (int x = 0; x + 1 < PD; ++x) {
+      pend[x] = pend[x + 1];
+      pv[x] = pv[x + 1];
+    }
+    pend[PD - 1] = ticket + u;
+    pv[PD - 1] = qseq + 1;
     // 5. stores: the user row, and the item row when the next update is on another item (or none)
-    const bool live1 = j + 1 < cnt, live2 = j + 2 < cnt, liveD = j + kUD < cnt;
+    const bool live1 = j + 1 < cnt, live2 = j + 2 < cnt, liveD = j + UD < cnt;
     rows.store(urs, u * rowb, p);
-    rows.store(irs, !live1 || i1 != i ? i * rowb : kOOB, q);
-    // 6. prefetch: update j+kUD's user row into this user slot if its ticket (polled at j-2) is due
-    //    -- every earlier update of that user, this wave's included, has landed -- and update j+2's
-    //    item row if it starts another item's run
-    const int32_t okN = !liveD || __builtin_amdgcn_readfirstlane(tk[slot]) == static_cast<int32_t>(qD);
+    if constexpr (!SINGLE) {
+      const uint32_t i1 = fi(s + 1);
+      rows.store(irs, !live1 || i1 != i ? i * rowb : kOOB, q);
+    }
+    // 6. prefetch: update j+UD's user row into this user slot if its ticket (polled TD updates ago) is
+    //    due -- every earlier update of that user, this wave's included, has landed -- and update
+    //    j+2's item row if it starts another item's run
+    const int32_t okN = !liveD || __builtin_amdgcn_readfirstlane(tk[ts]) == static_cast<int32_t>(qD);
     rows.load(urs, liveD && okN ? uD * rowb : kOOB, P[us]);
-    rows.load(irs, live2 && i2 != i1 ? i2 * rowb : kOOB, Q[slot]);
+    if constexpr (!SINGLE) {
+      const uint32_t i1 = fi(s + 1), i2 = fi(s + 2);
+      rows.load(irs, live2 && i2 != i1 ? i2 * rowb : kOOB, Q[slot]);
+    }
     okP[us] = okN;
-    // 7. poll update j+kUD+2's ticket (read at j+2)
-    tk[slot] = poll_issue(j + kUD + 2 < cnt ? ticket + uT : dummy_ticket);
+    // 7. poll update j+UD+TD's ticket (read at j+TD)
+    tk[ts] = poll_issue(j + UD + TD < cnt ? ticket + uT : dummy_ticket);
   };
   // full chunks run their updates with no exit test in between (ticket_wait.hpp, kernels_detsweep.hip)
   for (int32_t c0 = 0;; c0 += CH) {
@@ -266,9 +292,27 @@ __global__ __launch_bounds__(64) void k_online_f32(const int64_t* __restrict__ w
     C1 = chunk(c0 / CH + 2);
   }
 done:
+  if constexpr (SINGLE) rows.store(irs, fi(0) * rowb, q);
   __builtin_amdgcn_s_waitcnt(0x0F70);
-  publish(pend0, pv0, lane);
-  publish(pend1, pv1, lane);
+  publish_all();
+}
+
+// Waves [0, nsingle) hold one item each (the online plan's heavy-item waves, kernels_online.hip).
+template <int KPL, bool FULL>
+__global__ __launch_bounds__(64) void k_online_f32(const int64_t* __restrict__ wbeg, const DetEntry* __restrict__ ent,
+                                                   const uint32_t* __restrict__ useq, float* U, float* I,
+                                                   uint64_t u_bytes, uint64_t i_bytes, int k, float eta,
+                                                   int32_t* ticket, int32_t* dummy_ticket, int32_t* err, int nsingle) {
+  const int64_t jb = wbeg[blockIdx.x];
+  const int32_t cnt = static_cast<int32_t>(wbeg[blockIdx.x + 1] - jb);
+  if (cnt <= 0) return;
+  dummy_ticket += 16 * static_cast<int64_t>(blockIdx.x);  // this wave's own scratch line
+  if (static_cast<int>(blockIdx.x) < nsingle)
+    online_wave<KPL, FULL, kSingleDepth, kSingleDepth, kPubLate, true>(jb, cnt, ent, useq, U, I, u_bytes, i_bytes, k,
+                                                                        eta, ticket, dummy_ticket, err);
+  else
+    online_wave<KPL, FULL, 2, 2, kPubLate, false>(jb, cnt, ent, useq, U, I, u_bytes, i_bytes, k, eta, ticket,
+                                                  dummy_ticket, err);
 }
 
 template <int KPL, bool FULL>
@@ -295,13 +339,13 @@ int online_f32_capacity(int k) {
 
 void launch_online_f32(hipStream_t st, int nw, const int64_t* wbeg, const DetEntry* ent, const uint32_t* useq, float* U,
                        float* I, uint64_t u_bytes, uint64_t i_bytes, int k, double eta, int32_t* ticket,
-                       int32_t* dummy_ticket, int32_t* err, hipEvent_t ev0, hipEvent_t ev1) {
+                       int32_t* dummy_ticket, int32_t* err, int nsingle, hipEvent_t ev0, hipEvent_t ev1) {
   if (nw <= 0 || !online_f32_supports(k)) return;
   const dim3 g(static_cast<unsigned>(nw)), b(64);
   const float e = static_cast<float>(eta);
 #define MF_ON(KPL, FULL)                                                                                    \
   hipExtLaunchKernelGGL((k_online_f32<KPL, FULL>), g, b, 0, st, ev0, ev1, 0, wbeg, ent, useq, U, I, u_bytes, \
-                        i_bytes, k, e, ticket, dummy_ticket, err)
+                        i_bytes, k, e, ticket, dummy_ticket, err, nsingle)
   if (k == 64) MF_ON(1, true);
   else if (k < 64) MF_ON(1, false);
   else if (k == 128) MF_ON(2, true);

@@ -2093,10 +2093,12 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
     sc.wbeg.alloc(static_cast<size_t>(W + 1) * 8);
     const uint32_t* du = sc.in.as<uint32_t>();
     sc.touched.alloc(8);
-    online_sweep_plan(s.stream, sc, du, du + n, reinterpret_cast<const double*>(du + 2 * n), n, W32,
-                      static_cast<uint32_t>(ctx->U.rows()), static_cast<uint32_t>(ctx->I.rows()),
-                      s.det_dev.as<DetEntry>(), reinterpret_cast<uint32_t*>(s.det_dev.as<char>() + ebytes),
-                      sc.wbeg.as<int64_t>(), sc.touched.as<int32_t>());
+    // waves [0, nsingle) hold one item each: k_online_f32's lean single-item path (MFHIP_TEST
+    // online_single=0: the general path for every wave, the A/B switch)
+    const uint32_t nsingle = online_sweep_plan(
+        s.stream, sc, du, du + n, reinterpret_cast<const double*>(du + 2 * n), n, W32,
+        static_cast<uint32_t>(ctx->U.rows()), static_cast<uint32_t>(ctx->I.rows()), s.det_dev.as<DetEntry>(),
+        reinterpret_cast<uint32_t*>(s.det_dev.as<char>() + ebytes), sc.wbeg.as<int64_t>(), sc.touched.as<int32_t>());
     sc.uticket.alloc(static_cast<size_t>(std::max<int64_t>(ctx->U.rows(), 1)) * 4);
     MF_HIP(hipMemsetAsync(sc.uticket.get(), 0, static_cast<size_t>(std::max<int64_t>(ctx->U.rows(), 1)) * 4, s.stream));
     sc.err.alloc(4);
@@ -2107,7 +2109,8 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
       launch_online_f32(s.stream, static_cast<int>(W), sc.wbeg.as<int64_t>(), s.det_dev.as<DetEntry>(),
                         reinterpret_cast<const uint32_t*>(s.det_dev.as<char>() + ebytes), s.uf.as<float>(),
                         s.itf.as<float>(), s.uf.bytes(), s.itf.bytes(), k, ctx->P.online_learning_rate,
-                        sc.uticket.as<int32_t>(), sc.dummy.as<int32_t>(), sc.err.as<int32_t>(), t.start(), t.stop());
+                        sc.uticket.as<int32_t>(), sc.dummy.as<int32_t>(), sc.err.as<int32_t>(),
+                        test_knob("online_single") == "0" ? 0 : static_cast<int>(nsingle), t.start(), t.stop());
     } else if (det_online) {
       // the wave table goes through the host once (W descriptors): det_slot_table pairs each
       // single-item wave with its helper and gives the longest chains a CU each

@@ -192,9 +192,12 @@ def test_online_sweep_equals_level_replay(monkeypatch, mode, k):
     i[::37] = 3  # a hot item
     r = rng.integers(1, 6, n).astype(np.float64)
     res = {}
-    kerns = ("level", "sweep", "ticket") if mode == L.MODE_DETERMINISTIC_F64 else ("level", "sweep")
+    # f32 "multi": every wave on k_online_f32's general path (online_single=0), none on the lean
+    # single-item path the heavy items' waves take by default
+    kerns = ("level", "sweep", "ticket") if mode == L.MODE_DETERMINISTIC_F64 else ("level", "sweep", "multi")
     for kern in kerns:
-        set_knob(monkeypatch, "online_kernel", kern)
+        set_knob(monkeypatch, "online_kernel", "sweep" if kern == "multi" else kern)
+        set_knob(monkeypatch, "online_single", "0" if kern == "multi" else "1")
         p = L.default_params()
         p.num_factors, p.mode, p.online_learning_rate = k, mode, 0.01
         with mfhip.Context(p) as ctx:

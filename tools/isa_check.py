@@ -265,9 +265,11 @@ def flag_store_violations(kern, kernel_re, is_flag, mode, trace=False):
     s_mov constants are followed one way only): S is covered once a wait vmcnt(N) is reached with more
     than N memory operations issued after S.  A flag store reached while S is not covered is a
     violation in mode "all"; in mode "prev" only if another flag store was passed since S (S belongs
-    to an entry whose ticket is still held back until then).  Returns ([(kernel, flag addr, reason)],
+    to an entry whose ticket is still held back until then); in mode "prevN" (N = 1..9) only if N
+    flag stores were passed since S (tickets published N + 1 entries late).  Returns ([(kernel, flag addr, reason)],
     flag stores in the checked kernels)."""
     bad, checked = [], 0
+    allowed = int(mode[4:]) if mode.startswith("prev") and mode[4:] else 1
     for name, body in kern.items():
         if not re.search(kernel_re, name):
             continue
@@ -301,7 +303,7 @@ def flag_store_violations(kern, kernel_re, is_flag, mode, trace=False):
                 if m is not None and ops >= m:
                     continue  # S has landed
                 if is_flag(x):
-                    if mode == "all" or flags > 0:
+                    if mode == "all" or flags >= allowed:
                         found = (name, x.addr, f"{x.mn} at {x.addr:#x} can publish row store {s.mn} at {s.addr:#x} "
                                                f"before it lands ({ops} later ops, waits insufficient)")
                         if trace:
@@ -313,7 +315,7 @@ def flag_store_violations(kern, kernel_re, is_flag, mode, trace=False):
                                               if is_vmem(y.mn) or y.mn == "s_waitcnt" or "branch" in y.mn
                                               or (y.mn.startswith("s_") and ("vcc" in y.ops or "s_mov" in y.mn))],)
                         break
-                    flags = 1
+                    flags = min(flags + 1, allowed)
                 if is_vmem(x.mn):
                     ops = min(ops + 1, 64)
                 env = _step_env(x, dict(envt))
@@ -346,7 +348,7 @@ CHECKS = [
     (r"k_det_sweep2", "prev", buffer_ticket),
     (r"k_det_sweep_split", "prev", buffer_ticket),
     (r"k_online_sweepId", "prev", progress_flag),
-    (r"k_online_f32", "prev", progress_flag),
+    (r"k_online_f32", "prev3", progress_flag),  # kernels_online_sweep.hip kPubLate = 4
 ]
 
 
