@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--ml20m-epochs", type=int, default=9,
                     help="ML20M leg (BASELINE config 2, full size, fast f32, k=64) beside the NFLX line: timed "
                          "epochs (0 = off; only with --config NFLX on one GPU)")
+    ap.add_argument("--block-update-reps", type=int, default=3,
+                    help="deterministic leg: timed mf_block_update calls on one NFLX rating block (0 = off)")
     ap.add_argument("--item-split", type=int, default=0,
                     help="fast mode experiment: hot-item replicas (MFHIP_ITEM_SPLIT), max ratings per item chain "
                          "per rating block (0 = off)")
@@ -378,7 +380,7 @@ def det_leg(a, k, nb, train, test, ref, stream):
         rmse, _ = ctx.rmse(*test)
         online = online_leg(ctx, stream, a) if stream is not None else None
     launch_us = sp["kernel_ms"] * 1e3 / max(sp["kernel_launches"], 1)
-    blk = block_update_bench(train, k, nb, launch_us)
+    blk = block_update_bench(train, k, nb, launch_us, a.block_update_reps) if a.block_update_reps > 0 else None
     return {"metric": "SGD rating updates/sec, deterministic f64 (the reference's exact update order)",
             "value": round(st["updates"] / el, 1), "unit": "updates/s", "dtype": "f64", "epochs": a.det_epochs,
             "ms_per_step": round(el * 1e3 / a.det_epochs, 3), "kernel": det_kernel_name(k),

@@ -189,7 +189,7 @@ __device__ __forceinline__ void online_wave(const int64_t jb, const int32_t cnt,
     rows.load(urs, live && okP[x] ? u * rowb : kOOB, P[x]);
   }
   if constexpr (SINGLE) {
-    rows.load(irs, fi(0) * rowb, Q[0]);
+    rows.load(irs, fi(0) * rowb, Q[0]);  // (every entry of the wave has this item)
   } else {
 #pragma unroll
     for (int x = 0; x < 2; ++x) rows.load(irs, x < cnt && (x == 0 || fi(1) != fi(0)) ? fi(x) * rowb : kOOB, Q[x]);
@@ -215,6 +215,7 @@ __device__ __forceinline__ void online_wave(const int64_t jb, const int32_t cnt,
 #pragma unroll
   for (int c = 0; c < KPL; ++c) q[c] = SINGLE ? Q[0][c] : 0.f;
   uint32_t cur_i = 0;
+  const uint32_t single_off = SINGLE ? fi(0) * rowb : 0u;  // (the chunks move on; the item does not)
 
   // update j (chunk-relative s, a compile-time constant once unrolled); s + UD + TD < 2 CH
   auto update = [&](const int s, const int32_t j) {
@@ -292,7 +293,7 @@ __device__ __forceinline__ void online_wave(const int64_t jb, const int32_t cnt,
     C1 = chunk(c0 / CH + 2);
   }
 done:
-  if constexpr (SINGLE) rows.store(irs, fi(0) * rowb, q);
+  if constexpr (SINGLE) rows.store(irs, single_off, q);
   __builtin_amdgcn_s_waitcnt(0x0F70);
   publish_all();
 }
