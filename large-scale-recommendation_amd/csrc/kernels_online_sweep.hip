@@ -15,16 +15,19 @@
 // loaded when the item changed, and the previous update's stores were drained every update):
 //   * updates in chunks of 16 with the update's index a compile-time constant (every field a
 //     constant-lane v_readlane), full chunks without exit tests;
-//   * user rows prefetched kUD = 4 updates ahead and item rows two ahead, after the current
-//     update's stores (an item row is only ever written by this wave; an item that recurs after
+//   * rows prefetched after the current update's stores: the general path's user AND item rows two
+//     updates ahead (an item row is only ever written by this wave; an item that recurs after
 //     another one was stored at the switch, before the prefetch, so a prefetched item row is always
-//     current; a user row is prefetched only when its ticket is due, i.e. every earlier update of
-//     that user, this wave's included, has landed).  Two ahead the hot wave waited on its user rows
-//     (NFLX batch: 0.835 ms for a 2.3k-update chain);
-//   * the ticket of update j + kUD + 2 polled at update j (read at j + 2, when that update's row is
-//     prefetched only if it is already due), and tickets published kPD = 4 updates late: update j waits only for
-//     update j - 4's stores (vmcnt(NW): the operations issued after them), so a store's round trip
-//     overlaps four updates of compute.  A wave publishes every pending ticket before it blocks;
+//     current), a heavy item's wave (one item: its row loaded once, stored once) its user rows
+//     pub_late updates ahead; a user row is prefetched only when its ticket is due, i.e. every
+//     earlier update of that user, this wave's included, has landed;
+//   * ticket polls read two (general) or pub_late (single item) updates after they are issued, and
+//     tickets published pub_late (8 at k = 64/128/256) updates late: update j waits only for update
+//     j - 8's stores (vmcnt(NW): the operations issued after them).  vmcnt counts in issue order, so
+//     a wave waits, in effect, for the nearest of these distances: with every distance 2 the hot
+//     item's wave (the batch's critical path) waited on each update's stores two updates later
+//     (NFLX 1M batch 0.835 ms; profiles/r06_online_batch_timeline.txt).  A wave publishes every
+//     pending ticket before it blocks;
 //   * the dot product is online_f32.hpp's fixed tree (~10 dependent VALU operations, not a 128-add
 //     chain); the level replay uses the same arithmetic, so both give the same factors bit for bit.
 // Every update issues the same vector-memory operations (out-of-range offsets for rows it does not
@@ -46,8 +49,11 @@ namespace {
 constexpr int kSC1 = 16;                // buffer cache policy: sc1 (L1 bypass, write-through)
 constexpr uint32_t kOOB = 0xFFFFF000u;  // a row offset past the slab: the load returns 0, no store
 constexpr int kOnChunk = 16;            // updates per register chunk
-constexpr int kSingleDepth = 4;         // single-item waves: user rows, polls and tickets this many updates apart
-constexpr int kPubLate = 4;             // every wave publishes a ticket this many updates late (tools/isa_check.py)
+// Tickets are published pub_late(OPS) updates late (OPS = vector-memory operations per row: 1 for
+// k = 64 / 128 / 256), as far as vmcnt's 63 allows the general path's count (tools/isa_check.py
+// checks the built code against it); the single-item path also prefetches user rows and reads its
+// ticket polls that many updates on.
+constexpr int pub_late(int ops) { return ops == 1 ? 8 : 4; }
 
 __device__ __forceinline__ uint32_t rl(uint32_t v, int l) {
   return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), l));
@@ -152,7 +158,7 @@ __device__ __forceinline__ void online_wave(const int64_t jb, const int32_t cnt,
                                             int32_t* err) {
   using R = Rows<KPL, FULL>;
   constexpr int CH = kOnChunk;
-  static_assert(UD + TD < 2 * CH - CH + 1 && 2 <= UD && 2 <= TD && 1 <= PD, "ring distances");
+  static_assert(UD + TD <= CH && 2 <= UD && 2 <= TD && 1 <= PD, "ring distances (s + UD + TD < 2 CH)");
   // operations issued after update j-PD's stores up to update j's publish: j-PD's loads and poll,
   // then PD-1 whole updates (publish, stores, loads, poll); SINGLE moves no item row per update
   constexpr int IO = SINGLE ? 0 : R::OPS;  // item-row operations per update (load, store)
@@ -308,12 +314,13 @@ __global__ __launch_bounds__(64) void k_online_f32(const int64_t* __restrict__ w
   const int32_t cnt = static_cast<int32_t>(wbeg[blockIdx.x + 1] - jb);
   if (cnt <= 0) return;
   dummy_ticket += 16 * static_cast<int64_t>(blockIdx.x);  // this wave's own scratch line
+  constexpr int PD = pub_late(Rows<KPL, FULL>::OPS);
   if (static_cast<int>(blockIdx.x) < nsingle)
-    online_wave<KPL, FULL, kSingleDepth, kSingleDepth, kPubLate, true>(jb, cnt, ent, useq, U, I, u_bytes, i_bytes, k,
-                                                                        eta, ticket, dummy_ticket, err);
+    online_wave<KPL, FULL, PD, PD, PD, true>(jb, cnt, ent, useq, U, I, u_bytes, i_bytes, k, eta, ticket, dummy_ticket,
+                                             err);
   else
-    online_wave<KPL, FULL, 2, 2, kPubLate, false>(jb, cnt, ent, useq, U, I, u_bytes, i_bytes, k, eta, ticket,
-                                                  dummy_ticket, err);
+    online_wave<KPL, FULL, 2, 2, PD, false>(jb, cnt, ent, useq, U, I, u_bytes, i_bytes, k, eta, ticket, dummy_ticket,
+                                            err);
 }
 
 template <int KPL, bool FULL>
