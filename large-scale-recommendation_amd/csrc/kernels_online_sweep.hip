@@ -19,11 +19,11 @@
 //     updates ahead (an item row is only ever written by this wave; an item that recurs after
 //     another one was stored at the switch, before the prefetch, so a prefetched item row is always
 //     current), a heavy item's wave (one item: its row loaded once, stored once) its user rows
-//     pub_late updates ahead; a user row is prefetched only when its ticket is due, i.e. every
+//     kSingle updates ahead; a user row is prefetched only when its ticket is due, i.e. every
 //     earlier update of that user, this wave's included, has landed;
-//   * ticket polls read two (general) or pub_late (single item) updates after they are issued, and
-//     tickets published pub_late (8 at k = 64/128/256) updates late: update j waits only for update
-//     j - 8's stores (vmcnt(NW): the operations issued after them).  vmcnt counts in issue order, so
+//   * ticket polls read two (general) or kSingle (single item) updates after they are issued, and
+//     tickets published as many updates late: update j waits only for update j - 2's (j - kSingle's)
+//     stores (vmcnt(NW): the operations issued after them).  vmcnt counts in issue order, so
 //     a wave waits, in effect, for the nearest of these distances: with every distance 2 the hot
 //     item's wave (the batch's critical path) waited on each update's stores two updates later
 //     (NFLX 1M batch 0.835 ms; profiles/r06_online_batch_timeline.txt).  A wave publishes every
@@ -49,11 +49,13 @@ namespace {
 constexpr int kSC1 = 16;                // buffer cache policy: sc1 (L1 bypass, write-through)
 constexpr uint32_t kOOB = 0xFFFFF000u;  // a row offset past the slab: the load returns 0, no store
 constexpr int kOnChunk = 16;            // updates per register chunk
-// Tickets are published pub_late(OPS) updates late (OPS = vector-memory operations per row: 1 for
-// k = 64 / 128 / 256), as far as vmcnt's 63 allows the general path's count (tools/isa_check.py
-// checks the built code against it); the single-item path also prefetches user rows and reads its
-// ticket polls that many updates on.
-constexpr int pub_late(int ops) { return ops == 1 ? 8 : 4; }
+// The general path publishes a ticket two updates late, the single-item path kSingle late, and
+// prefetches its user rows and reads its ticket polls kSingle updates on (tools/isa_check.py checks
+// the built code against both).  Measured on NFLX 1M batches (gpurun_out/r6f, r6g): every wave at
+// 2 -- 0.835 ms per launch; single 4 / general 4 -- 0.663 ms; single 8 / general 8 -- 0.806 ms
+// (a ticket published late holds its consumers back, and the hot wave's users come from the
+// general waves).
+constexpr int kSingle = 4;
 
 __device__ __forceinline__ uint32_t rl(uint32_t v, int l) {
   return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), l));
@@ -314,13 +316,12 @@ __global__ __launch_bounds__(64) void k_online_f32(const int64_t* __restrict__ w
   const int32_t cnt = static_cast<int32_t>(wbeg[blockIdx.x + 1] - jb);
   if (cnt <= 0) return;
   dummy_ticket += 16 * static_cast<int64_t>(blockIdx.x);  // this wave's own scratch line
-  constexpr int PD = pub_late(Rows<KPL, FULL>::OPS);
   if (static_cast<int>(blockIdx.x) < nsingle)
-    online_wave<KPL, FULL, PD, PD, PD, true>(jb, cnt, ent, useq, U, I, u_bytes, i_bytes, k, eta, ticket, dummy_ticket,
-                                             err);
+    online_wave<KPL, FULL, kSingle, kSingle, kSingle, true>(jb, cnt, ent, useq, U, I, u_bytes, i_bytes, k, eta, ticket,
+                                                            dummy_ticket, err);
   else
-    online_wave<KPL, FULL, 2, 2, PD, false>(jb, cnt, ent, useq, U, I, u_bytes, i_bytes, k, eta, ticket, dummy_ticket,
-                                            err);
+    online_wave<KPL, FULL, 2, 2, 2, false>(jb, cnt, ent, useq, U, I, u_bytes, i_bytes, k, eta, ticket, dummy_ticket,
+                                           err);
 }
 
 template <int KPL, bool FULL>

@@ -348,9 +348,9 @@ CHECKS = [
     (r"k_det_sweep2", "prev", buffer_ticket),
     (r"k_det_sweep_split", "prev", buffer_ticket),
     (r"k_online_sweepId", "prev", progress_flag),
-    # kernels_online_sweep.hip pub_late(OPS): 8 where a row is one access per lane, else 4
-    (r"k_online_f32ILi\dELb1E|k_online_f32ILi1ELb0E", "prev7", progress_flag),
-    (r"k_online_f32ILi[234]ELb0E", "prev3", progress_flag),
+    # kernels_online_sweep.hip: the single-item path publishes kSingle = 4 late (the general path 2,
+    # which this allowance covers too)
+    (r"k_online_f32", "prev3", progress_flag),
 ]
 
 
