@@ -34,8 +34,7 @@ bool online_f32_supports(int k);
 int online_f32_capacity(int k);
 void launch_online_f32(hipStream_t st, int nw, const int64_t* wbeg, const DetEntry* ent, const uint32_t* useq, float* U,
                        float* I, uint64_t u_bytes, uint64_t i_bytes, int k, double eta, int32_t* ticket,
-                       int32_t* dummy_ticket, int32_t* err, int nsingle, int sdepth, hipEvent_t ev0,
-                       hipEvent_t ev1);
+                       int32_t* dummy_ticket, int32_t* err, int nsingle, hipEvent_t ev0, hipEvent_t ev1);
 // k_online_sweep's inputs from one batch in sequence order (eu / ei / er: user row, item row,
 // rating of update x; device arrays), on the device (kernels_online.hip): ent / useq (n each,
 // grouped by wave = item row mod W, sequence order inside a wave, useq = the update's rank among

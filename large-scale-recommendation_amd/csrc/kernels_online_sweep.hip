@@ -56,9 +56,6 @@ constexpr int kOnChunk = 16;            // updates per register chunk
 // (a ticket published late holds its consumers back, and the hot wave's users come from the
 // general waves).
 constexpr int kSingle = 4;
-// the deeper single-item variant (MFHIP_TEST online_single_depth=8): 8 where the general count fits
-// vmcnt, 6 for the widest rows
-constexpr int deep_single(int ops) { return ops <= 3 ? 8 : 6; }
 
 __device__ __forceinline__ uint32_t rl(uint32_t v, int l) {
   return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), l));
@@ -314,17 +311,12 @@ template <int KPL, bool FULL>
 __global__ __launch_bounds__(64) void k_online_f32(const int64_t* __restrict__ wbeg, const DetEntry* __restrict__ ent,
                                                    const uint32_t* __restrict__ useq, float* U, float* I,
                                                    uint64_t u_bytes, uint64_t i_bytes, int k, float eta,
-                                                   int32_t* ticket, int32_t* dummy_ticket, int32_t* err, int nsingle,
-                                                   int sdepth) {
+                                                   int32_t* ticket, int32_t* dummy_ticket, int32_t* err, int nsingle) {
   const int64_t jb = wbeg[blockIdx.x];
   const int32_t cnt = static_cast<int32_t>(wbeg[blockIdx.x + 1] - jb);
   if (cnt <= 0) return;
   dummy_ticket += 16 * static_cast<int64_t>(blockIdx.x);  // this wave's own scratch line
-  constexpr int DS = deep_single(Rows<KPL, FULL>::OPS);
-  if (static_cast<int>(blockIdx.x) < nsingle && sdepth > kSingle)
-    online_wave<KPL, FULL, DS, DS, DS, true>(jb, cnt, ent, useq, U, I, u_bytes, i_bytes, k, eta, ticket, dummy_ticket,
-                                             err);
-  else if (static_cast<int>(blockIdx.x) < nsingle)
+  if (static_cast<int>(blockIdx.x) < nsingle)
     online_wave<KPL, FULL, kSingle, kSingle, kSingle, true>(jb, cnt, ent, useq, U, I, u_bytes, i_bytes, k, eta, ticket,
                                                             dummy_ticket, err);
   else
@@ -356,14 +348,13 @@ int online_f32_capacity(int k) {
 
 void launch_online_f32(hipStream_t st, int nw, const int64_t* wbeg, const DetEntry* ent, const uint32_t* useq, float* U,
                        float* I, uint64_t u_bytes, uint64_t i_bytes, int k, double eta, int32_t* ticket,
-                       int32_t* dummy_ticket, int32_t* err, int nsingle, int sdepth, hipEvent_t ev0,
-                       hipEvent_t ev1) {
+                       int32_t* dummy_ticket, int32_t* err, int nsingle, hipEvent_t ev0, hipEvent_t ev1) {
   if (nw <= 0 || !online_f32_supports(k)) return;
   const dim3 g(static_cast<unsigned>(nw)), b(64);
   const float e = static_cast<float>(eta);
 #define MF_ON(KPL, FULL)                                                                                    \
   hipExtLaunchKernelGGL((k_online_f32<KPL, FULL>), g, b, 0, st, ev0, ev1, 0, wbeg, ent, useq, U, I, u_bytes, \
-                        i_bytes, k, e, ticket, dummy_ticket, err, nsingle, sdepth)
+                        i_bytes, k, e, ticket, dummy_ticket, err, nsingle)
   if (k == 64) MF_ON(1, true);
   else if (k < 64) MF_ON(1, false);
   else if (k == 128) MF_ON(2, true);

@@ -2110,8 +2110,7 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
                         reinterpret_cast<const uint32_t*>(s.det_dev.as<char>() + ebytes), s.uf.as<float>(),
                         s.itf.as<float>(), s.uf.bytes(), s.itf.bytes(), k, ctx->P.online_learning_rate,
                         sc.uticket.as<int32_t>(), sc.dummy.as<int32_t>(), sc.err.as<int32_t>(),
-                        test_knob("online_single") == "0" ? 0 : static_cast<int>(nsingle),
-                        test_knob("online_single_depth") == "8" ? 8 : 4, t.start(), t.stop());
+                        test_knob("online_single") == "0" ? 0 : static_cast<int>(nsingle), t.start(), t.stop());
     } else if (det_online) {
       // the wave table goes through the host once (W descriptors): det_slot_table pairs each
       // single-item wave with its helper and gives the longest chains a CU each
