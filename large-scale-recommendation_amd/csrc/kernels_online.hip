@@ -8,10 +8,10 @@
 //             the user's ticket word reaches it)
 //   waves   : stable sort of (wave of the item row, x) -> wave w's updates in sequence order; every
 //             update of an item lands in one wave, so the item's order is the sequence order.  An
-//             item with at least the mean wave load gets a wave of its own (waves 0 .. H-1 in
-//             count-descending order, so the hottest always get one; any item -> wave map gives
-//             the same factors), the others go to H + row mod (W - H).  The hottest items' chains bound the
-//             launch, so they should not share their wave with other items' updates.
+//             item with at least the mean wave load (on a 1-in-4 sample) gets a wave of its own
+//             (waves 0 .. H-1 in row order; any item -> wave map gives the same factors), the others
+//             go to H + row mod (W - H).  The hottest items' chains bound the launch, so they should
+//             not share their wave with other items' updates.
 //   wbeg[w] : first position of wave w (lower bound in the sorted wave keys), wbeg[W] = n
 //   touched : distinct user rows (run heads of the user sort) and item rows (run heads of a
 //             key-only item sort) of the batch (UpdateSeparatedHashMap.updates,
@@ -41,32 +41,33 @@ unsigned grid_for(int64_t n) {
   return static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((n + kThreads - 1) / kThreads, 1 << 16)));
 }
 
-__global__ void k_item_count(const uint32_t* __restrict__ ei, int64_t n, uint32_t* __restrict__ cnt) {
-  for (int64_t x = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; x < n;
-       x += static_cast<int64_t>(gridDim.x) * blockDim.x)
+// per item row, the updates of every S-th entry of the batch (the heavy items only need to be found,
+// not counted exactly: any item -> wave map gives the same factors; a sample cuts the atomics on
+// the hottest counters S-fold)
+__global__ void k_item_count(const uint32_t* __restrict__ ei, int64_t n, int S, uint32_t* __restrict__ cnt) {
+  for (int64_t x = (blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x) * S; x < n;
+       x += static_cast<int64_t>(gridDim.x) * blockDim.x * S)
     atomicAdd(cnt + ei[x], 1u);
+}
+
+__global__ void k_heavy_flags(const uint32_t* __restrict__ cnt, uint32_t rows, uint32_t Ts, int32_t* __restrict__ flag) {
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < rows;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    flag[i] = cnt[i] >= Ts ? 1 : 0;
+}
+
+// iwave[item] = its rank among the heavy items in row order (< H), else -1
+__global__ void k_heavy_assign(const int32_t* __restrict__ flag, const int32_t* __restrict__ pos, uint32_t rows,
+                               uint32_t H, int32_t* __restrict__ iwave) {
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < rows;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    iwave[i] = flag[i] && static_cast<uint32_t>(pos[i]) < H ? pos[i] : -1;
 }
 
 __global__ void k_iota(int64_t n, int32_t* __restrict__ iota) {
   for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
        i += static_cast<int64_t>(gridDim.x) * blockDim.x)
     iota[i] = static_cast<int32_t>(i);
-}
-
-__global__ void k_iota_rows(uint32_t rows, int32_t* __restrict__ iota, int32_t* __restrict__ iwave) {
-  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < rows;
-       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    iota[i] = static_cast<int32_t>(i);
-    iwave[i] = -1;
-  }
-}
-
-// iwave[item] = rank r of a heavy item row in count-descending order (count >= T, r < H)
-__global__ void k_heavy(const uint32_t* __restrict__ cnt_sorted, const int32_t* __restrict__ item_sorted, uint32_t H,
-                        uint32_t T, int32_t* __restrict__ iwave) {
-  for (int64_t r = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; r < H;
-       r += static_cast<int64_t>(gridDim.x) * blockDim.x)
-    if (cnt_sorted[r] >= T) iwave[item_sorted[r]] = static_cast<int32_t>(r);
 }
 
 __global__ void k_keys(const uint32_t* __restrict__ eu, const uint32_t* __restrict__ ei, int64_t n, uint32_t W,
@@ -267,26 +268,28 @@ uint32_t online_sweep_plan(hipStream_t st, OnlineSweepScratch& sc, const uint32_
   const uint32_t T = static_cast<uint32_t>(std::max<double>(2.0, std::ceil(mult * static_cast<double>(n) / W)));
   size_t tb = 0;
   if (H > 0 && item_rows > 0) {
-    // the H most-rated items (ties by row) that reach T, by a descending radix sort of the counts
+    // the items that reach T on a 1-in-kSample sample of the batch, in row order, at most H of them
+    // (round 5 sorted the exact counts and took the H largest: 78 us of contended atomics and a
+    // radix sort per NFLX 1M batch, profiles/r06_online_batch_timeline.txt; a batch has a few dozen
+    // heavy items against H = W / 4)
+    constexpr int kSample = 4;
     const size_t ib = static_cast<size_t>(item_rows) * 4;
-    sc.icnt.alloc(2 * ib);  // counts, then the sorted counts
+    sc.icnt.alloc(ib);
     sc.iwave.alloc(ib);
-    sc.irows.alloc(2 * ib);  // row iota, then the rows in count order
+    sc.irows.alloc(2 * ib);  // flags, then their exclusive prefix
     uint32_t* cnt = sc.icnt.as<uint32_t>();
-    int32_t* rows = sc.irows.as<int32_t>();
+    int32_t* flag = sc.irows.as<int32_t>();
     MF_HIP(hipMemsetAsync(cnt, 0, ib, st));
-    hipLaunchKernelGGL(k_item_count, dim3(grid_for(n)), dim3(kThreads), 0, st, ei, n, cnt);
-    hipLaunchKernelGGL(k_iota_rows, dim3(grid_for(item_rows)), dim3(kThreads), 0, st, item_rows, rows,
-                       sc.iwave.as<int32_t>());
-    const int ni = static_cast<int>(item_rows), cb = bits_for(static_cast<uint64_t>(n) + 1);
-    MF_HIP(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tb, cnt, cnt + item_rows, rows, rows + item_rows, ni, 0,
-                                                        cb, st));
+    hipLaunchKernelGGL(k_item_count, dim3(grid_for((n + kSample - 1) / kSample)), dim3(kThreads), 0, st, ei, n, kSample,
+                       cnt);
+    const uint32_t Ts = std::max<uint32_t>(1, (T + kSample - 1) / kSample);
+    hipLaunchKernelGGL(k_heavy_flags, dim3(grid_for(item_rows)), dim3(kThreads), 0, st, cnt, item_rows, Ts, flag);
+    const int ni = static_cast<int>(item_rows);
+    MF_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, flag, flag + item_rows, ni, st));
     sc.tmp.alloc(std::max<size_t>(tb, 256));
-    MF_HIP(hipcub::DeviceRadixSort::SortPairsDescending(sc.tmp.get(), tb, cnt, cnt + item_rows, rows, rows + item_rows,
-                                                        ni, 0, cb, st));
-    const uint32_t Hn = std::min<uint32_t>(H, item_rows);
-    hipLaunchKernelGGL(k_heavy, dim3(grid_for(Hn)), dim3(kThreads), 0, st, cnt + item_rows, rows + item_rows, Hn, T,
-                       sc.iwave.as<int32_t>());
+    MF_HIP(hipcub::DeviceScan::ExclusiveSum(sc.tmp.get(), tb, flag, flag + item_rows, ni, st));
+    hipLaunchKernelGGL(k_heavy_assign, dim3(grid_for(item_rows)), dim3(kThreads), 0, st, flag, flag + item_rows,
+                       item_rows, H, sc.iwave.as<int32_t>());
   }
   hipLaunchKernelGGL(k_keys, dim3(grid_for(n)), dim3(kThreads), 0, st, eu, ei, n, W, H,
                      H > 0 && item_rows > 0 ? sc.iwave.as<int32_t>() : nullptr, sc.wkey.as<uint32_t>(),
