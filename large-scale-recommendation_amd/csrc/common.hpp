@@ -7,12 +7,17 @@
 #include <cstring>
 #include <cstdlib>
 #include <atomic>
+#include <condition_variable>
+#include <exception>
 #include <functional>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <thread>
 #include <vector>
+
+#include <unistd.h>
 
 #include "mfhip.h"
 #include "mfhip_testing.h"
@@ -208,6 +213,94 @@ inline int host_threads() {
   return static_cast<int>(std::max(1u, std::min(hc, 32u)));
 }
 
+// The host workers behind parallel_for / parallel_tasks: host_threads() - 1 threads made once per
+// process and parked on a condition variable; the calling thread runs share 0.  Starting 16
+// threads per call cost more than the work of an online micro-batch's staging copy
+// (tools/micro/host_stage.cpp).  A call from a worker (nested), a call while another thread's
+// job runs, or a call in a forked child (the pool's threads are not there) starts its own
+// threads instead, as before.  The pool is never destroyed: its parked threads end with the
+// process.
+class WorkerPool {
+ public:
+  static WorkerPool* instance() {
+    static WorkerPool* p = new WorkerPool(host_threads());
+    return p->pid_ == ::getpid() ? p : nullptr;
+  }
+  // f(0..w-1) on the caller and w-1 workers; false (nothing run) when the pool cannot take it
+  bool try_run(int w, const std::function<void(int)>& f) {
+    if (in_worker() || w - 1 > static_cast<int>(th_.size())) return false;
+    std::unique_lock<std::mutex> busy(run_, std::try_to_lock);
+    if (!busy.owns_lock()) return false;
+    {
+      std::lock_guard<std::mutex> g(m_);
+      job_ = &f;
+      width_ = w;
+      left_ = w - 1;
+      ++gen_;
+    }
+    wake_.notify_all();
+    std::exception_ptr err;
+    in_worker() = true;  // a parallel_for inside f(0) starts threads of its own (run_ is held)
+    try {
+      f(0);
+    } catch (...) {
+      err = std::current_exception();  // the workers still hold f: wait for them first
+    }
+    in_worker() = false;
+    std::unique_lock<std::mutex> lk(m_);
+    done_.wait(lk, [&] { return left_ == 0; });
+    job_ = nullptr;
+    lk.unlock();
+    if (err) std::rethrow_exception(err);
+    return true;
+  }
+
+ private:
+  explicit WorkerPool(int n) : pid_(::getpid()) {
+    for (int t = 1; t < n; ++t) th_.emplace_back([this, t] { loop(t); });
+    for (auto& x : th_) x.detach();
+  }
+  static bool& in_worker() {
+    static thread_local bool w = false;
+    return w;
+  }
+  void loop(int t) {
+    in_worker() = true;
+    uint64_t seen = 0;
+    std::unique_lock<std::mutex> lk(m_);
+    for (;;) {
+      wake_.wait(lk, [&] { return gen_ != seen; });
+      seen = gen_;
+      if (t >= width_) continue;  // not part of this job
+      const std::function<void(int)>* f = job_;
+      lk.unlock();
+      (*f)(t);  // an exception here ends the process, as it did in a std::thread of its own
+      lk.lock();
+      if (--left_ == 0) done_.notify_one();
+    }
+  }
+  const pid_t pid_;
+  std::vector<std::thread> th_;
+  std::mutex run_, m_;
+  std::condition_variable wake_, done_;
+  uint64_t gen_ = 0;
+  const std::function<void(int)>* job_ = nullptr;
+  int width_ = 0, left_ = 0;
+};
+
+// f(0..w-1), one share per host worker
+inline void run_workers(int w, const std::function<void(int)>& f) {
+  if (w <= 1) {
+    f(0);
+    return;
+  }
+  if (WorkerPool* p = WorkerPool::instance(); p && p->try_run(w, f)) return;
+  std::vector<std::thread> th;
+  th.reserve(w);
+  for (int t = 0; t < w; ++t) th.emplace_back(f, t);
+  for (auto& x : th) x.join();
+}
+
 // parallel_for over [0, n) in contiguous chunks; fn(begin, end, worker).
 inline void parallel_for(int64_t n, const std::function<void(int64_t, int64_t, int)>& fn,
                          int max_workers = 0, int64_t min_chunk = 1 << 14) {
@@ -215,15 +308,11 @@ inline void parallel_for(int64_t n, const std::function<void(int64_t, int64_t, i
   int w = max_workers > 0 ? max_workers : host_threads();
   w = static_cast<int>(std::min<int64_t>(w, (n + min_chunk - 1) / min_chunk));
   if (w <= 1) { fn(0, n, 0); return; }
-  std::vector<std::thread> th;
-  th.reserve(w);
   const int64_t chunk = (n + w - 1) / w;
-  for (int t = 0; t < w; ++t) {
-    int64_t b = t * chunk, e = std::min(n, b + chunk);
-    if (b >= e) break;
-    th.emplace_back(fn, b, e, t);
-  }
-  for (auto& x : th) x.join();
+  run_workers(w, [&](int t) {
+    const int64_t b = t * chunk, e = std::min(n, b + chunk);
+    if (b < e) fn(b, e, t);
+  });
 }
 
 // parallel over independent tasks 0..n-1, dynamically: each worker takes the next task index
@@ -234,10 +323,7 @@ inline void parallel_tasks(int64_t n, const std::function<void(int64_t)>& fn, in
   w = static_cast<int>(std::min<int64_t>(w, n));
   if (w <= 1) { for (int64_t t = 0; t < n; ++t) fn(t); return; }
   std::atomic<int64_t> next{0};
-  std::vector<std::thread> th;
-  for (int t = 0; t < w; ++t)
-    th.emplace_back([&] { for (int64_t x; (x = next.fetch_add(1)) < n;) fn(x); });
-  for (auto& x : th) x.join();
+  run_workers(w, [&](int) { for (int64_t x; (x = next.fetch_add(1)) < n;) fn(x); });
 }
 
 // Releases large host buffers on a background thread: returning a touched multi-GB allocation

@@ -39,12 +39,14 @@ void launch_online_f32(hipStream_t st, int nw, const int64_t* wbeg, const DetEnt
 // rating of update x; device arrays), on the device (kernels_online.hip): ent / useq (n each,
 // grouped by wave = item row mod W, sequence order inside a wave, useq = the update's rank among
 // its user's updates) and wbeg (W + 1); touched[0..1] = distinct user / item rows of the batch.
-// user_rows / item_rows bound eu / ei.
+// user_rows / item_rows bound eu / ei.  erf non-null: the ratings are floats there (the f32
+// sweep's upload) and er is not read.
 struct OnlineSweepScratch;
 // Returns H: waves [0, H) hold one item each (the heavy items), the others any number.
 uint32_t online_sweep_plan(hipStream_t st, OnlineSweepScratch& sc, const uint32_t* eu, const uint32_t* ei,
                            const double* er, int64_t n, uint32_t W, uint32_t user_rows, uint32_t item_rows,
-                           DetEntry* ent, uint32_t* useq, int64_t* wbeg, int32_t* touched);
+                           DetEntry* ent, uint32_t* useq, int64_t* wbeg, int32_t* touched,
+                           const float* erf = nullptr);
 // The online batch's id -> row lookup on the device, over a mirror of the host IdIndex (same
 // hash, same slots; id_index.hpp): in[0, n) user ids and in[n, 2n) item ids (the batch as
 // uploaded) are replaced by their rows, 0xFFFFFFFF where the table has no such id; *misses counts

@@ -97,14 +97,17 @@ __global__ void k_tickets(const int32_t* __restrict__ ux, const int32_t* __restr
     ticket[ux[p]] = static_cast<uint32_t>(p - start[p]);
 }
 
+// R: the uploaded ratings' type (float: the f32 sweep's upload, rounded on the host -- the sweep
+// rounds r to float first in any case, online_f32.hpp)
+template <typename R>
 __global__ void k_gather(const int32_t* __restrict__ wx, const uint32_t* __restrict__ eu,
-                         const uint32_t* __restrict__ ei, const double* __restrict__ er,
+                         const uint32_t* __restrict__ ei, const R* __restrict__ er,
                          const uint32_t* __restrict__ ticket, int64_t n, DetEntry* __restrict__ ent,
                          uint32_t* __restrict__ useq) {
   for (int64_t y = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; y < n;
        y += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     const int32_t x = wx[y];
-    ent[y] = DetEntry{eu[x], ei[x], er[x]};
+    ent[y] = DetEntry{eu[x], ei[x], static_cast<double>(er[x])};
     useq[y] = ticket[x];
   }
 }
@@ -245,7 +248,7 @@ void online_det_entries(hipStream_t st, OnlineSweepScratch& sc, const DetEntry* 
 
 uint32_t online_sweep_plan(hipStream_t st, OnlineSweepScratch& sc, const uint32_t* eu, const uint32_t* ei,
                            const double* er, int64_t n, uint32_t W, uint32_t user_rows, uint32_t item_rows,
-                           DetEntry* ent, uint32_t* useq, int64_t* wbeg, int32_t* touched) {
+                           DetEntry* ent, uint32_t* useq, int64_t* wbeg, int32_t* touched, const float* erf) {
   MF_REQUIRE(n > 0 && n < (int64_t{1} << 31) && W >= 1, "online sweep plan: bad batch shape");
   const int N = static_cast<int>(n);
   sc.ukey.alloc(n * 4);
@@ -347,8 +350,12 @@ uint32_t online_sweep_plan(hipStream_t st, OnlineSweepScratch& sc, const uint32_
   hipLaunchKernelGGL(k_wave_begin, dim3(grid_for(W + 1)), dim3(kThreads), 0, st, sc.wkey2.as<uint32_t>(), n, W,
                      wbeg);
   MF_HIP(hipStreamWaitEvent(st, sc.ev2, 0));
-  hipLaunchKernelGGL(k_gather, dim3(grid_for(n)), dim3(kThreads), 0, st, sc.wx.as<int32_t>(), eu, ei, er,
-                     sc.ticket.as<uint32_t>(), n, ent, useq);
+  if (erf)
+    hipLaunchKernelGGL(k_gather<float>, dim3(grid_for(n)), dim3(kThreads), 0, st, sc.wx.as<int32_t>(), eu, ei, erf,
+                       sc.ticket.as<uint32_t>(), n, ent, useq);
+  else
+    hipLaunchKernelGGL(k_gather<double>, dim3(grid_for(n)), dim3(kThreads), 0, st, sc.wx.as<int32_t>(), eu, ei, er,
+                       sc.ticket.as<uint32_t>(), n, ent, useq);
   MF_HIP(hipStreamWaitEvent(st, sc.ev3, 0));  // touched[1]; and nothing on s3 outlives the plan
   MF_HIP(hipGetLastError());
   return H > 0 && item_rows > 0 ? H : 0;

@@ -1909,6 +1909,18 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
   // the sweep in arrival order takes the rows straight into its pinned upload buffer (user rows,
   // item rows, ratings: 16 B per rating), with no staging pass; otherwise they go to on_ur / on_ir
   const bool direct = cap > 0 && flavour != MF_ONLINE_SPARK_SWEEP;
+  // the f32 sweep's upload carries the ratings as floats (12 B per rating instead of 16): the
+  // sweep rounds each rating to float first in any case (online_f32.hpp), so the bits are the same
+  const bool rf32 = f32_online;
+  const size_t in_bytes = static_cast<size_t>(n) * (rf32 ? 12 : 16);
+  auto stage_r = [&](void* dst, int64_t lo2, int64_t hi2) {  // ratings [lo2, hi2) into the upload's rating array
+    if (rf32) {
+      float* f = static_cast<float*>(dst);
+      for (int64_t x = lo2; x < hi2; ++x) f[x] = static_cast<float>(r[x]);
+    } else {
+      std::memcpy(static_cast<double*>(dst) + lo2, r + lo2, static_cast<size_t>(hi2 - lo2) * 8);
+    }
+  };
   uint32_t* ur = nullptr;
   uint32_t* ir = nullptr;
   if (direct) {
@@ -1944,17 +1956,16 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
     OnlineSweepScratch& sc = s.online_sc;
     sync_dev_index(s, ctx->U.index, s.didx[0]);
     sync_dev_index(s, ctx->I.index, s.didx[1]);
-    const size_t ibytes = static_cast<size_t>(n) * 16;
-    sc.in.alloc(ibytes);
+    sc.in.alloc(in_bytes);
     // (staging in pieces with each piece's upload queued behind it was slower: 2-3 ms against ~1 ms
     // per NFLX batch, gpurun_out/r6d)
     parallel_for(n, [&](int64_t lo2, int64_t hi2, int) {
       const size_t c = static_cast<size_t>(hi2 - lo2);
       std::memcpy(ur + lo2, u + lo2, c * 4);
       std::memcpy(ir + lo2, i + lo2, c * 4);
-      std::memcpy(reinterpret_cast<double*>(ir + n) + lo2, r + lo2, c * 8);
+      stage_r(ir + n, lo2, hi2);
     });
-    MF_HIP(hipMemcpyAsync(sc.in.get(), ur, ibytes, hipMemcpyHostToDevice, s.stream));
+    MF_HIP(hipMemcpyAsync(sc.in.get(), ur, in_bytes, hipMemcpyHostToDevice, s.stream));
     clk.lap("online: staging + upload");
     sc.miss.alloc(4);
     MF_HIP(hipMemsetAsync(sc.miss.get(), 0, 4, s.stream));
@@ -1974,7 +1985,7 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
     parallel_for(n, [&](int64_t lo2, int64_t hi2, int) {
       ctx->U.index.find_many(u + lo2, hi2 - lo2, ur + lo2);
       ctx->I.index.find_many(i + lo2, hi2 - lo2, ir + lo2);
-      if (direct) std::memcpy(reinterpret_cast<double*>(ir + n) + lo2, r + lo2, static_cast<size_t>(hi2 - lo2) * 8);
+      if (direct) stage_r(ir + n, lo2, hi2);
       int64_t m = 0;
       for (int64_t j = lo2; j < hi2; ++j) m += (ur[j] == kMiss) + (ir[j] == kMiss);
       misses += m;
@@ -2067,27 +2078,28 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
     // tickets are built on the device (online_sweep_plan, kernels_online.hip)
     OnlineSweepScratch& sc = s.online_sc;
     const size_t ebytes = static_cast<size_t>(n) * sizeof(DetEntry), qbytes = static_cast<size_t>(n) * 4;
-    const size_t ibytes = static_cast<size_t>(n) * 16;
     if (!direct) {  // the Spark-sweep order: staged here
       MF_HIP(hipStreamSynchronize(s.stream));  // det_pin may still feed an earlier copy
-      s.det_pin.alloc(ibytes);
+      s.det_pin.alloc(in_bytes);
       uint32_t* pu = s.det_pin.as<uint32_t>();
       uint32_t* pi = pu + n;
       double* pr = reinterpret_cast<double*>(pi + n);
+      float* prf = reinterpret_cast<float*>(pi + n);
       parallel_for(n, [&](int64_t lo2, int64_t hi2, int) {
         for (int64_t x = lo2; x < hi2; ++x) {
           const int32_t j = order[x];
           pu[x] = ur[j];
           pi[x] = ir[j];
-          pr[x] = r[j];
+          if (rf32) prf[x] = static_cast<float>(r[j]);
+          else pr[x] = r[j];
         }
       });
       clk.lap("online: sweep staging");
     }
     uint32_t* pu = s.det_pin.as<uint32_t>();
     if (!uploaded) {  // (the device lookup left the batch's rows in sc.in already)
-      sc.in.alloc(ibytes);
-      MF_HIP(hipMemcpyAsync(sc.in.get(), pu, ibytes, hipMemcpyHostToDevice, s.stream));
+      sc.in.alloc(in_bytes);
+      MF_HIP(hipMemcpyAsync(sc.in.get(), pu, in_bytes, hipMemcpyHostToDevice, s.stream));
     }
     s.det_dev.alloc(ebytes + qbytes);
     sc.wbeg.alloc(static_cast<size_t>(W + 1) * 8);
@@ -2098,7 +2110,8 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
     const uint32_t nsingle = online_sweep_plan(
         s.stream, sc, du, du + n, reinterpret_cast<const double*>(du + 2 * n), n, W32,
         static_cast<uint32_t>(ctx->U.rows()), static_cast<uint32_t>(ctx->I.rows()), s.det_dev.as<DetEntry>(),
-        reinterpret_cast<uint32_t*>(s.det_dev.as<char>() + ebytes), sc.wbeg.as<int64_t>(), sc.touched.as<int32_t>());
+        reinterpret_cast<uint32_t*>(s.det_dev.as<char>() + ebytes), sc.wbeg.as<int64_t>(), sc.touched.as<int32_t>(),
+        rf32 ? reinterpret_cast<const float*>(du + 2 * n) : nullptr);
     sc.uticket.alloc(static_cast<size_t>(std::max<int64_t>(ctx->U.rows(), 1)) * 4);
     MF_HIP(hipMemsetAsync(sc.uticket.get(), 0, static_cast<size_t>(std::max<int64_t>(ctx->U.rows(), 1)) * 4, s.stream));
     sc.err.alloc(4);
