@@ -29,12 +29,14 @@ void launch_online_sweep(hipStream_t st, int nw, const int64_t* wbeg, const DetE
                          void* U, void* I, int k, double eta, bool f64, int32_t* ticket, int32_t* err);
 // The f32 batch at k <= 256 (k_online_f32, kernels_online_sweep.hip): the same plan and tickets,
 // rows and tickets pipelined two updates deep, the dot product of online_f32.hpp (the f32 level
-// replay's).  dummy_ticket: 16 int32 per wave of scratch.  ev0 / ev1 (may be null) time the launch.
+// replay's).  dummy_ticket: 16 int32 per wave of scratch.  skip (may be null): the launch does
+// nothing when *skip != 0 (read on the device).  ev0 / ev1 (may be null) time the launch.
 bool online_f32_supports(int k);
 int online_f32_capacity(int k);
 void launch_online_f32(hipStream_t st, int nw, const int64_t* wbeg, const DetEntry* ent, const uint32_t* useq, float* U,
                        float* I, uint64_t u_bytes, uint64_t i_bytes, int k, double eta, int32_t* ticket,
-                       int32_t* dummy_ticket, int32_t* err, int nsingle, hipEvent_t ev0, hipEvent_t ev1);
+                       int32_t* dummy_ticket, int32_t* err, int nsingle, const int32_t* skip, hipEvent_t ev0,
+                       hipEvent_t ev1);
 // k_online_sweep's inputs from one batch in sequence order (eu / ei / er: user row, item row,
 // rating of update x; device arrays), on the device (kernels_online.hip): ent / useq (n each,
 // grouped by wave = item row mod W, sequence order inside a wave, useq = the update's rank among

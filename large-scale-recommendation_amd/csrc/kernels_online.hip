@@ -43,11 +43,15 @@ unsigned grid_for(int64_t n) {
 
 // per item row, the updates of every S-th entry of the batch (the heavy items only need to be found,
 // not counted exactly: any item -> wave map gives the same factors; a sample cuts the atomics on
-// the hottest counters S-fold)
-__global__ void k_item_count(const uint32_t* __restrict__ ei, int64_t n, int S, uint32_t* __restrict__ cnt) {
+// the hottest counters S-fold).  Rows >= rows (an id the device lookup did not find: the plan is
+// built before the host has seen the miss count, and rebuilt when there are misses) are skipped.
+__global__ void k_item_count(const uint32_t* __restrict__ ei, int64_t n, int S, uint32_t rows,
+                             uint32_t* __restrict__ cnt) {
   for (int64_t x = (blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x) * S; x < n;
-       x += static_cast<int64_t>(gridDim.x) * blockDim.x * S)
-    atomicAdd(cnt + ei[x], 1u);
+       x += static_cast<int64_t>(gridDim.x) * blockDim.x * S) {
+    const uint32_t i = ei[x];
+    if (i < rows) atomicAdd(cnt + i, 1u);
+  }
 }
 
 __global__ void k_heavy_flags(const uint32_t* __restrict__ cnt, uint32_t rows, uint32_t Ts, int32_t* __restrict__ flag) {
@@ -71,12 +75,12 @@ __global__ void k_iota(int64_t n, int32_t* __restrict__ iota) {
 }
 
 __global__ void k_keys(const uint32_t* __restrict__ eu, const uint32_t* __restrict__ ei, int64_t n, uint32_t W,
-                       uint32_t H, const int32_t* __restrict__ iwave, uint32_t* __restrict__ wkey,
+                       uint32_t H, const int32_t* __restrict__ iwave, uint32_t rows, uint32_t* __restrict__ wkey,
                        int32_t* __restrict__ iota) {
   for (int64_t x = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; x < n;
        x += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     const uint32_t i = ei[x];
-    const int32_t w = iwave ? iwave[i] : -1;
+    const int32_t w = iwave && i < rows ? iwave[i] : -1;  // (i >= rows: a miss, k_item_count)
     wkey[x] = w >= 0 ? static_cast<uint32_t>(w) : H + i % (W - H);
     iota[x] = static_cast<int32_t>(x);
   }
@@ -284,7 +288,7 @@ uint32_t online_sweep_plan(hipStream_t st, OnlineSweepScratch& sc, const uint32_
     int32_t* flag = sc.irows.as<int32_t>();
     MF_HIP(hipMemsetAsync(cnt, 0, ib, st));
     hipLaunchKernelGGL(k_item_count, dim3(grid_for((n + kSample - 1) / kSample)), dim3(kThreads), 0, st, ei, n, kSample,
-                       cnt);
+                       item_rows, cnt);
     const uint32_t Ts = std::max<uint32_t>(1, (T + kSample - 1) / kSample);
     hipLaunchKernelGGL(k_heavy_flags, dim3(grid_for(item_rows)), dim3(kThreads), 0, st, cnt, item_rows, Ts, flag);
     const int ni = static_cast<int>(item_rows);
@@ -295,7 +299,7 @@ uint32_t online_sweep_plan(hipStream_t st, OnlineSweepScratch& sc, const uint32_
                        item_rows, H, sc.iwave.as<int32_t>());
   }
   hipLaunchKernelGGL(k_keys, dim3(grid_for(n)), dim3(kThreads), 0, st, eu, ei, n, W, H,
-                     H > 0 && item_rows > 0 ? sc.iwave.as<int32_t>() : nullptr, sc.wkey.as<uint32_t>(),
+                     H > 0 && item_rows > 0 ? sc.iwave.as<int32_t>() : nullptr, item_rows, sc.wkey.as<uint32_t>(),
                      sc.iota.as<int32_t>());
   const int ub = bits_for(user_rows), wb = bits_for(W);
   // tickets on s2 (user sort, run starts, ranks) and the touched items on s3 (a key-only item sort)

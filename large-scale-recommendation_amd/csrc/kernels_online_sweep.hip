@@ -307,11 +307,16 @@ done:
 }
 
 // Waves [0, nsingle) hold one item each (the online plan's heavy-item waves, kernels_online.hip).
+// skip (may be null): a non-zero count there -- ids the device lookup did not find -- makes every
+// wave return at once (the host was not waiting for that count; it rebuilds the batch and runs it
+// again).
 template <int KPL, bool FULL>
 __global__ __launch_bounds__(64) void k_online_f32(const int64_t* __restrict__ wbeg, const DetEntry* __restrict__ ent,
                                                    const uint32_t* __restrict__ useq, float* U, float* I,
                                                    uint64_t u_bytes, uint64_t i_bytes, int k, float eta,
-                                                   int32_t* ticket, int32_t* dummy_ticket, int32_t* err, int nsingle) {
+                                                   int32_t* ticket, int32_t* dummy_ticket, int32_t* err, int nsingle,
+                                                   const int32_t* __restrict__ skip) {
+  if (skip && *skip != 0) return;
   const int64_t jb = wbeg[blockIdx.x];
   const int32_t cnt = static_cast<int32_t>(wbeg[blockIdx.x + 1] - jb);
   if (cnt <= 0) return;
@@ -348,13 +353,14 @@ int online_f32_capacity(int k) {
 
 void launch_online_f32(hipStream_t st, int nw, const int64_t* wbeg, const DetEntry* ent, const uint32_t* useq, float* U,
                        float* I, uint64_t u_bytes, uint64_t i_bytes, int k, double eta, int32_t* ticket,
-                       int32_t* dummy_ticket, int32_t* err, int nsingle, hipEvent_t ev0, hipEvent_t ev1) {
+                       int32_t* dummy_ticket, int32_t* err, int nsingle, const int32_t* skip, hipEvent_t ev0,
+                       hipEvent_t ev1) {
   if (nw <= 0 || !online_f32_supports(k)) return;
   const dim3 g(static_cast<unsigned>(nw)), b(64);
   const float e = static_cast<float>(eta);
 #define MF_ON(KPL, FULL)                                                                                    \
   hipExtLaunchKernelGGL((k_online_f32<KPL, FULL>), g, b, 0, st, ev0, ev1, 0, wbeg, ent, useq, U, I, u_bytes, \
-                        i_bytes, k, e, ticket, dummy_ticket, err, nsingle)
+                        i_bytes, k, e, ticket, dummy_ticket, err, nsingle, skip)
   if (k == 64) MF_ON(1, true);
   else if (k < 64) MF_ON(1, false);
   else if (k == 128) MF_ON(2, true);

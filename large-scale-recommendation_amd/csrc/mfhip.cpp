@@ -96,6 +96,7 @@ struct Shard {
   PinnedBuf det_pin;
   OnlineSweepScratch online_sc;  // online micro-batches (k_online_sweep)
   DevIndex didx[2];              // device mirrors of the user [0] / item [1] IdIndex (online id lookup)
+  PinnedBuf small_pin;           // online batch: {lookup misses, sweep error, touched users, items}, read back async
   DevBuf blk_u, blk_i, blk_ru, blk_ri;  // mf_block_update: the block's factor rows and lambda / omega
   // fast mode
   DevBuf fast_recs, fast_cells, fast_blks;
@@ -1245,7 +1246,7 @@ struct PhaseClock {
   void lap(const char* what) {
     if (!on) return;
     const auto now = std::chrono::steady_clock::now();
-    std::fprintf(stderr, "[mfhip] %-28s %8.3f s\n", what, std::chrono::duration<double>(now - t).count());
+    std::fprintf(stderr, "[mfhip] %-28s %10.3f ms\n", what, 1e3 * std::chrono::duration<double>(now - t).count());
     t = now;
   }
 };
@@ -1951,6 +1952,57 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
   // online_lookup=host keeps the host lookup (the tests compare the two bit for bit).
   const bool dev_lookup = direct && test_knob("online_lookup") != "host";
   bool uploaded = false;
+  // the sweep's device plan (online_sweep_plan) of the batch in sc.in.  On the device-lookup path it
+  // is queued right behind the lookup, before the host waits for the miss count, so the host's ~100
+  // plan launches overlap the upload's DMA; misses (new ids) void it and it runs again after the
+  // host has given them rows.
+  int64_t W = 1;
+  if (cap > 0) {
+    int64_t wmax = 4096;
+    if (const char* v = exp_knob("MFHIP_ONLINE_WAVES")) wmax = std::max(1, std::atoi(v));
+    W = std::max<int64_t>(1, std::min<int64_t>({static_cast<int64_t>(cap / 2), wmax, n}));
+  }
+  const size_t ebytes = static_cast<size_t>(n) * sizeof(DetEntry), qbytes = static_cast<size_t>(n) * 4;
+  bool planned = false;
+  uint32_t nsingle = 0;
+  auto plan_batch = [&]() {
+    OnlineSweepScratch& sc = s.online_sc;
+    s.det_dev.alloc(ebytes + qbytes);
+    sc.wbeg.alloc(static_cast<size_t>(W + 1) * 8);
+    sc.touched.alloc(8);
+    const uint32_t* du = sc.in.as<uint32_t>();
+    // waves [0, nsingle) hold one item each: k_online_f32's lean single-item path
+    nsingle = online_sweep_plan(
+        s.stream, sc, du, du + n, reinterpret_cast<const double*>(du + 2 * n), n, static_cast<uint32_t>(W),
+        static_cast<uint32_t>(ctx->U.rows()), static_cast<uint32_t>(ctx->I.rows()), s.det_dev.as<DetEntry>(),
+        reinterpret_cast<uint32_t*>(s.det_dev.as<char>() + ebytes), sc.wbeg.as<int64_t>(), sc.touched.as<int32_t>(),
+        rf32 ? reinterpret_cast<const float*>(du + 2 * n) : nullptr);
+    planned = true;
+  };
+  // the f32 sweep of the planned batch, queued with its error word and touched counts read back into
+  // pinned memory (pin4[1..3]); skip: the lookup's miss count (the launch does nothing when non-zero)
+  s.small_pin.alloc(16);
+  int32_t* pin4 = s.small_pin.as<int32_t>();
+  auto queue_f32_sweep = [&](const int32_t* skip) {
+    OnlineSweepScratch& sc = s.online_sc;
+    const size_t ub = static_cast<size_t>(std::max<int64_t>(ctx->U.rows(), 1)) * 4;
+    sc.uticket.alloc(ub);
+    MF_HIP(hipMemsetAsync(sc.uticket.get(), 0, ub, s.stream));
+    sc.err.alloc(4);
+    MF_HIP(hipMemsetAsync(sc.err.get(), 0, 4, s.stream));
+    sc.dummy.alloc(static_cast<size_t>(W) * 64);
+    {
+      LaunchTimer t(s, ctx->profiling, true);
+      launch_online_f32(s.stream, static_cast<int>(W), sc.wbeg.as<int64_t>(), s.det_dev.as<DetEntry>(),
+                        reinterpret_cast<const uint32_t*>(s.det_dev.as<char>() + ebytes), s.uf.as<float>(),
+                        s.itf.as<float>(), s.uf.bytes(), s.itf.bytes(), k, ctx->P.online_learning_rate,
+                        sc.uticket.as<int32_t>(), sc.dummy.as<int32_t>(), sc.err.as<int32_t>(),
+                        test_knob("online_single") == "0" ? 0 : static_cast<int>(nsingle), skip, t.start(), t.stop());
+    }
+    MF_HIP(hipGetLastError());
+    MF_HIP(hipMemcpyAsync(pin4 + 1, sc.err.get(), 4, hipMemcpyDeviceToHost, s.stream));
+    MF_HIP(hipMemcpyAsync(pin4 + 2, sc.touched.get(), 8, hipMemcpyDeviceToHost, s.stream));
+  };
   if (dev_lookup) {
     DeviceGuard g(s.device);
     OnlineSweepScratch& sc = s.online_sc;
@@ -1972,11 +2024,35 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
     const DevIndex &du = s.didx[0], &di = s.didx[1];
     launch_id_lookup(s.stream, sc.in.as<uint32_t>(), n, du.cap ? du.slots.get() : nullptr, du.cap - 1,
                      di.cap ? di.slots.get() : nullptr, di.cap - 1, sc.miss.as<int32_t>());
-    int32_t m = 0;
-    MF_HIP(hipMemcpyAsync(&m, sc.miss.get(), 4, hipMemcpyDeviceToHost, s.stream));
+    MF_HIP(hipMemcpyAsync(pin4, sc.miss.get(), 4, hipMemcpyDeviceToHost, s.stream));
+    plan_batch();  // (the plan's kernels skip rows past the tables: the misses)
+    // f32: the sweep goes right behind the plan, so the batch runs through without the host in the
+    // loop; a batch with misses skips it on the device and takes the path below
+    const bool queued = f32_online;
+    if (queued) {
+      ensure_rows(ctx, s, kSideU, std::max<int64_t>(ctx->U.rows(), 1));
+      ensure_rows(ctx, s, MF_SIDE_ITEM, std::max<int64_t>(ctx->I.rows(), 1));
+      queue_f32_sweep(sc.miss.as<int32_t>());
+    }
+    clk.lap("online: lookup + plan queued");
     MF_HIP(hipStreamSynchronize(s.stream));
+    const int32_t m = pin4[0];
     misses = m;
+    if (queued && m == 0) {
+      clk.lap("online: sweep (device)");
+      if (pin4[1]) {
+        ctx->failed = "online sweep: a wave waited > 1 s for a user ticket (waves not co-resident?); "
+                      "set MFHIP_TEST=online_kernel=level (INTEGRATION.md section 5)";
+        fail(MF_ERR_TIMEOUT, ctx->failed);
+      }
+      if (tu) *tu = pin4[2];
+      if (ti) *ti = pin4[3];
+      ctx->stats.kernel_launches += 1;
+      ctx->stats.updates += n;
+      return;
+    }
     if (m > 0) {  // the rows as found (kMiss where absent) back into the pinned buffer
+      planned = false;
       MF_HIP(hipMemcpyAsync(ur, sc.in.get(), static_cast<size_t>(n) * 8, hipMemcpyDeviceToHost, s.stream));
       MF_HIP(hipStreamSynchronize(s.stream));
     }
@@ -2070,14 +2146,10 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
     // one persistent launch (k_online_sweep): items spread over the waves, each wave's updates in
     // sequence order, and per update the number of earlier updates of its user (its ticket value)
     DeviceGuard g(s.device);
-    int64_t wmax = 4096;
-    if (const char* v = exp_knob("MFHIP_ONLINE_WAVES")) wmax = std::max(1, std::atoi(v));
-    const int64_t W = std::max<int64_t>(1, std::min<int64_t>({static_cast<int64_t>(cap / 2), wmax, n}));
     const uint32_t W32 = static_cast<uint32_t>(W);
     // the batch in sequence order goes up as is (16 bytes an update); the per-wave lists and the
     // tickets are built on the device (online_sweep_plan, kernels_online.hip)
     OnlineSweepScratch& sc = s.online_sc;
-    const size_t ebytes = static_cast<size_t>(n) * sizeof(DetEntry), qbytes = static_cast<size_t>(n) * 4;
     if (!direct) {  // the Spark-sweep order: staged here
       MF_HIP(hipStreamSynchronize(s.stream));  // det_pin may still feed an earlier copy
       s.det_pin.alloc(in_bytes);
@@ -2101,30 +2173,15 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
       sc.in.alloc(in_bytes);
       MF_HIP(hipMemcpyAsync(sc.in.get(), pu, in_bytes, hipMemcpyHostToDevice, s.stream));
     }
-    s.det_dev.alloc(ebytes + qbytes);
-    sc.wbeg.alloc(static_cast<size_t>(W + 1) * 8);
-    const uint32_t* du = sc.in.as<uint32_t>();
-    sc.touched.alloc(8);
-    // waves [0, nsingle) hold one item each: k_online_f32's lean single-item path (MFHIP_TEST
-    // online_single=0: the general path for every wave, the A/B switch)
-    const uint32_t nsingle = online_sweep_plan(
-        s.stream, sc, du, du + n, reinterpret_cast<const double*>(du + 2 * n), n, W32,
-        static_cast<uint32_t>(ctx->U.rows()), static_cast<uint32_t>(ctx->I.rows()), s.det_dev.as<DetEntry>(),
-        reinterpret_cast<uint32_t*>(s.det_dev.as<char>() + ebytes), sc.wbeg.as<int64_t>(), sc.touched.as<int32_t>(),
-        rf32 ? reinterpret_cast<const float*>(du + 2 * n) : nullptr);
-    sc.uticket.alloc(static_cast<size_t>(std::max<int64_t>(ctx->U.rows(), 1)) * 4);
-    MF_HIP(hipMemsetAsync(sc.uticket.get(), 0, static_cast<size_t>(std::max<int64_t>(ctx->U.rows(), 1)) * 4, s.stream));
-    sc.err.alloc(4);
-    MF_HIP(hipMemsetAsync(sc.err.get(), 0, 4, s.stream));
+    if (!planned) plan_batch();
     if (f32_online) {
-      sc.dummy.alloc(static_cast<size_t>(W) * 64);
-      LaunchTimer t(s, ctx->profiling, true);
-      launch_online_f32(s.stream, static_cast<int>(W), sc.wbeg.as<int64_t>(), s.det_dev.as<DetEntry>(),
-                        reinterpret_cast<const uint32_t*>(s.det_dev.as<char>() + ebytes), s.uf.as<float>(),
-                        s.itf.as<float>(), s.uf.bytes(), s.itf.bytes(), k, ctx->P.online_learning_rate,
-                        sc.uticket.as<int32_t>(), sc.dummy.as<int32_t>(), sc.err.as<int32_t>(),
-                        test_knob("online_single") == "0" ? 0 : static_cast<int>(nsingle), t.start(), t.stop());
+      queue_f32_sweep(nullptr);
     } else if (det_online) {
+      const size_t ub = static_cast<size_t>(std::max<int64_t>(ctx->U.rows(), 1)) * 4;
+      sc.uticket.alloc(ub);
+      MF_HIP(hipMemsetAsync(sc.uticket.get(), 0, ub, s.stream));
+      sc.err.alloc(4);
+      MF_HIP(hipMemsetAsync(sc.err.get(), 0, 4, s.stream));
       // the wave table goes through the host once (W descriptors): det_slot_table pairs each
       // single-item wave with its helper and gives the longest chains a CU each
       uint32_t *eu = nullptr, *ei = nullptr, *eq = nullptr;
@@ -2147,17 +2204,24 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
                         ctx->P.online_learning_rate, sc.uticket.as<int32_t>(), sc.err.as<int32_t>(), t.start(),
                         t.stop());
     } else {
+      const size_t ub = static_cast<size_t>(std::max<int64_t>(ctx->U.rows(), 1)) * 4;
+      sc.uticket.alloc(ub);
+      MF_HIP(hipMemsetAsync(sc.uticket.get(), 0, ub, s.stream));
+      sc.err.alloc(4);
+      MF_HIP(hipMemsetAsync(sc.err.get(), 0, 4, s.stream));
       LaunchTimer t(s, ctx->profiling);
       launch_online_sweep(s.stream, static_cast<int>(W), sc.wbeg.as<int64_t>(), s.det_dev.as<DetEntry>(),
                           reinterpret_cast<const uint32_t*>(s.det_dev.as<char>() + ebytes), s.uf.get(), s.itf.get(), k,
                           ctx->P.online_learning_rate, ctx->f64, sc.uticket.as<int32_t>(), sc.err.as<int32_t>());
     }
     MF_HIP(hipGetLastError());
-    int32_t err = 0, touched[2] = {0, 0};
-    MF_HIP(hipMemcpyAsync(&err, sc.err.get(), 4, hipMemcpyDeviceToHost, s.stream));
-    MF_HIP(hipMemcpyAsync(touched, sc.touched.get(), 8, hipMemcpyDeviceToHost, s.stream));
+    if (!f32_online) {
+      MF_HIP(hipMemcpyAsync(pin4 + 1, sc.err.get(), 4, hipMemcpyDeviceToHost, s.stream));
+      MF_HIP(hipMemcpyAsync(pin4 + 2, sc.touched.get(), 8, hipMemcpyDeviceToHost, s.stream));
+    }
     MF_HIP(hipStreamSynchronize(s.stream));
     clk.lap("online: sweep (device)");
+    const int32_t err = pin4[1], touched[2] = {pin4[2], pin4[3]};
     if (err) {
       // waves that gave up skipped the rest of their updates and the batch's new ids are already
       // in the index: the model is partly updated, so the context refuses further work (as the
