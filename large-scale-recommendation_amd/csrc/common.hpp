@@ -122,9 +122,9 @@ struct OnlineSweepScratch {
   DevBuf icnt, iwave, irows;               // per item row: update counts (+ sorted), own wave (-1: none), rows by count
   DevBuf soa, multi, waves;                // the f64 sweep's entry arrays, multi-item flags, wave table
   DevBuf miss;                             // the device id lookup's miss count
-  // the plan's independent sorts run side by side: the tickets' user sort on s2, the touched-item
-  // sort on s3 (each with its own hipCUB scratch and keys), joined back into the caller's stream
-  DevBuf tmp2, tmp3, iota2, ikey, iflag;
+  // the plan's independent parts run side by side: the tickets' user sort on s2, the touched-item
+  // flags on s3 (each with its own scratch), joined back into the caller's stream
+  DevBuf tmp2, tmp3, iota2, iflag;
   hipStream_t s2 = nullptr, s3 = nullptr;
   hipEvent_t ev_in = nullptr, ev2 = nullptr, ev3 = nullptr;
   OnlineSweepScratch() = default;

@@ -13,9 +13,8 @@
 //             go to H + row mod (W - H).  The hottest items' chains bound the launch, so they should
 //             not share their wave with other items' updates.
 //   wbeg[w] : first position of wave w (lower bound in the sorted wave keys), wbeg[W] = n
-//   touched : distinct user rows (run heads of the user sort) and item rows (run heads of a
-//             key-only item sort) of the batch (UpdateSeparatedHashMap.updates,
-//             OfflineSpark.scala:33-67)
+//   touched : distinct user rows (run heads of the user sort) and item rows (a flag per item row)
+//             of the batch (UpdateSeparatedHashMap.updates, OfflineSpark.scala:33-67)
 // HBM-bound integer work (4-byte keys, 4-byte payloads).  Bitwise the host plan: the factors of
 // the sweep equal the level replay's (tests/test_gpu_online.py).
 
@@ -24,6 +23,7 @@
 #include <hipcub/device/device_radix_sort.hpp>
 #include <hipcub/device/device_reduce.hpp>
 #include <hipcub/device/device_scan.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
 #include <cmath>
@@ -129,11 +129,26 @@ __global__ void k_wave_begin(const uint32_t* __restrict__ wsorted, int64_t n, ui
   }
 }
 
+// flag[row] = 1 for every row of the batch (rows >= rows: lookup misses, skipped)
+__global__ void k_row_flags(const uint32_t* __restrict__ rowv, int64_t n, uint32_t rows, int32_t* __restrict__ flag) {
+  for (int64_t x = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; x < n;
+       x += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const uint32_t r = rowv[x];
+    if (r < rows) flag[r] = 1;
+  }
+}
+
 __global__ void k_head_flags(const uint32_t* __restrict__ sorted, int64_t n, int32_t* __restrict__ flag) {
   for (int64_t p = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; p < n;
        p += static_cast<int64_t>(gridDim.x) * blockDim.x)
     flag[p] = (p == 0 || sorted[p] != sorted[p - 1]) ? 1 : 0;
 }
+
+// The plan's stable sorts: rocprim's radix sort with the merge-sort path off.  Its default config
+// sorts up to 2^20 keys by block sort + 8 merge passes (17 launches of 5-10 us for a 1M batch,
+// gpurun_out/r6o); onesweep takes a histogram, a scan and one pass per 8 key bits.  Both are stable:
+// the same output.
+using SortCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, rocprim::default_config, 0>;
 
 int bits_for(uint64_t v) {  // radix bits that hold every key < v
   int b = 1;
@@ -302,22 +317,21 @@ uint32_t online_sweep_plan(hipStream_t st, OnlineSweepScratch& sc, const uint32_
                      H > 0 && item_rows > 0 ? sc.iwave.as<int32_t>() : nullptr, item_rows, sc.wkey.as<uint32_t>(),
                      sc.iota.as<int32_t>());
   const int ub = bits_for(user_rows), wb = bits_for(W);
-  // tickets on s2 (user sort, run starts, ranks) and the touched items on s3 (a key-only item sort)
+  // tickets on s2 (user sort, run starts, ranks) and the touched items on s3 (item-row flags)
   // run beside the wave keys and the wave sort on st; both only read the uploaded batch
   sc.side_streams();
   sc.iota2.alloc(n * 4);
-  sc.ikey.alloc(n * 4);
-  sc.iflag.alloc(n * 4);
+  sc.iflag.alloc(static_cast<size_t>(std::max<uint32_t>(item_rows, 1)) * 4);
   MF_HIP(hipEventRecord(sc.ev_in, st));
   MF_HIP(hipStreamWaitEvent(sc.s2, sc.ev_in, 0));
   MF_HIP(hipStreamWaitEvent(sc.s3, sc.ev_in, 0));
   size_t tb2 = 0, tb3 = 0;
   hipLaunchKernelGGL(k_iota, dim3(grid_for(n)), dim3(kThreads), 0, sc.s2, n, sc.iota2.as<int32_t>());
-  MF_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb2, eu, sc.ukey.as<uint32_t>(), sc.iota2.as<int32_t>(),
-                                            sc.ux.as<int32_t>(), N, 0, ub, sc.s2));
+  MF_HIP(rocprim::radix_sort_pairs<SortCfg>(nullptr, tb2, eu, sc.ukey.as<uint32_t>(), sc.iota2.as<int32_t>(),
+                                             sc.ux.as<int32_t>(), N, 0, ub, sc.s2));
   sc.tmp2.alloc(std::max<size_t>(tb2, 256));
-  MF_HIP(hipcub::DeviceRadixSort::SortPairs(sc.tmp2.get(), tb2, eu, sc.ukey.as<uint32_t>(), sc.iota2.as<int32_t>(),
-                                            sc.ux.as<int32_t>(), N, 0, ub, sc.s2));
+  MF_HIP(rocprim::radix_sort_pairs<SortCfg>(sc.tmp2.get(), tb2, eu, sc.ukey.as<uint32_t>(), sc.iota2.as<int32_t>(),
+                                             sc.ux.as<int32_t>(), N, 0, ub, sc.s2));
   hipLaunchKernelGGL(k_run_heads, dim3(grid_for(n)), dim3(kThreads), 0, sc.s2, sc.ukey.as<uint32_t>(), n,
                      sc.head.as<int32_t>());
   MF_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb2, sc.head.as<int32_t>(), sc.start.as<int32_t>(), hipcub::Max(),
@@ -334,23 +348,20 @@ uint32_t online_sweep_plan(hipStream_t st, OnlineSweepScratch& sc, const uint32_
   sc.tmp2.alloc(std::max<size_t>(tb2, 256));
   MF_HIP(hipcub::DeviceReduce::Sum(sc.tmp2.get(), tb2, sc.head.as<int32_t>(), touched, N, sc.s2));
   MF_HIP(hipEventRecord(sc.ev2, sc.s2));
-  // touched items (s3)
-  MF_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb3, ei, sc.ikey.as<uint32_t>(), N, 0, bits_for(item_rows), sc.s3));
+  // touched items (s3): a flag per item row, summed
+  const int nir = static_cast<int>(std::max<uint32_t>(item_rows, 1));
+  MF_HIP(hipMemsetAsync(sc.iflag.get(), 0, static_cast<size_t>(nir) * 4, sc.s3));
+  hipLaunchKernelGGL(k_row_flags, dim3(grid_for(n)), dim3(kThreads), 0, sc.s3, ei, n, item_rows, sc.iflag.as<int32_t>());
+  MF_HIP(hipcub::DeviceReduce::Sum(nullptr, tb3, sc.iflag.as<int32_t>(), touched + 1, nir, sc.s3));
   sc.tmp3.alloc(std::max<size_t>(tb3, 256));
-  MF_HIP(hipcub::DeviceRadixSort::SortKeys(sc.tmp3.get(), tb3, ei, sc.ikey.as<uint32_t>(), N, 0, bits_for(item_rows),
-                                           sc.s3));
-  hipLaunchKernelGGL(k_head_flags, dim3(grid_for(n)), dim3(kThreads), 0, sc.s3, sc.ikey.as<uint32_t>(), n,
-                     sc.iflag.as<int32_t>());
-  MF_HIP(hipcub::DeviceReduce::Sum(nullptr, tb3, sc.iflag.as<int32_t>(), touched + 1, N, sc.s3));
-  sc.tmp3.alloc(std::max<size_t>(tb3, 256));
-  MF_HIP(hipcub::DeviceReduce::Sum(sc.tmp3.get(), tb3, sc.iflag.as<int32_t>(), touched + 1, N, sc.s3));
+  MF_HIP(hipcub::DeviceReduce::Sum(sc.tmp3.get(), tb3, sc.iflag.as<int32_t>(), touched + 1, nir, sc.s3));
   MF_HIP(hipEventRecord(sc.ev3, sc.s3));
   // waves (st): the wave sort, then the gather once the tickets are in
-  MF_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, sc.wkey.as<uint32_t>(), sc.wkey2.as<uint32_t>(),
-                                            sc.iota.as<int32_t>(), sc.wx.as<int32_t>(), N, 0, wb, st));
+  MF_HIP(rocprim::radix_sort_pairs<SortCfg>(nullptr, tb, sc.wkey.as<uint32_t>(), sc.wkey2.as<uint32_t>(),
+                                             sc.iota.as<int32_t>(), sc.wx.as<int32_t>(), N, 0, wb, st));
   sc.tmp.alloc(std::max<size_t>(tb, 256));
-  MF_HIP(hipcub::DeviceRadixSort::SortPairs(sc.tmp.get(), tb, sc.wkey.as<uint32_t>(), sc.wkey2.as<uint32_t>(),
-                                            sc.iota.as<int32_t>(), sc.wx.as<int32_t>(), N, 0, wb, st));
+  MF_HIP(rocprim::radix_sort_pairs<SortCfg>(sc.tmp.get(), tb, sc.wkey.as<uint32_t>(), sc.wkey2.as<uint32_t>(),
+                                             sc.iota.as<int32_t>(), sc.wx.as<int32_t>(), N, 0, wb, st));
   hipLaunchKernelGGL(k_wave_begin, dim3(grid_for(W + 1)), dim3(kThreads), 0, st, sc.wkey2.as<uint32_t>(), n, W,
                      wbeg);
   MF_HIP(hipStreamWaitEvent(st, sc.ev2, 0));
