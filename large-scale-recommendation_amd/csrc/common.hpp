@@ -119,7 +119,7 @@ struct OnlineSweepScratch {
   DevBuf ukey, wkey, wkey2, iota, ux, wx, head, start, ticket, tmp;
   DevBuf in, wbeg, uticket, err, touched;  // the batch as uploaded; wave starts, tickets, error flag, counts
   DevBuf dummy;                            // k_online_f32: a scratch ticket line per wave
-  DevBuf icnt, iwave, irows;               // per item row: update counts (+ sorted), own wave (-1: none), rows by count
+  DevBuf icnt, iwave;                      // per item row: sampled update counts, own wave (-1: none)
   DevBuf soa, multi, waves;                // the f64 sweep's entry arrays, multi-item flags, wave table
   DevBuf miss;                             // the device id lookup's miss count
   // the plan's independent parts run side by side: the tickets' user sort on s2, the touched-item

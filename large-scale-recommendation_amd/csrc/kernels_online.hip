@@ -54,18 +54,33 @@ __global__ void k_item_count(const uint32_t* __restrict__ ei, int64_t n, int S, 
   }
 }
 
-__global__ void k_heavy_flags(const uint32_t* __restrict__ cnt, uint32_t rows, uint32_t Ts, int32_t* __restrict__ flag) {
-  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < rows;
-       i += static_cast<int64_t>(gridDim.x) * blockDim.x)
-    flag[i] = cnt[i] >= Ts ? 1 : 0;
-}
-
-// iwave[item] = its rank among the heavy items in row order (< H), else -1
-__global__ void k_heavy_assign(const int32_t* __restrict__ flag, const int32_t* __restrict__ pos, uint32_t rows,
-                               uint32_t H, int32_t* __restrict__ iwave) {
-  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < rows;
-       i += static_cast<int64_t>(gridDim.x) * blockDim.x)
-    iwave[i] = flag[i] && static_cast<uint32_t>(pos[i]) < H ? pos[i] : -1;
+// iwave[item] = its rank among the items with cnt >= Ts in row order when that rank is < H, else
+// -1: one block, each thread a contiguous run of rows, a block-wide exclusive scan of the runs'
+// counts in LDS (one launch instead of flags + a device scan + an assign pass: ~4 launches of
+// 8-9 us each on the critical path of a batch's plan)
+constexpr int kHeavyThreads = 1024;
+__global__ __launch_bounds__(kHeavyThreads) void k_heavy_assign(const uint32_t* __restrict__ cnt, uint32_t rows,
+                                                                 uint32_t Ts, uint32_t H, int32_t* __restrict__ iwave) {
+  __shared__ uint32_t part[kHeavyThreads];
+  const uint32_t t = threadIdx.x;
+  const uint32_t per = (rows + kHeavyThreads - 1) / kHeavyThreads;
+  const uint32_t lo = min(rows, t * per), hi = min(rows, lo + per);
+  uint32_t c = 0;
+  for (uint32_t i = lo; i < hi; ++i) c += cnt[i] >= Ts;
+  part[t] = c;
+  __syncthreads();
+  for (uint32_t d = 1; d < kHeavyThreads; d <<= 1) {  // inclusive Hillis-Steele scan
+    const uint32_t v = t >= d ? part[t - d] : 0u;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint32_t pos = part[t] - c;  // exclusive
+  for (uint32_t i = lo; i < hi; ++i) {
+    const bool heavy = cnt[i] >= Ts;
+    iwave[i] = heavy && pos < H ? static_cast<int32_t>(pos) : -1;
+    pos += heavy;
+  }
 }
 
 __global__ void k_iota(int64_t n, int32_t* __restrict__ iota) {
@@ -298,20 +313,13 @@ uint32_t online_sweep_plan(hipStream_t st, OnlineSweepScratch& sc, const uint32_
     const size_t ib = static_cast<size_t>(item_rows) * 4;
     sc.icnt.alloc(ib);
     sc.iwave.alloc(ib);
-    sc.irows.alloc(2 * ib);  // flags, then their exclusive prefix
     uint32_t* cnt = sc.icnt.as<uint32_t>();
-    int32_t* flag = sc.irows.as<int32_t>();
     MF_HIP(hipMemsetAsync(cnt, 0, ib, st));
     hipLaunchKernelGGL(k_item_count, dim3(grid_for((n + kSample - 1) / kSample)), dim3(kThreads), 0, st, ei, n, kSample,
                        item_rows, cnt);
     const uint32_t Ts = std::max<uint32_t>(1, (T + kSample - 1) / kSample);
-    hipLaunchKernelGGL(k_heavy_flags, dim3(grid_for(item_rows)), dim3(kThreads), 0, st, cnt, item_rows, Ts, flag);
-    const int ni = static_cast<int>(item_rows);
-    MF_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, flag, flag + item_rows, ni, st));
-    sc.tmp.alloc(std::max<size_t>(tb, 256));
-    MF_HIP(hipcub::DeviceScan::ExclusiveSum(sc.tmp.get(), tb, flag, flag + item_rows, ni, st));
-    hipLaunchKernelGGL(k_heavy_assign, dim3(grid_for(item_rows)), dim3(kThreads), 0, st, flag, flag + item_rows,
-                       item_rows, H, sc.iwave.as<int32_t>());
+    hipLaunchKernelGGL(k_heavy_assign, dim3(1), dim3(kHeavyThreads), 0, st, cnt, item_rows, Ts, H,
+                       sc.iwave.as<int32_t>());
   }
   hipLaunchKernelGGL(k_keys, dim3(grid_for(n)), dim3(kThreads), 0, st, eu, ei, n, W, H,
                      H > 0 && item_rows > 0 ? sc.iwave.as<int32_t>() : nullptr, item_rows, sc.wkey.as<uint32_t>(),

@@ -97,6 +97,7 @@ struct Shard {
   OnlineSweepScratch online_sc;  // online micro-batches (k_online_sweep)
   DevIndex didx[2];              // device mirrors of the user [0] / item [1] IdIndex (online id lookup)
   PinnedBuf small_pin;           // online batch: {lookup misses, sweep error, touched users, items}, read back async
+  PinnedBuf slots_pin;           // online f64 batch: the wave table read back for det_slot_table
   DevBuf blk_u, blk_i, blk_ru, blk_ri;  // mf_block_update: the block's factor rows and lambda / omega
   // fast mode
   DevBuf fast_recs, fast_cells, fast_blks;
@@ -2003,6 +2004,22 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
     MF_HIP(hipMemcpyAsync(pin4 + 1, sc.err.get(), 4, hipMemcpyDeviceToHost, s.stream));
     MF_HIP(hipMemcpyAsync(pin4 + 2, sc.touched.get(), 8, hipMemcpyDeviceToHost, s.stream));
   };
+  // the f64 sweep's entry arrays and wave table from the plan; the table comes back to the host
+  // (pinned) for det_slot_table, read after the next stream sync
+  uint32_t *det_eu = nullptr, *det_ei = nullptr, *det_eq = nullptr;
+  double* det_er = nullptr;
+  bool det_entries = false;
+  auto queue_det_entries = [&]() {
+    OnlineSweepScratch& sc = s.online_sc;
+    sc.waves.alloc(static_cast<size_t>(det_slot_room(W)) * sizeof(DetWave));
+    online_det_entries(s.stream, sc, s.det_dev.as<DetEntry>(),
+                       reinterpret_cast<const uint32_t*>(s.det_dev.as<char>() + ebytes), sc.wbeg.as<int64_t>(), n,
+                       static_cast<uint32_t>(W), det_eu, det_ei, det_eq, det_er, sc.waves.as<DetWave>());
+    s.slots_pin.alloc(static_cast<size_t>(det_slot_room(W)) * sizeof(DetWave));
+    MF_HIP(hipMemcpyAsync(s.slots_pin.as<DetWave>(), sc.waves.get(), static_cast<size_t>(W) * sizeof(DetWave),
+                          hipMemcpyDeviceToHost, s.stream));
+    det_entries = true;
+  };
   if (dev_lookup) {
     DeviceGuard g(s.device);
     OnlineSweepScratch& sc = s.online_sc;
@@ -2033,6 +2050,8 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
       ensure_rows(ctx, s, kSideU, std::max<int64_t>(ctx->U.rows(), 1));
       ensure_rows(ctx, s, MF_SIDE_ITEM, std::max<int64_t>(ctx->I.rows(), 1));
       queue_f32_sweep(sc.miss.as<int32_t>());
+    } else if (det_online) {
+      queue_det_entries();  // (void with the plan when there are misses)
     }
     clk.lap("online: lookup + plan queued");
     MF_HIP(hipStreamSynchronize(s.stream));
@@ -2052,7 +2071,7 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
       return;
     }
     if (m > 0) {  // the rows as found (kMiss where absent) back into the pinned buffer
-      planned = false;
+      planned = det_entries = false;
       MF_HIP(hipMemcpyAsync(ur, sc.in.get(), static_cast<size_t>(n) * 8, hipMemcpyDeviceToHost, s.stream));
       MF_HIP(hipStreamSynchronize(s.stream));
     }
@@ -2141,12 +2160,10 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
         order.insert(order.end(), c.begin(), c.end());
       }
   }
-  std::vector<DetWave> det_slots;  // the f64 sweep's slot table (alive until the sync below)
   if (cap > 0) {
     // one persistent launch (k_online_sweep): items spread over the waves, each wave's updates in
     // sequence order, and per update the number of earlier updates of its user (its ticket value)
     DeviceGuard g(s.device);
-    const uint32_t W32 = static_cast<uint32_t>(W);
     // the batch in sequence order goes up as is (16 bytes an update); the per-wave lists and the
     // tickets are built on the device (online_sweep_plan, kernels_online.hip)
     OnlineSweepScratch& sc = s.online_sc;
@@ -2183,24 +2200,20 @@ void online_update(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double
       sc.err.alloc(4);
       MF_HIP(hipMemsetAsync(sc.err.get(), 0, 4, s.stream));
       // the wave table goes through the host once (W descriptors): det_slot_table pairs each
-      // single-item wave with its helper and gives the longest chains a CU each
-      uint32_t *eu = nullptr, *ei = nullptr, *eq = nullptr;
-      double* er = nullptr;
-      sc.waves.alloc(static_cast<size_t>(det_slot_room(W)) * sizeof(DetWave));
-      online_det_entries(s.stream, sc, s.det_dev.as<DetEntry>(),
-                         reinterpret_cast<const uint32_t*>(s.det_dev.as<char>() + ebytes), sc.wbeg.as<int64_t>(), n,
-                         W32, eu, ei, eq, er, sc.waves.as<DetWave>());
-      det_slots.resize(static_cast<size_t>(det_slot_room(W)));
-      MF_HIP(hipMemcpyAsync(det_slots.data(), sc.waves.get(), static_cast<size_t>(W) * sizeof(DetWave),
-                            hipMemcpyDeviceToHost, s.stream));
-      MF_HIP(hipStreamSynchronize(s.stream));
+      // single-item wave with its helper and gives the longest chains a CU each (queued behind the
+      // device lookup on that path, so that one sync brings back the miss count and the table)
+      if (!det_entries) {
+        queue_det_entries();
+        MF_HIP(hipStreamSynchronize(s.stream));
+      }
+      DetWave* slots = s.slots_pin.as<DetWave>();
       const int64_t nslots =
-          det_slot_table(det_slots.data(), W, cap / 2, test_knob("det_alone") != "0", device_cu_count(s.device));
-      MF_HIP(hipMemcpyAsync(sc.waves.get(), det_slots.data(), static_cast<size_t>(nslots) * sizeof(DetWave),
+          det_slot_table(slots, W, cap / 2, test_knob("det_alone") != "0", device_cu_count(s.device));
+      MF_HIP(hipMemcpyAsync(sc.waves.get(), slots, static_cast<size_t>(nslots) * sizeof(DetWave),
                             hipMemcpyHostToDevice, s.stream));
       LaunchTimer t(s, ctx->profiling, true);
-      launch_online_det(s.stream, det_slots.empty() ? nullptr : sc.waves.as<DetWave>(), static_cast<int>(nslots), eu, ei,
-                        eq, er, s.uf.as<double>(), s.itf.as<double>(), s.uf.bytes(), s.itf.bytes(), k,
+      launch_online_det(s.stream, sc.waves.as<DetWave>(), static_cast<int>(nslots), det_eu, det_ei, det_eq, det_er,
+                        s.uf.as<double>(), s.itf.as<double>(), s.uf.bytes(), s.itf.bytes(), k,
                         ctx->P.online_learning_rate, sc.uticket.as<int32_t>(), sc.err.as<int32_t>(), t.start(),
                         t.stop());
     } else {
