@@ -412,8 +412,13 @@ __device__ __forceinline__ void link_get_row(MFHIP_LDS(double) * at, double (&v)
 // to the ticket wait's own bound (poll_until: ~2^20 polls, 1-2 s).  So this bound is a clock, and
 // longer (~4 s on the 100 MHz s_memrealtime): a helper that times out sets err itself, and the
 // chain must not be the one to fail the launch first (its message would name the wrong wait).
+// The clock is read only once the first check has failed: an s_memrealtime in flight is a
+// scalar-memory operation, and those return out of order, so every LDS wait behind it waits with
+// lgkmcnt(0) for the clock too -- read at every call, it cost the helper's per-entry hand-over
+// ~45 ns (tools/det_chain_bench.py: 416 vs 370 ns per chained update, gpurun_out/r6y).
 template <typename F>
 __device__ __forceinline__ void link_wait(F v, int32_t want, int32_t* err, int lane) {
+  if (__builtin_amdgcn_readfirstlane(v()) >= want) return;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   while (__builtin_amdgcn_readfirstlane(v()) < want) {
     __builtin_amdgcn_s_sleep(1);
