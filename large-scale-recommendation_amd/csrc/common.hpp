@@ -144,6 +144,13 @@ struct OnlineSweepScratch {
   }
 };
 
+// Device scratch of det_device_build (kernels_online.hip), sized once for a shard's largest superstep.
+struct DetBuildScratch {
+  DevBuf ent, wkey, wkey2, ukey, ukey2, iota, wx, ux, head, start, ticket, tmp, tmp2, blocks;
+  int64_t n_max = 0;
+  size_t tmp_bytes = 0, tmp2_bytes = 0;
+};
+
 // Pinned host staging buffer.
 class PinnedBuf {
  public:

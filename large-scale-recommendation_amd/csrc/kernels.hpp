@@ -63,6 +63,25 @@ void launch_id_scatter(hipStream_t st, void* slots, const uint32_t* pos, const v
 void online_det_entries(hipStream_t st, OnlineSweepScratch& sc, const DetEntry* ent, const uint32_t* useq,
                         const int64_t* wbeg, int64_t n, uint32_t W, uint32_t*& eu, uint32_t*& ei, uint32_t*& eq,
                         double*& er, struct DetWave* waves);
+// The deterministic sweep's superstep input built on the device (MFHIP_TEST det_build=host: on the
+// host, plan.cpp build_det_step -- the same arrays, bit for bit).  One block of the superstep:
+struct DetBuildBlock {
+  int64_t e0;     // its first entry in the superstep's arrays
+  int64_t st;     // its first rating in the device copy of RatingBlocks::det_aos
+  int64_t iwoff;  // its item -> wave map in the concatenated maps
+  uint32_t i0;    // first global item row of its item block
+  uint32_t w0;    // its first wave in the superstep's wave order
+};
+static_assert(sizeof(DetBuildBlock) == 32, "DetBuildBlock is two 16-B words");
+struct DetBuildScratch;
+// ord[e0 + j] = the block's j-th rating in shuffle order (position inside the block, from the
+// host's JVM shuffle); out = the entries in wave order (a wave's entries in shuffle order) with
+// useq = the user's count of earlier ratings in shuffle order: exactly build_det_step's SoA.
+// Reserve scratch for up to n_max entries first (det_device_build_reserve; no allocation after).
+void det_device_build_reserve(DetBuildScratch& sc, int64_t n_max, uint32_t wave_bound, uint32_t user_rows);
+void det_device_build(hipStream_t st, DetBuildScratch& sc, const int32_t* ord, int64_t n, const DetBuildBlock* blocks,
+                      int nblk, const DetEntry* aos, const int32_t* item_wave, uint32_t wave_bound,
+                      uint32_t user_rows, uint32_t* ou, uint32_t* oi, uint32_t* oq, double* orr);
 // Per-rating records of the online operators (mf_online_update_out), f64 rows of k at
 // [src[entry] * k]: kOutNext = (user', item') (FlinkOnlineMF.scala:131-135), kOutDelta =
 // (user + deltaItem, deltaItem) with user before the update (PSOfflineOnlineMF.scala:174-176).

@@ -385,3 +385,105 @@ uint32_t online_sweep_plan(hipStream_t st, OnlineSweepScratch& sc, const uint32_
 }
 
 }  // namespace mfhip
+
+// ---------------------------------------------------------------------------------------------
+// The deterministic sweep's superstep input on the device (kernels.hpp det_device_build): the host
+// build of plan.cpp build_det_step as a gather, two stable radix sorts and a scatter.  The host
+// keeps only the JVM shuffle (sequential per block) and uploads the permutation (4 B per rating
+// instead of the 20-B entries), and the ~15 ms of host gather / prefix / scatter per NFLX
+// superstep become ~1 ms of kernels on the copy stream beside the previous superstep's sweep.
+namespace mfhip {
+namespace {
+
+__global__ void k_db_gather(const int32_t* __restrict__ ord, int64_t n, const DetBuildBlock* __restrict__ blocks,
+                            int nblk, const DetEntry* __restrict__ aos, const int32_t* __restrict__ iw,
+                            DetEntry* __restrict__ ent, uint32_t* __restrict__ wkey, uint32_t* __restrict__ ukey,
+                            int32_t* __restrict__ iota) {
+  for (int64_t j = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; j < n;
+       j += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    int x = 0;
+    while (x + 1 < nblk && blocks[x + 1].e0 <= j) ++x;  // a superstep holds c blocks (a handful)
+    const DetBuildBlock b = blocks[x];
+    const DetEntry d = aos[b.st + ord[j]];
+    ent[j] = d;
+    wkey[j] = b.w0 + static_cast<uint32_t>(iw[b.iwoff + (d.i - b.i0)]);
+    ukey[j] = d.u;
+    iota[j] = static_cast<int32_t>(j);
+  }
+}
+
+// entry p of the wave-major order: rating j = wx[p] (a wave's ratings in shuffle order)
+__global__ void k_db_scatter(const int32_t* __restrict__ wx, int64_t n, const DetEntry* __restrict__ ent,
+                             const uint32_t* __restrict__ ticket, uint32_t* __restrict__ ou, uint32_t* __restrict__ oi,
+                             uint32_t* __restrict__ oq, double* __restrict__ orr) {
+  for (int64_t p = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; p < n;
+       p += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int32_t j = wx[p];
+    const DetEntry d = ent[j];
+    ou[p] = d.u;
+    oi[p] = d.i;
+    oq[p] = ticket[j];
+    orr[p] = d.r;
+  }
+}
+
+}  // namespace
+
+void det_device_build_reserve(DetBuildScratch& sc, int64_t n_max, uint32_t wave_bound, uint32_t user_rows) {
+  MF_REQUIRE(n_max >= 0 && n_max < (int64_t{1} << 31), "det device build: superstep too large");
+  const int64_t n = std::max<int64_t>(n_max, 1);
+  const int N = static_cast<int>(n);
+  sc.ent.alloc(n * sizeof(DetEntry));
+  for (DevBuf* b : {&sc.wkey, &sc.wkey2, &sc.ukey, &sc.ukey2, &sc.iota, &sc.wx, &sc.ux, &sc.head, &sc.start, &sc.ticket})
+    b->alloc(n * 4);
+  size_t a = 0, b2 = 0, c = 0;
+  MF_HIP(rocprim::radix_sort_pairs<SortCfg>(nullptr, a, sc.wkey.as<uint32_t>(), sc.wkey2.as<uint32_t>(),
+                                             sc.iota.as<int32_t>(), sc.wx.as<int32_t>(), N, 0, bits_for(wave_bound)));
+  MF_HIP(rocprim::radix_sort_pairs<SortCfg>(nullptr, b2, sc.ukey.as<uint32_t>(), sc.ukey2.as<uint32_t>(),
+                                             sc.iota.as<int32_t>(), sc.ux.as<int32_t>(), N, 0, bits_for(user_rows)));
+  MF_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, c, sc.head.as<int32_t>(), sc.start.as<int32_t>(), hipcub::Max(), N));
+  sc.tmp_bytes = std::max<size_t>(std::max(a, b2), 256);
+  sc.tmp2_bytes = std::max<size_t>(c, 256);
+  sc.tmp.alloc(sc.tmp_bytes);
+  sc.tmp2.alloc(sc.tmp2_bytes);
+  sc.n_max = n_max;
+}
+
+void det_device_build(hipStream_t st, DetBuildScratch& sc, const int32_t* ord, int64_t n, const DetBuildBlock* blocks,
+                      int nblk, const DetEntry* aos, const int32_t* item_wave, uint32_t wave_bound,
+                      uint32_t user_rows, uint32_t* ou, uint32_t* oi, uint32_t* oq, double* orr) {
+  if (n <= 0) return;
+  MF_REQUIRE(n <= sc.n_max, "det device build: more ratings than the scratch was reserved for");
+  const int N = static_cast<int>(n);
+  hipLaunchKernelGGL(k_db_gather, dim3(grid_for(n)), dim3(kThreads), 0, st, ord, n, blocks, nblk, aos, item_wave,
+                     sc.ent.as<DetEntry>(), sc.wkey.as<uint32_t>(), sc.ukey.as<uint32_t>(), sc.iota.as<int32_t>());
+  size_t tb = 0;
+  // wave-major order, a wave's ratings in shuffle order (stable)
+  MF_HIP(rocprim::radix_sort_pairs<SortCfg>(nullptr, tb, sc.wkey.as<uint32_t>(), sc.wkey2.as<uint32_t>(),
+                                             sc.iota.as<int32_t>(), sc.wx.as<int32_t>(), N, 0, bits_for(wave_bound), st));
+  MF_REQUIRE(tb <= sc.tmp_bytes, "det device build: sort scratch");
+  MF_HIP(rocprim::radix_sort_pairs<SortCfg>(sc.tmp.get(), tb, sc.wkey.as<uint32_t>(), sc.wkey2.as<uint32_t>(),
+                                             sc.iota.as<int32_t>(), sc.wx.as<int32_t>(), N, 0, bits_for(wave_bound), st));
+  // useq: the rank of a rating among its user's ratings in shuffle order (users of a superstep's
+  // blocks are disjoint: each block has its own user block)
+  MF_HIP(rocprim::radix_sort_pairs<SortCfg>(nullptr, tb, sc.ukey.as<uint32_t>(), sc.ukey2.as<uint32_t>(),
+                                             sc.iota.as<int32_t>(), sc.ux.as<int32_t>(), N, 0, bits_for(user_rows), st));
+  MF_REQUIRE(tb <= sc.tmp_bytes, "det device build: sort scratch");
+  MF_HIP(rocprim::radix_sort_pairs<SortCfg>(sc.tmp.get(), tb, sc.ukey.as<uint32_t>(), sc.ukey2.as<uint32_t>(),
+                                             sc.iota.as<int32_t>(), sc.ux.as<int32_t>(), N, 0, bits_for(user_rows), st));
+  hipLaunchKernelGGL(k_run_heads, dim3(grid_for(n)), dim3(kThreads), 0, st, sc.ukey2.as<uint32_t>(), n,
+                     sc.head.as<int32_t>());
+  tb = 0;
+  MF_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb, sc.head.as<int32_t>(), sc.start.as<int32_t>(), hipcub::Max(),
+                                           N, st));
+  MF_REQUIRE(tb <= sc.tmp2_bytes, "det device build: scan scratch");
+  MF_HIP(hipcub::DeviceScan::InclusiveScan(sc.tmp2.get(), tb, sc.head.as<int32_t>(), sc.start.as<int32_t>(),
+                                           hipcub::Max(), N, st));
+  hipLaunchKernelGGL(k_tickets, dim3(grid_for(n)), dim3(kThreads), 0, st, sc.ux.as<int32_t>(), sc.start.as<int32_t>(), n,
+                     sc.ticket.as<uint32_t>());
+  hipLaunchKernelGGL(k_db_scatter, dim3(grid_for(n)), dim3(kThreads), 0, st, sc.wx.as<int32_t>(), n,
+                     sc.ent.as<DetEntry>(), sc.ticket.as<uint32_t>(), ou, oi, oq, orr);
+  MF_HIP(hipGetLastError());
+}
+
+}  // namespace mfhip

@@ -122,6 +122,16 @@ struct Shard {
   DetBuf det_buf[kDetSlots];
   DevBuf det_ticket, det_err, det_scratch;
   int64_t det_n_max = 0, det_nw_max = 0;
+  // the superstep's input built on the device (det_device_build; MFHIP_TEST det_build=host: on the
+  // host): the rating blocks' 16-B records, the blocks' item -> wave maps, per superstep index
+  // (s-1) mod n its block table and its wave / slot table (both fixed: a wave's count is the sum
+  // of its items' counts), the uploaded shuffle permutation, and the build's scratch
+  DevBuf det_aos_dev, det_iw, det_bt, det_ord;
+  DetBuildScratch det_bs;
+  std::vector<std::vector<DetWave>> det_sm_slots;
+  std::vector<int64_t> det_sm_n;
+  std::vector<int32_t> det_sm_nblk;
+  uint32_t det_wave_bound = 1;
   // evaluation scratch
   DevBuf ev_u, ev_i, ev_r, ev_mult, ev_out, ev_part;
   // profiling
@@ -158,6 +168,7 @@ struct mf_ctx {
   bool fast_sys = false;          // pair cells as one systolic launch per superstep (k_sweep_pair_sys)
   bool det_sweep = false;         // deterministic mode: one persistent k_det_sweep launch per superstep
   bool det_split = false;         // ... with single-item chains split over two waves (k_det_sweep_split)
+  bool det_dev_build = false;     // ... its input built on the device from the host's shuffle (det_device_build)
   bool det_alone = true;          // ... the longest chains on CUs of their own (det_slot_table)
   int64_t det_split_blocks = 0;   // resident blocks of k_det_sweep_split (per device share)
   int64_t det_cu_period = 256;    // CUs of the device: blocks b and b + period share a CU
@@ -1047,6 +1058,34 @@ void det_build(mf_ctx* ctx, int64_t superstep, int slot) {
     }
   } done{t_build};
   std::vector<int64_t> blocks, seeds;
+  if (ctx->det_dev_build) {
+    // the device builds the entries (det_run): here only each block's JVM shuffle, written as the
+    // uploaded permutation, and the superstep index's fixed slot table
+    const int64_t sm = (superstep - 1) % ctx->nb;
+    for (auto& s : ctx->shards) {
+      DetBuf& db = s.det_buf[slot];
+      det_blocks(ctx, s, superstep, blocks, seeds);
+      db.n = s.det_sm_n[sm];
+      db.nw = static_cast<int64_t>(s.det_sm_slots[sm].size());
+      if (db.n == 0) continue;
+      const DetOffsets o = det_offsets(s.det_n_max, s.det_nw_max);
+      char* base = db.pin.as<char>();
+      std::memcpy(base + o.waves, s.det_sm_slots[sm].data(), static_cast<size_t>(db.nw) * sizeof(DetWave));
+      int32_t* ord = reinterpret_cast<int32_t*>(base + o.u);  // (the host path's u region)
+      std::vector<int64_t> e0(blocks.size() + 1, 0);
+      for (size_t x = 0; x < blocks.size(); ++x) e0[x + 1] = e0[x] + ctx->rb.size(blocks[x]);
+      std::vector<uint64_t> rseeds(blocks.size());
+      if (!ctx->P.has_seed) {
+        std::random_device rd;
+        for (auto& v : rseeds) v = (static_cast<uint64_t>(rd()) << 32) ^ rd();
+      }
+      parallel_tasks(static_cast<int64_t>(blocks.size()), [&](int64_t x) {
+        JavaRandom rng(ctx->P.has_seed ? seeds[x] : static_cast<int64_t>(rseeds[x]));
+        scala_shuffle(rng, ord + e0[x], e0[x + 1] - e0[x]);  // DSGDforMF.scala:392-393
+      });
+    }
+    return;
+  }
   for (auto& s : ctx->shards) {
     DetBuf& db = s.det_buf[slot];
     det_blocks(ctx, s, superstep, blocks, seeds);
@@ -1128,16 +1167,32 @@ void det_run(mf_ctx* ctx, int64_t count) {
       const DetOffsets o = det_offsets(sh.det_n_max, sh.det_nw_max);
       const char* hp = db.pin.as<char>();
       char* dp = db.dev.as<char>();
-      const std::pair<size_t, size_t> regions[] = {{o.waves, static_cast<size_t>(db.nw) * sizeof(DetWave)},
-                                                   {o.u, static_cast<size_t>(db.n) * 4},
-                                                   {o.i, static_cast<size_t>(db.n) * 4},
-                                                   {o.qf, static_cast<size_t>(db.n) * 4},
-                                                   {o.r, static_cast<size_t>(db.n) * 8}};
       // staging copy on the copy stream, after the sweep that last read this buffer (s-3), so it
       // overlaps the sweeps still running on the compute stream
       MF_HIP(hipStreamWaitEvent(sh.copy_stream, db.swept, 0));
-      for (const auto& rg : regions)
-        MF_HIP(hipMemcpyAsync(dp + rg.first, hp + rg.first, rg.second, hipMemcpyHostToDevice, sh.copy_stream));
+      if (ctx->det_dev_build) {
+        // the slot table and the shuffle permutation go up; the entries are built on the device
+        // (det_device_build), on the same stream
+        const int64_t sm = (s - 1) % ctx->nb;
+        MF_HIP(hipMemcpyAsync(dp + o.waves, hp + o.waves, static_cast<size_t>(db.nw) * sizeof(DetWave),
+                              hipMemcpyHostToDevice, sh.copy_stream));
+        MF_HIP(hipMemcpyAsync(sh.det_ord.get(), hp + o.u, static_cast<size_t>(db.n) * 4, hipMemcpyHostToDevice,
+                              sh.copy_stream));
+        det_device_build(sh.copy_stream, sh.det_bs, sh.det_ord.as<int32_t>(), db.n,
+                         sh.det_bt.as<DetBuildBlock>() + static_cast<size_t>(sm) * ctx->c, sh.det_sm_nblk[sm],
+                         sh.det_aos_dev.as<DetEntry>(), sh.det_iw.as<int32_t>(), sh.det_wave_bound,
+                         static_cast<uint32_t>(ctx->U.rows()), reinterpret_cast<uint32_t*>(dp + o.u),
+                         reinterpret_cast<uint32_t*>(dp + o.i), reinterpret_cast<uint32_t*>(dp + o.qf),
+                         reinterpret_cast<double*>(dp + o.r));
+      } else {
+        const std::pair<size_t, size_t> regions[] = {{o.waves, static_cast<size_t>(db.nw) * sizeof(DetWave)},
+                                                     {o.u, static_cast<size_t>(db.n) * 4},
+                                                     {o.i, static_cast<size_t>(db.n) * 4},
+                                                     {o.qf, static_cast<size_t>(db.n) * 4},
+                                                     {o.r, static_cast<size_t>(db.n) * 8}};
+        for (const auto& rg : regions)
+          MF_HIP(hipMemcpyAsync(dp + rg.first, hp + rg.first, rg.second, hipMemcpyHostToDevice, sh.copy_stream));
+      }
       MF_HIP(hipEventRecord(db.copied, sh.copy_stream));
       db.pending = true;
       MF_HIP(hipStreamWaitEvent(sh.stream, db.copied, 0));
@@ -1252,6 +1307,80 @@ struct PhaseClock {
   }
 };
 
+// The device build of the det sweep's input (kernels.hpp det_device_build): per shard, the rating
+// blocks' records and item -> wave maps on the device, and per superstep index its block table and
+// wave / slot table.  A wave's entries are its items' ratings of the block, so its count -- and
+// with it the wave table and the slot table -- is the same every time the block comes round; only
+// the order inside the waves (the shuffle) changes.
+void prepare_det_device_build(mf_ctx* ctx) {
+  const int32_t n = ctx->nb;
+  const DetEntry* aos = ctx->rb.det_aos.data();
+  const int64_t total = static_cast<int64_t>(ctx->rb.det_aos.size());
+  for (auto& s : ctx->shards) {
+    DeviceGuard g(s.device);
+    const DetSweepLayout& L = s.det_layout;
+    const int64_t nb2 = static_cast<int64_t>(n) * n;
+    // per rating block of this shard: its wave counts and its item -> wave map's offset
+    std::vector<std::vector<int64_t>> wcnt(nb2);
+    std::vector<int64_t> iwoff(nb2, -1);
+    std::vector<int32_t> iw;
+    for (int64_t b = 0; b < nb2; ++b)
+      if (L.block_waves[b] > 0 && !L.item_wave[b].empty()) {
+        iwoff[b] = static_cast<int64_t>(iw.size());
+        iw.insert(iw.end(), L.item_wave[b].begin(), L.item_wave[b].end());
+      }
+    parallel_tasks(nb2, [&](int64_t b) {
+      if (L.block_waves[b] <= 0 || ctx->rb.size(b) == 0) return;
+      const int64_t i0 = ctx->I.block_start[b % n];
+      wcnt[b].assign(L.block_waves[b], 0);
+      for (int64_t e = ctx->rb.start[b]; e < ctx->rb.start[b + 1]; ++e) wcnt[b][L.item_wave[b][aos[e].i - i0]]++;
+    });
+    s.det_sm_slots.assign(n, {});
+    s.det_sm_n.assign(n, 0);
+    s.det_sm_nblk.assign(n, 0);
+    std::vector<DetBuildBlock> bt(static_cast<size_t>(n) * std::max(ctx->c, 1));
+    std::vector<int64_t> blocks, seeds;
+    for (int32_t sm = 0; sm < n; ++sm) {
+      det_blocks(ctx, s, sm + 1, blocks, seeds);  // the blocks of superstep s depend on (s-1) mod n
+      std::vector<DetWave> waves;
+      int64_t e0 = 0;
+      for (size_t x = 0; x < blocks.size(); ++x) {
+        const int64_t b = blocks[x];
+        MF_REQUIRE(iwoff[b] >= 0 && static_cast<int64_t>(wcnt[b].size()) == L.block_waves[b],
+                   "det device build: a block without its wave layout");
+        bt[static_cast<size_t>(sm) * ctx->c + x] =
+            DetBuildBlock{e0, ctx->rb.start[b], iwoff[b], static_cast<uint32_t>(ctx->I.block_start[b % n]),
+                          static_cast<uint32_t>(waves.size())};
+        int64_t at = e0;
+        for (int32_t w = 0; w < L.block_waves[b]; ++w) {
+          waves.push_back(DetWave{at, static_cast<int32_t>(wcnt[b][w]), L.wave_single[b][w] ? kDetWaveSingleItem : 0});
+          at += wcnt[b][w];
+        }
+        e0 = at;
+      }
+      const int64_t nw = static_cast<int64_t>(waves.size());
+      waves.resize(static_cast<size_t>(det_slot_room(nw)));
+      const int64_t nslots =
+          ctx->det_split ? det_slot_table(waves.data(), nw, ctx->det_split_blocks, ctx->det_alone, ctx->det_cu_period)
+                         : nw;
+      waves.resize(static_cast<size_t>(nslots));
+      s.det_sm_slots[sm] = std::move(waves);
+      s.det_sm_n[sm] = e0;
+      s.det_sm_nblk[sm] = static_cast<int32_t>(blocks.size());
+    }
+    s.det_aos_dev.alloc(static_cast<size_t>(std::max<int64_t>(total, 1)) * sizeof(DetEntry));
+    if (total > 0)
+      MF_HIP(hipMemcpy(s.det_aos_dev.get(), aos, static_cast<size_t>(total) * sizeof(DetEntry), hipMemcpyHostToDevice));
+    s.det_iw.alloc(std::max<size_t>(iw.size(), 1) * 4);
+    if (!iw.empty()) MF_HIP(hipMemcpy(s.det_iw.get(), iw.data(), iw.size() * 4, hipMemcpyHostToDevice));
+    s.det_bt.alloc(bt.size() * sizeof(DetBuildBlock));
+    MF_HIP(hipMemcpy(s.det_bt.get(), bt.data(), bt.size() * sizeof(DetBuildBlock), hipMemcpyHostToDevice));
+    s.det_ord.alloc(static_cast<size_t>(std::max<int64_t>(s.det_n_max, 1)) * 4);
+    s.det_wave_bound = static_cast<uint32_t>(std::max<int64_t>(s.det_nw_max, 1));
+    det_device_build_reserve(s.det_bs, s.det_n_max, s.det_wave_bound, static_cast<uint32_t>(ctx->U.rows()));
+  }
+}
+
 // Deterministic mode: the persistent sweep's item -> wave layout and staging buffers, unless
 // MFHIP_TEST det_kernel=level (one launch per dependency level, det_superstep) or the device
 // cannot hold a superstep's waves.  Waves per superstep and shard: half the device's resident
@@ -1332,6 +1461,10 @@ void prepare_det_sweep(mf_ctx* ctx) {
   ctx->det_split_blocks = cap / 2;
   ctx->det_alone = test_knob("det_alone") != "0";
   ctx->det_cu_period = device_cu_count(ctx->shards[0].device);
+  // MFHIP_TEST det_build=device: the sweep's input built on the device (measured slower, see
+  // profiles/r06_det_device_build_ab.txt: the build's traffic slows the running chain)
+  ctx->det_dev_build = test_knob("det_build") == "device";
+  if (ctx->det_dev_build) prepare_det_device_build(ctx);
 }
 
 void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, int64_t n) {
