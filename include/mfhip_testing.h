@@ -19,18 +19,19 @@ extern "C" {
    mf_debug_fast_schedule: for every input rating, the rating block (ub*n+ib), rotation
    sub-step, item group and position inside its cell of the fast-mode plan with `groups`
    groups per rating block (groups < 0: the systolic sweep's per-block choice for a budget of
-   -groups waves per superstep, as mf_dsgd_prepare makes it with MFHIP_TEST=sys_waves=-groups),
-   MF_BLOCKING_* `blocking` and hazard window `window` (0: 8). */
+   -groups waves per superstep, as mf_dsgd_prepare makes it with MFHIP_TEST=sys_waves=-groups for
+   rank k: the group model's constants depend on the row width, plan.hpp sys_cell_ns /
+   sys_run_pair_ns), MF_BLOCKING_* `blocking` and hazard window `window` (0: 8). */
 int mf_debug_levels(const uint32_t* urow, const uint32_t* irow, const int32_t* order, int64_t n,
                     int32_t* level_out);
 int mf_debug_fast_schedule(const int32_t* users, const int32_t* items, int64_t n, int32_t n_blocks,
-                           int64_t seed, int32_t groups, int32_t blocking, int32_t window, int32_t* block_out,
-                           int32_t* substep_out, int32_t* group_out, int64_t* pos_out);
+                           int64_t seed, int32_t groups, int32_t blocking, int32_t window, int32_t k,
+                           int32_t* block_out, int32_t* substep_out, int32_t* group_out, int64_t* pos_out);
 /* mf_debug_fast_split: mf_debug_fast_schedule with hot-item replicas (the MFHIP_ITEM_SPLIT
    experiment, item_split ratings per chain); replica_out[j] = 0 when rating j updates its item's own row, r >= 1 when it
    updates replica r (merged when the superstep ends). */
 int mf_debug_fast_split(const int32_t* users, const int32_t* items, int64_t n, int32_t n_blocks,
-                        int64_t seed, int32_t groups, int32_t blocking, int32_t window, int32_t item_split,
+                        int64_t seed, int32_t groups, int32_t blocking, int32_t window, int32_t k, int32_t item_split,
                         int32_t* block_out, int32_t* substep_out, int32_t* group_out, int64_t* pos_out,
                         int32_t* replica_out);
 /* mf_debug_ring_schedule: the item-block ring step ring_shift runs after superstep `superstep`

@@ -436,9 +436,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
 // issued, so it arrives while those stores drain (vmcnt(4) waits for the stores only): a cell no
 // longer starts with a record fetch on its critical path (an empty cell reads nothing; past the
 // last cell the last cell's records are read again, unused).  The neighbour's progress is polled
-// after the drain, as late as possible (read before the drain it was too often not yet there: an
-// extra poll round trip, ML20M 5.98 vs 5.60 ms per epoch).
-template <int KPL, int D, bool PRE>
+// after the drain (read before the drain it was too often not yet there: an extra poll round trip,
+// ML20M 5.98 vs 5.60 ms per epoch in round 3); EARLY also reads it once with the drain, and a
+// neighbour already done then needs no poll (kEarlyPoll below).
+template <int KPL, int D, bool PRE, bool EARLY>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_sweep_pair_sys(
     const SysWave* __restrict__ sw, const WaveDesc* __restrict__ sys, int nw, int lbase, const u4v* __restrict__ recs,
     float* __restrict__ U, float* __restrict__ I, uint64_t u_bytes, uint64_t i_bytes, float eta,
@@ -468,9 +469,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   WaveDesc d = my[0];
   ChunkRaw L0;
   if (PRE) first_chunks(d, L0);
+  uint32_t seen = base;  // the neighbour's progress as last read
   for (int t = 0; t < w.G; ++t) {
     const WaveDesc dn = my[t + 1 < w.G ? t + 1 : t];  // scalar load, used after this cell
-    if (t > 0 && w.G > 1) {
+    if (t > 0 && w.G > 1 && static_cast<int32_t>(seen - (base + static_cast<uint32_t>(t))) < 0) {
       const uint32_t want = base + static_cast<uint32_t>(t);
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       for (;;) {
@@ -492,12 +494,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     uint64_t wait_clk = 0;
     if (!PRE && d.steps > 0) first_chunks(d, L0);
     if (d.steps > 0) pair_cell<KPL, D, kSC1>(d, L0, recs, urs, irs, eta, lane, wait_clk);
+    // EARLY: the neighbour's progress read together with this cell's store drain (issued after
+    // the stores, completes with them), so a neighbour already done costs no poll round trip
+    uint32_t early = 0;
+    if (EARLY && t + 1 < w.G) early = __hip_atomic_load(nb_prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (PRE) {
       first_chunks(dn, L0);
       __builtin_amdgcn_s_waitcnt(0x0F74);  // vmcnt(4): the 4 loads above may fly, every older store has landed
     } else {
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): every user-row store of this wave has landed
     }
+    if (EARLY && t + 1 < w.G) seen = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(early)));
     if (lane == 0)
       __hip_atomic_store(my_prog, static_cast<int32_t>(base + static_cast<uint32_t>(t) + 1u), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
@@ -527,17 +534,20 @@ void dispatch(hipStream_t st, const WaveDesc* waves, int nwaves, const PairRec* 
                         0, waves, reinterpret_cast<const u4v*>(recs), U, I, ub, ib, eta, trace);
 }
 
-// Record preload across the cell boundary (PRE): on for k >= 128 (NFLX 22.49-22.67 vs 22.56-22.81 ms
-// per epoch, A/B/A/B), off for k = 64 (ML20M 5.86-5.98 vs 5.59-5.60 ms: its cells are short and its
-// waves tightly coupled).  One instance per k.
+// Record preload across the cell boundary (PRE): on for every k since round 6 (ML20M 4.41-4.42 ->
+// 4.26-4.27 ms per epoch, profiles/r06_ML20M_cell_ab.txt; off at k = 64 until then: 5.86-5.98 vs
+// 5.59-5.60 ms in round 3, before the per-width rings).  EARLY (the neighbour's progress read with
+// the drain): NFLX 20.00 / 19.98 -> 19.91 / 19.82 ms, ML20M 4.22 -> 4.25 / 4.26 ms -- k = 128 only.
 template <int KPL>
-constexpr bool kCellPreload = KPL >= 2;
+constexpr bool kCellPreload = true;
+template <int KPL>
+constexpr bool kEarlyPoll = KPL == 2;
 
 template <int KPL>
 void dispatch_sys(hipStream_t st, const SysWave* sw, const WaveDesc* sys, int nw, int lbase, const PairRec* recs,
                   float* U, float* I, uint64_t ub, uint64_t ib, float eta, int32_t* prog, uint32_t base, int32_t* err,
                   uint64_t* trace, hipEvent_t ev0, hipEvent_t ev1, const int32_t* place) {
-  hipExtLaunchKernelGGL((k_sweep_pair_sys<KPL, pair_ring(KPL), kCellPreload<KPL>>), dim3(static_cast<unsigned>(nw)),
+  hipExtLaunchKernelGGL((k_sweep_pair_sys<KPL, pair_ring(KPL), kCellPreload<KPL>, kEarlyPoll<KPL>>), dim3(static_cast<unsigned>(nw)),
                         dim3(64), 0, st, ev0, ev1, 0, sw, sys, nw, lbase, reinterpret_cast<const u4v*>(recs), U, I, ub,
                         ib, eta, prog, base, err, trace, place);
 }
@@ -547,7 +557,7 @@ int sys_capacity() {
   int dev = 0, cus = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sweep_pair_sys<KPL, pair_ring(KPL), kCellPreload<KPL>>, 64,
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sweep_pair_sys<KPL, pair_ring(KPL), kCellPreload<KPL>, kEarlyPoll<KPL>>, 64,
                                                    0) != hipSuccess)
     return 0;
   return cus * per_cu;

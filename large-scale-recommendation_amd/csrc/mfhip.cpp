@@ -1547,9 +1547,10 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
             std::vector<int64_t> size(nb2, 0);
             for (int64_t b = 0; b < nb2; ++b) size[b] = ctx->rb.size(b);
             gb = choose_block_groups(size, device_block_tops(s.stream, dev_rb, ctx->rb, ctx->I), ctx->nb, ctx->c,
-                                     s.index, simds, sys_cell_ns(k));
+                                     s.index, simds, sys_cell_ns(k), sys_run_pair_ns(k));
           } else {
-            gb = choose_block_groups(ctx->rb, ctx->I, ctx->c, s.index, simds, ctx->item_split, sys_cell_ns(k));
+            gb = choose_block_groups(ctx->rb, ctx->I, ctx->c, s.index, simds, ctx->item_split, sys_cell_ns(k),
+                                     sys_run_pair_ns(k));
           }
           for (int64_t b = 0; b < nb2; ++b)
             if (gb[b] > 0) block_groups[b] = gb[b];
@@ -3021,19 +3022,19 @@ int mf_debug_levels(const uint32_t* urow, const uint32_t* irow, const int32_t* o
 }
 
 int mf_debug_fast_schedule(const int32_t* u, const int32_t* i, int64_t n, int32_t n_blocks, int64_t seed,
-                           int32_t groups, int32_t blocking, int32_t window, int32_t* block_out,
+                           int32_t groups, int32_t blocking, int32_t window, int32_t k, int32_t* block_out,
                            int32_t* substep_out, int32_t* group_out, int64_t* pos_out) {
-  return mf_debug_fast_split(u, i, n, n_blocks, seed, groups, blocking, window, 0, block_out, substep_out, group_out,
+  return mf_debug_fast_split(u, i, n, n_blocks, seed, groups, blocking, window, k, 0, block_out, substep_out, group_out,
                              pos_out, nullptr);
 }
 
 namespace mfhip {
 namespace {
 int debug_fast_plan(const int32_t* u, const int32_t* i, int64_t n, int32_t n_blocks, int64_t seed, int32_t groups,
-                    int32_t blocking, int32_t window, int32_t item_split, int32_t* block_out, int32_t* substep_out, int32_t* group_out, int64_t* pos_out,
+                    int32_t blocking, int32_t window, int32_t k, int32_t item_split, int32_t* block_out, int32_t* substep_out, int32_t* group_out, int64_t* pos_out,
                     int32_t* replica_out) {
   return guarded([&] {
-    MF_REQUIRE(n >= 0 && n_blocks >= 1 && groups != 0 && item_split >= 0, "bad argument");
+    MF_REQUIRE(n >= 0 && n_blocks >= 1 && groups != 0 && item_split >= 0 && k >= 1, "bad argument");
     MF_REQUIRE(n == 0 || (u && i && block_out && substep_out && group_out && pos_out), "null argument");
     SideLayout U, I;
     const Blocking bl = blocking == MF_BLOCKING_BALANCED ? Blocking::kBalanced : Blocking::kJvm;
@@ -3045,7 +3046,8 @@ int debug_fast_plan(const int32_t* u, const int32_t* i, int64_t n, int32_t n_blo
     FastPlan fp;
     std::vector<int64_t> src;
     std::vector<int32_t> block_groups;  // groups < 0: the systolic per-block choice for -groups waves
-    if (groups < 0) block_groups = choose_block_groups(rb, I, n_blocks, 0, -groups, item_split);
+    if (groups < 0)
+      block_groups = choose_block_groups(rb, I, n_blocks, 0, -groups, item_split, sys_cell_ns(k), sys_run_pair_ns(k));
     const uint32_t scratch_base = static_cast<uint32_t>(I.rows() + 1);
     build_fast_plan(fp, rb, U, I, groups > 0 ? groups : 8, 1, 1.0,
                     static_cast<uint64_t>(seed) * 0x9E3779B97F4A7C15ULL + 1, static_cast<uint32_t>(U.rows()), &src,
@@ -3083,9 +3085,10 @@ int debug_fast_plan(const int32_t* u, const int32_t* i, int64_t n, int32_t n_blo
 }  // namespace mfhip
 
 int mf_debug_fast_split(const int32_t* u, const int32_t* i, int64_t n, int32_t n_blocks, int64_t seed,
-                        int32_t groups, int32_t blocking, int32_t window, int32_t item_split, int32_t* block_out,
-                        int32_t* substep_out, int32_t* group_out, int64_t* pos_out, int32_t* replica_out) {
-  return mfhip::debug_fast_plan(u, i, n, n_blocks, seed, groups, blocking, window, item_split, block_out,
+                        int32_t groups, int32_t blocking, int32_t window, int32_t k, int32_t item_split,
+                        int32_t* block_out, int32_t* substep_out, int32_t* group_out, int64_t* pos_out,
+                        int32_t* replica_out) {
+  return mfhip::debug_fast_plan(u, i, n, n_blocks, seed, groups, blocking, window, k, item_split, block_out,
                                 substep_out, group_out, pos_out, replica_out);
 }
 

@@ -1269,7 +1269,7 @@ void build_pair_plan(PairPlan& pp, const FastPlan& fp, int32_t nb, int32_t c, in
 void lpt_assign(const std::vector<int64_t>& load, int32_t G, std::vector<int32_t>& group) { lpt_groups(load, G, group); }
 
 std::vector<int32_t> choose_block_groups(const RatingBlocks& rb, const SideLayout& I, int32_t c, int32_t shard,
-                                         int32_t waves, int32_t split_run, double cell_ns) {
+                                         int32_t waves, int32_t split_run, double cell_ns, double run_ns) {
   const int32_t nb = rb.n_blocks;
   const int64_t nb2 = static_cast<int64_t>(nb) * nb;
   std::vector<int64_t> size(nb2, 0), top(nb2, 0);  // ratings, ratings of the most rated item
@@ -1283,14 +1283,14 @@ std::vector<int32_t> choose_block_groups(const RatingBlocks& rb, const SideLayou
     size[b] = rb.size(b);
     top[b] = split_run > 0 ? std::min(mx, split_run) : mx;
   });
-  return choose_block_groups(size, top, nb, c, shard, waves, cell_ns);
+  return choose_block_groups(size, top, nb, c, shard, waves, cell_ns, run_ns);
 }
 
 std::vector<int32_t> choose_block_groups(const std::vector<int64_t>& size, const std::vector<int64_t>& top, int32_t nb,
-                                         int32_t c, int32_t shard, int32_t waves, double cell_ns) {
+                                         int32_t c, int32_t shard, int32_t waves, double cell_ns, double run_ns) {
   const int64_t nb2 = static_cast<int64_t>(nb) * nb;
   std::vector<int32_t> Gb(nb2, 0);
-  double pair_ns = kSysPairNs, run_ns = kSysRunPairNs;
+  double pair_ns = kSysPairNs;
   if (const char* v = exp_knob("MFHIP_SYS_MODEL"))  // tuning knob: "cell_ns,pair_ns,run_pair_ns"
     std::sscanf(v, "%lf,%lf,%lf", &cell_ns, &pair_ns, &run_ns);
   auto wave_ns = [&](int64_t b, int32_t G) {

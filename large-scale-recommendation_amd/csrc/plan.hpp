@@ -381,15 +381,21 @@ constexpr double kSysCellNs = 6000.0;     // per-cell start, drain, hand-off and
 // With the round-5 rings the cell cost re-swept lower at k <= 128 (profiles/r05_group_model.txt:
 // ML20M 4.65 -> 4.49 ms, NFLX 20.03 -> 19.97 ms at 5 us); k = 256 keeps 6 us (its 5-us schedule moves
 // YAHOO@0.05's RMSE past the 0.5% gate).
-constexpr double sys_cell_ns(int k) { return k <= 128 ? 5000.0 : kSysCellNs; }
+// Round 6, with the record preload at k = 64 (profiles/r06_ML20M_cell_ab.txt): k = 64 re-swept to
+// 3.5 us per cell and 230 ns per run pair (ML20M 4.26 -> 4.13 ms); NFLX stays at 5 us / 186 ns
+// (210 / 230 / 170 / 155 ns: 20.45 / 21.17 / 20.23 / 21.20 ms against 19.87).
+constexpr double sys_cell_ns(int k) { return k <= 64 ? 3500.0 : k <= 128 ? 5000.0 : kSysCellNs; }
 constexpr double kSysPairNs = 300.0;      // mixed-cell pair step incl. no-op halves and group imbalance (tuned)
 constexpr double kSysRunPairNs = 186.0;   // single-item-run pair step (wave trace)
+constexpr double sys_run_pair_ns(int k) { return k <= 64 ? 230.0 : kSysRunPairNs; }
 // split_run > 0: an item's run counts at most split_run ratings (hot-item replicas).
 std::vector<int32_t> choose_block_groups(const RatingBlocks& rb, const SideLayout& I, int32_t c, int32_t shard,
-                                         int32_t waves, int32_t split_run = 0, double cell_ns = kSysCellNs);
+                                         int32_t waves, int32_t split_run = 0, double cell_ns = kSysCellNs,
+                                         double run_ns = kSysRunPairNs);
 // The same model on per-block rating counts and most-rated-item counts (size / top, n*n each,
 // shard blocks only; e.g. from device histograms, kernels_plan.hip device_block_tops).
 std::vector<int32_t> choose_block_groups(const std::vector<int64_t>& size, const std::vector<int64_t>& top, int32_t nb,
-                                         int32_t c, int32_t shard, int32_t waves, double cell_ns = kSysCellNs);
+                                         int32_t c, int32_t shard, int32_t waves, double cell_ns = kSysCellNs,
+                                         double run_ns = kSysRunPairNs);
 
 }  // namespace mfhip

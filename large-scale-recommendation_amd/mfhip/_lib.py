@@ -157,9 +157,9 @@ def lib() -> C.CDLL:
         "mf_learning_rate": (C.c_int, [C.c_int, C.c_double, C.c_int32, C.c_double, C.c_double, _f64p]),
         "mf_debug_levels": (C.c_int, [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), _i32p, C.c_int64, _i32p]),
         "mf_debug_fast_schedule": (C.c_int, [_i32p, _i32p, C.c_int64, C.c_int32, C.c_int64, C.c_int32, C.c_int32,
-                                             C.c_int32, _i32p, _i32p, _i32p, _i64p]),
+                                             C.c_int32, C.c_int32, _i32p, _i32p, _i32p, _i64p]),
         "mf_debug_fast_split": (C.c_int, [_i32p, _i32p, C.c_int64, C.c_int32, C.c_int64, C.c_int32, C.c_int32,
-                                          C.c_int32, C.c_int32, _i32p, _i32p, _i32p, _i64p, _i32p]),
+                                          C.c_int32, C.c_int32, C.c_int32, _i32p, _i32p, _i32p, _i64p, _i32p]),
         "mf_fast_plan_window": (C.c_int, [C.c_int32, _i32p]),
         "mf_fast_kernel_name": (C.c_char_p, [C.c_int32]),
         "mf_get_params": (C.c_int, [C.c_void_p, C.POINTER(mf_params)]),

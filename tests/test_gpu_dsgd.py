@@ -259,7 +259,7 @@ def test_edge_cases():
 def fast_replay_reference(d, k, nb, seed, G, iterations, lam, lr):
     """Serialise the fast plan (superstep, sub-step, group, position) and replay it in f64."""
     from test_schedule import fast_plan_window, fast_schedule
-    b, t, g, p = fast_schedule(d.u, d.i, nb, seed, G, window=fast_plan_window(k))
+    b, t, g, p = fast_schedule(d.u, d.i, nb, seed, G, window=fast_plan_window(k), k=k)
     uids = np.unique(d.u); iids = np.unique(d.i)
     urow = np.searchsorted(uids, d.u).astype(np.int32)
     irow = np.searchsorted(iids, d.i).astype(np.int32)
@@ -281,7 +281,7 @@ def fast_split_replay_reference(d, k, nb, seed, G, iterations, lam, lr, split):
     copy of its item's row, takes its chain of updates, and the item ends as the mean of its R
     chains (plan.hpp SplitItem)."""
     from test_schedule import fast_plan_window, fast_schedule_split
-    b, t, g, p, rep = fast_schedule_split(d.u, d.i, nb, seed, G, split, window=fast_plan_window(k))
+    b, t, g, p, rep = fast_schedule_split(d.u, d.i, nb, seed, G, split, window=fast_plan_window(k), k=k)
     uids = np.unique(d.u); iids = np.unique(d.i)
     urow = np.searchsorted(uids, d.u).astype(np.int32)
     irow = np.searchsorted(iids, d.i).astype(np.int32)

@@ -55,22 +55,22 @@ def fast_plan_window(k):
     return w.value
 
 
-def fast_schedule(u, i, nb, seed, G, blocking=L.BLOCKING_REFERENCE, window=0):
+def fast_schedule(u, i, nb, seed, G, blocking=L.BLOCKING_REFERENCE, window=0, k=128):
     n = len(u)
     b = np.empty(n, np.int32); t = np.empty(n, np.int32); g = np.empty(n, np.int32); p = np.empty(n, np.int64)
     L.check(L.lib().mf_debug_fast_schedule(L.ptr(L.as_i32(u), C.c_int32), L.ptr(L.as_i32(i), C.c_int32), n, nb,
-                                           seed, G, blocking, window, L.ptr(b, C.c_int32), L.ptr(t, C.c_int32), L.ptr(g, C.c_int32),
+                                           seed, G, blocking, window, k, L.ptr(b, C.c_int32), L.ptr(t, C.c_int32), L.ptr(g, C.c_int32),
                                            L.ptr(p, C.c_int64)))
     return b, t, g, p
 
 
-def fast_schedule_split(u, i, nb, seed, G, item_split, blocking=L.BLOCKING_REFERENCE, window=0):
+def fast_schedule_split(u, i, nb, seed, G, item_split, blocking=L.BLOCKING_REFERENCE, window=0, k=128):
     """fast_schedule plus the hot-item replica each rating updates (0 = the item's own row)."""
     n = len(u)
     b = np.empty(n, np.int32); t = np.empty(n, np.int32); g = np.empty(n, np.int32); p = np.empty(n, np.int64)
     r = np.empty(n, np.int32)
     L.check(L.lib().mf_debug_fast_split(L.ptr(L.as_i32(u), C.c_int32), L.ptr(L.as_i32(i), C.c_int32), n, nb,
-                                        seed, G, blocking, window, item_split, L.ptr(b, C.c_int32),
+                                        seed, G, blocking, window, k, item_split, L.ptr(b, C.c_int32),
                                         L.ptr(t, C.c_int32), L.ptr(g, C.c_int32), L.ptr(p, C.c_int64),
                                         L.ptr(r, C.c_int32)))
     return b, t, g, p, r

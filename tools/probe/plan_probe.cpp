@@ -60,7 +60,7 @@ int main(int argc, char** argv) {
       const int c = nb / G;
       std::vector<int32_t> Gall(static_cast<size_t>(nb) * nb, 0);
       for (int g = 0; g < G; ++g) {
-        const auto gb = choose_block_groups(rb, I, c, g, waves, 0, sys_cell_ns(k));
+        const auto gb = choose_block_groups(rb, I, c, g, waves, 0, sys_cell_ns(k), sys_run_pair_ns(k));
         for (size_t b = 0; b < gb.size(); ++b) if (gb[b] > 0) Gall[b] = gb[b];
       }
       FastPlan fp;
@@ -89,7 +89,7 @@ int main(int argc, char** argv) {
     }
     return 0;
   }
-  const auto Gb = choose_block_groups(rb, I, nb, 0, waves, 0, sys_cell_ns(k));
+  const auto Gb = choose_block_groups(rb, I, nb, 0, waves, 0, sys_cell_ns(k), sys_run_pair_ns(k));
   std::printf("block groups %.3f s\n", lap());
   FastPlan fp;
   build_fast_plan(fp, rb, U, I, 128, k, 1.0, 0 * 0x9E3779B97F4A7C15ULL + 1, static_cast<uint32_t>(U.rows()), nullptr,

@@ -32,7 +32,7 @@ blk = np.empty(n, np.int32); sub = np.empty(n, np.int32); grp = np.empty(n, np.i
 win = C.c_int32()
 L.lib().mf_fast_plan_window(k, C.byref(win))
 P = lambda x, t: x.ctypes.data_as(C.POINTER(t))
-rc = L.lib().mf_debug_fast_schedule(P(tu, C.c_int32), P(ti, C.c_int32), n, nb, 0, a.groups, 0, win.value,
+rc = L.lib().mf_debug_fast_schedule(P(tu, C.c_int32), P(ti, C.c_int32), n, nb, 0, a.groups, 0, win.value, k,
                                     P(blk, C.c_int32), P(sub, C.c_int32), P(grp, C.c_int32), P(pos, C.c_int64))
 assert rc == 0, L.lib().mf_last_error()
 G = a.groups
