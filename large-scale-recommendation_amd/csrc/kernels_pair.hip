@@ -453,10 +453,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   // superstep's waves from lbase on (progress words and SysWave::nbr count from the superstep's
   // first wave).
   // place (host-made, sys_placement): the same XCD ranges, permuted inside an XCD so that the
-  // heaviest waves get the CUs with the fewest other waves (blocks k, k+32, k+64 of an XCD share a CU)
+  // heaviest waves get the CUs with the fewest other waves (blocks k, k+32, k+64 of an XCD share a CU);
+  // with empty blocks (-1) the heaviest wave of each XCD has its CU to itself (nw counts them too)
   const int b = static_cast<int>(blockIdx.x);
   const int x = b % 8, per = nw / 8, extra = nw % 8;
   const int L = place ? place[b] : x * per + min(x, extra) + b / 8;
+  if (L < 0) return;  // an empty block of the placement (it only keeps a heavy wave's CU to itself)
   const SysWave w = sw[L];
   const WaveDesc* my = sys + w.cell0;
   int32_t* my_prog = prog + static_cast<int64_t>(lbase + L) * kProgStride;

@@ -108,6 +108,8 @@ struct Shard {
   std::vector<WaveDesc> st_waves_host;  // kept only when tracing
   DevBuf st_sys, st_sysw;               // systolic pair tables (PairPlan::sys, sys_waves)
   DevBuf st_place;                      // per systolic wave slot: block -> wave of its launch (sys_placement)
+  std::vector<int64_t> st_place_off;     // per superstep: its first slot in st_place (nb + 1)
+  std::vector<int32_t> st_place_pad;     // per superstep: empty blocks per XCD in its launch (sys_placement)
   std::vector<int64_t> st_sys_off;      // PairPlan::sys_off
   std::vector<WaveDesc> st_sys_host;    // kept only when tracing
   std::vector<SysWave> st_sysw_host;    // kept only when tracing
@@ -688,8 +690,15 @@ void det_superstep(mf_ctx* ctx, Shard& s, int64_t superstep, int32_t iteration, 
 // identical (tests compare with the per-sub-step launches bit for bit).  MFHIP_SYS_PLACE=0: the
 // plain XCD-contiguous map.  Measured and dropped: per-CU wave counts chosen against a crowding
 // factor (1 / 1.3 / 1.52 / 1.8 per waves on the CU), spare slots padded with empty blocks -- NFLX
-// 21.6 vs 21.3 ms, ML20M equal (profiles/r03_placement_NFLX.txt).
-void sys_placement(const PairPlan& pp, int64_t w0, int64_t a, int64_t z, std::vector<int32_t>& place) {
+// 21.6 vs 21.3 ms, ML20M equal (profiles/r03_placement_NFLX.txt).  Kept since round 6: one empty
+// block per XCD as the heaviest wave's partner, so each rating block's hot-item wave has a CU to
+// itself (NFLX 19.88 -> 19.74 ms, profiles/r06_sys_isolation_ab.txt; single-run pairs now weigh
+// 185 ns: at 171 the hot wave sometimes ranked 16th-54th of its XCD).
+// pad (>= 0): empty blocks per XCD (place = -1, they exit at once), dealt as the lightest partners:
+// the heaviest wave of each XCD then shares its CU with empty blocks only -- alone on it when pad
+// covers its CU's other slots (sys_iso_pad).  place gets nw + 8 pad entries from out on.
+void sys_placement(const PairPlan& pp, int64_t w0, int64_t a, int64_t z, std::vector<int32_t>& place, int64_t out,
+                   int32_t pad = 0) {
   const int64_t nw = z - a;
   if (nw <= 0) return;
   std::vector<double> load(nw, 0.0);
@@ -697,16 +706,18 @@ void sys_placement(const PairPlan& pp, int64_t w0, int64_t a, int64_t z, std::ve
     const SysWave& sw = pp.sys_waves[w0 + a + L];
     for (int32_t t = 0; t < sw.G; ++t) {
       const WaveDesc& d = pp.sys[sw.cell0 + t];
-      if (d.steps > 0) load[L] += 2000.0 + d.steps * (d.cells == kWaveSingleRun || d.cells == kWaveSingleRunFwd ? 171.0 : 218.0);
+      if (d.steps > 0) load[L] += 2000.0 + d.steps * (d.cells == kWaveSingleRun || d.cells == kWaveSingleRunFwd ? 185.0 : 218.0);
     }
   }
   const int64_t per = nw / 8, extra = nw % 8;
   for (int64_t x = 0; x < 8; ++x) {
-    const int64_t n = per + (x < extra ? 1 : 0), base = x * per + std::min(x, extra);
-    if (n == 0) continue;
-    std::vector<int64_t> byload(n);  // this XCD's waves, heaviest first
-    std::iota(byload.begin(), byload.end(), base);
-    std::stable_sort(byload.begin(), byload.end(), [&](int64_t u, int64_t v) { return load[u] > load[v]; });
+    const int64_t nx = per + (x < extra ? 1 : 0), base = x * per + std::min(x, extra);
+    if (nx == 0) continue;
+    const int64_t n = nx + pad;  // this XCD's blocks
+    std::vector<int64_t> byload(n);  // this XCD's waves, heaviest first, then the empty blocks (-1)
+    std::iota(byload.begin(), byload.begin() + nx, base);
+    std::fill(byload.begin() + nx, byload.end(), -1);
+    std::stable_sort(byload.begin(), byload.begin() + nx, [&](int64_t u, int64_t v) { return load[u] > load[v]; });
     std::vector<int64_t> cus(std::min<int64_t>(n, 32));  // CU slots, fewest waves first
     std::iota(cus.begin(), cus.end(), 0);
     auto members = [&](int64_t c) { return (n - c + 31) / 32; };
@@ -714,8 +725,20 @@ void sys_placement(const PairPlan& pp, int64_t w0, int64_t a, int64_t z, std::ve
     int64_t hi = 0, lo = n - 1;
     for (int64_t c : cus)
       for (int64_t kk = c, m = 0; kk < n; kk += 32, ++m)
-        place[w0 + a + x + 8 * kk] = static_cast<int32_t>(m == 0 ? byload[hi++] : byload[lo--]);
+        place[out + x + 8 * kk] = static_cast<int32_t>(m == 0 ? byload[hi++] : byload[lo--]);
   }
+}
+
+// Empty blocks per XCD that leave the `iso` heaviest waves of every XCD alone on their CUs: iso x
+// (the fewest blocks a CU slot holds - 1) once the XCD holds nw / 8 + pad blocks; 0 when the launch
+// could not hold them all at once (cap).
+int32_t sys_iso_pad(int64_t nw, int64_t cap, int32_t iso) {
+  for (int32_t pad = 0; pad <= 3 * iso; ++pad) {
+    const int64_t n = (nw + 7) / 8 + pad;  // the fullest XCD's blocks (a smaller XCD needs no more)
+    const int64_t fewest = n <= 32 ? 1 : n / 32;  // blocks of its emptiest CU slot
+    if (iso * (fewest - 1) <= pad) return nw + 8 * pad <= cap ? pad : 0;
+  }
+  return 0;
 }
 
 void fast_superstep(mf_ctx* ctx, Shard& s, int64_t superstep, double eta) {
@@ -738,12 +761,15 @@ void fast_superstep(mf_ctx* ctx, Shard& s, int64_t superstep, double eta) {
     auto sweep = [&](hipStream_t st, int64_t a, int64_t z) {  // waves [a, z) of the superstep
       if (z <= a) return;
       LaunchTimer tm(s, ctx->profiling, true);
-      launch_sweep_pair_sys(st, s.st_sysw.as<SysWave>() + w0 + a, s.st_sys.as<WaveDesc>(), static_cast<int>(z - a),
+      // with a placement table the launch has its empty blocks too (sys_placement pad)
+      const bool placed = s.st_place.get() != nullptr;
+      const int64_t blocks = z - a + (placed && a == 0 && z == nw ? 8 * s.st_place_pad[smod] : 0);
+      launch_sweep_pair_sys(st, s.st_sysw.as<SysWave>() + w0 + a, s.st_sys.as<WaveDesc>(), static_cast<int>(blocks),
                             static_cast<int>(a), s.st_recs.as<PairRec>(), s.uf.as<float>(), s.itf.as<float>(),
                             s.uf.bytes(), s.itf.bytes(), ctx->P.num_factors, static_cast<float>(eta),
                             s.fast_prog.as<int32_t>(), s.sys_base, s.fast_err.as<int32_t>(),
                             s.st_trace.get() ? s.st_trace.as<uint64_t>() : nullptr, tm.start(), tm.stop(),
-                            s.st_place.get() ? s.st_place.as<int32_t>() + w0 + a : nullptr);
+                            placed ? s.st_place.as<int32_t>() + s.st_place_off[smod] + a : nullptr);
       ctx->stats.kernel_launches += 1;
     };
     if (ctx->ring_overlap) {
@@ -1523,6 +1549,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
     ctx->fast_pair = fk == FastKernel::kPair;
     ctx->fast_sys = false;
     std::vector<int32_t> block_groups;  // systolic sweep, automatic G: one G_j per rating block
+    int64_t sys_cap = 0;                // blocks of one systolic launch that can be resident at once
     if (ctx->fast_pair && want_pair_sys()) {
       int cap = 1 << 30, simds = 1 << 30;
       for (auto& s : ctx->shards) {
@@ -1561,6 +1588,7 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
       // (the one-GPU rehearsal of the ring), all of theirs together
       if (const char* v = std::getenv("MFHIP_DEVICE_SHARERS"))
         if (ctx->rank_mode && std::atoi(v) > 1) cap /= std::atoi(v);
+      sys_cap = cap;
       bool fits = cap > 0;
       for (int32_t sm = 0; sm < ctx->nb && fits; ++sm) {
         std::vector<std::pair<int, int64_t>> per_dev;  // (device, waves of superstep sm)
@@ -1710,16 +1738,45 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
           s.st_sys_off = pp.sys_off;
           s.st_sys_block_off = pp.sys_block_off;
           s.st_place.release();
+          s.st_place_off.assign(ctx->nb + 1, 0);
+          s.st_place_pad.assign(ctx->nb, 0);
           if (test_knob("sys_place") != "0" && !pp.sys_waves.empty()) {
-            std::vector<int32_t> place(pp.sys_waves.size(), 0);
+            // empty blocks isolate each XCD's heaviest wave (one launch per superstep, one shard:
+            // the co-residency check above counted this shard's waves alone); MFHIP_TEST sys_iso=N:
+            // its N heaviest (0: none)
+            int32_t iso = !ctx->ring_overlap && ctx->shards.size() == 1 ? 1 : 0;
+            if (const std::string v = test_knob("sys_iso"); !v.empty() && iso) iso = std::clamp(std::atoi(v.c_str()), 0, 8);
             for (int32_t sm = 0; sm < ctx->nb; ++sm) {
-              const int64_t w0 = pp.sys_off[sm], nw = pp.sys_off[sm + 1] - w0;
+              const int64_t nw = pp.sys_off[sm + 1] - pp.sys_off[sm];
+              s.st_place_pad[sm] = iso ? sys_iso_pad(nw, sys_cap, iso) : 0;
+              s.st_place_off[sm + 1] = s.st_place_off[sm] + nw + 8 * s.st_place_pad[sm];
+            }
+            std::vector<int32_t> place(static_cast<size_t>(s.st_place_off[ctx->nb]), 0);
+            for (int32_t sm = 0; sm < ctx->nb; ++sm) {
+              const int64_t w0 = pp.sys_off[sm], nw = pp.sys_off[sm + 1] - w0, out = s.st_place_off[sm];
               if (ctx->ring_overlap) {  // the two launches of fast_superstep
                 const int64_t split = pp.sys_block_off[static_cast<size_t>(sm) * (ctx->c + 1) + ctx->c - 1];
-                sys_placement(pp, w0, 0, split, place);
-                sys_placement(pp, w0, split, nw, place);
+                sys_placement(pp, w0, 0, split, place, out);
+                sys_placement(pp, w0, split, nw, place, out + split);
               } else {
-                sys_placement(pp, w0, 0, nw, place);
+                sys_placement(pp, w0, 0, nw, place, out, s.st_place_pad[sm]);
+              }
+              // per launch: every wave exactly once, the rest empty (a missing wave would stall its
+              // neighbours)
+              const int64_t cut = ctx->ring_overlap
+                                      ? pp.sys_block_off[static_cast<size_t>(sm) * (ctx->c + 1) + ctx->c - 1]
+                                      : nw;
+              for (const auto& [b0, len, waves] : {std::tuple<int64_t, int64_t, int64_t>{out, cut + 8 * s.st_place_pad[sm], cut},
+                                                   std::tuple<int64_t, int64_t, int64_t>{out + cut, nw - cut, nw - cut}}) {
+                std::vector<uint8_t> seen(static_cast<size_t>(waves), 0);
+                int64_t empty = 0;
+                for (int64_t b = b0; b < b0 + len; ++b) {
+                  const int32_t L = place[b];
+                  if (L < 0) { ++empty; continue; }
+                  MF_REQUIRE(L < waves && !seen[L], "systolic placement is not a permutation");
+                  seen[L] = 1;
+                }
+                MF_REQUIRE(empty == len - waves, "systolic placement: empty blocks miscounted");
               }
             }
             s.st_place.alloc(place.size() * sizeof(int32_t));
