@@ -730,13 +730,16 @@ void sys_placement(const PairPlan& pp, int64_t w0, int64_t a, int64_t z, std::ve
 }
 
 // Empty blocks per XCD that leave the `iso` heaviest waves of every XCD alone on their CUs: iso x
-// (the fewest blocks a CU slot holds - 1) once the XCD holds nw / 8 + pad blocks; 0 when the launch
-// could not hold them all at once (cap).
+// (the fewest blocks a CU slot holds - 1) once the XCD holds nw / 8 + pad blocks.  0 when the
+// launch could not hold them all at once (cap), or when the padding would put one more wave on the
+// fullest CUs (YAHOO, 126 waves per XCD: pad 3 makes a five-wave CU, 236.6 -> 270 ms per epoch).
 int32_t sys_iso_pad(int64_t nw, int64_t cap, int32_t iso) {
+  const int64_t n0 = (nw + 7) / 8;  // the fullest XCD's waves (a smaller XCD needs no more)
   for (int32_t pad = 0; pad <= 3 * iso; ++pad) {
-    const int64_t n = (nw + 7) / 8 + pad;  // the fullest XCD's blocks (a smaller XCD needs no more)
+    const int64_t n = n0 + pad;
     const int64_t fewest = n <= 32 ? 1 : n / 32;  // blocks of its emptiest CU slot
-    if (iso * (fewest - 1) <= pad) return nw + 8 * pad <= cap ? pad : 0;
+    if (iso * (fewest - 1) <= pad)
+      return nw + 8 * pad <= cap && (n + 31) / 32 == (n0 + 31) / 32 ? pad : 0;
   }
   return 0;
 }
@@ -1743,8 +1746,9 @@ void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, i
           if (test_knob("sys_place") != "0" && !pp.sys_waves.empty()) {
             // empty blocks isolate each XCD's heaviest wave (one launch per superstep, one shard:
             // the co-residency check above counted this shard's waves alone); MFHIP_TEST sys_iso=N:
-            // its N heaviest (0: none)
-            int32_t iso = !ctx->ring_overlap && ctx->shards.size() == 1 ? 1 : 0;
+            // its N heaviest (0: none).  Default: k <= 128 (NFLX -0.7%, ML20M even; YAHOO's four-wave
+            // CUs lose 0.3% to the slots the empty blocks take, profiles/r06_sys_isolation_ab.txt)
+            int32_t iso = !ctx->ring_overlap && ctx->shards.size() == 1 && k <= 128 ? 1 : 0;
             if (const std::string v = test_knob("sys_iso"); !v.empty() && iso) iso = std::clamp(std::atoi(v.c_str()), 0, 8);
             for (int32_t sm = 0; sm < ctx->nb; ++sm) {
               const int64_t nw = pp.sys_off[sm + 1] - pp.sys_off[sm];
