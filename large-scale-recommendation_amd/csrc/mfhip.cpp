@@ -64,6 +64,7 @@ struct DetBuf {
   hipEvent_t copied = nullptr;  // the H2D from `pin` finished (pin may be rewritten)
   hipEvent_t swept = nullptr;   // the sweep that read `dev` finished (dev may be rewritten)
   bool pending = false;         // `copied` was recorded and not yet waited for
+  bool dev_built = false;       // det_build left only the shuffle here: the device builds the entries
   int64_t n = 0, nw = 0;
   DetStepScratch scratch;  // build_det_step's gathers for this slot (kept: no page faults per superstep)
 };
@@ -171,6 +172,10 @@ struct mf_ctx {
   bool det_sweep = false;         // deterministic mode: one persistent k_det_sweep launch per superstep
   bool det_split = false;         // ... with single-item chains split over two waves (k_det_sweep_split)
   bool det_dev_build = false;     // ... its input built on the device from the host's shuffle (det_device_build)
+  bool det_dev_ready = false;     // ... the device build prepared (the switch below may turn it on)
+  bool det_mixed = false;         // ... MFHIP_TEST det_build=mixed: switch from the third superstep on
+  std::atomic<bool> det_switch{false};  // ... the host builds fell behind the device: device builds from now on
+  int det_idle = 0;               // ... consecutive supersteps whose build the device had to wait for
   bool det_alone = true;          // ... the longest chains on CUs of their own (det_slot_table)
   int64_t det_split_blocks = 0;   // resident blocks of k_det_sweep_split (per device share)
   int64_t det_cu_period = 256;    // CUs of the device: blocks b and b + period share a CU
@@ -1087,13 +1092,14 @@ void det_build(mf_ctx* ctx, int64_t superstep, int slot) {
     }
   } done{t_build};
   std::vector<int64_t> blocks, seeds;
-  if (ctx->det_dev_build) {
+  if (ctx->det_dev_build || ctx->det_switch.load(std::memory_order_acquire)) {
     // the device builds the entries (det_run): here only each block's JVM shuffle, written as the
     // uploaded permutation, and the superstep index's fixed slot table
     const int64_t sm = (superstep - 1) % ctx->nb;
     for (auto& s : ctx->shards) {
       DetBuf& db = s.det_buf[slot];
       det_blocks(ctx, s, superstep, blocks, seeds);
+      db.dev_built = true;
       db.n = s.det_sm_n[sm];
       db.nw = static_cast<int64_t>(s.det_sm_slots[sm].size());
       if (db.n == 0) continue;
@@ -1118,6 +1124,7 @@ void det_build(mf_ctx* ctx, int64_t superstep, int slot) {
   for (auto& s : ctx->shards) {
     DetBuf& db = s.det_buf[slot];
     det_blocks(ctx, s, superstep, blocks, seeds);
+    db.dev_built = false;
     db.n = db.nw = 0;
     for (int64_t b : blocks) {
       db.n += ctx->rb.size(b);
@@ -1186,6 +1193,26 @@ void det_run(mf_ctx* ctx, int64_t count) {
       builds[slot].get();  // every superstep of the run has a build (taken over or started here)
       wait_build_ns += since(t);
     }
+    // auto mode: when the device has already finished the previous superstep twice in a row by the
+    // time its host build is done, the host is the bottleneck (a busy or small host): from then on
+    // the builds leave the gather / sorts / scatter to the device (det_device_build), whose host
+    // part is the shuffle alone.  Either build gives the same entries, so the factors do not change.
+    if (ctx->det_dev_ready && !ctx->det_dev_build && !ctx->det_switch.load() && x >= 2) {
+      bool idle = true;
+      for (auto& sh : ctx->shards) {
+        const DetBuf& pb = sh.det_buf[(slot + kDetSlots - 1) % kDetSlots];
+        if (pb.n == 0) continue;
+        DeviceGuard g(sh.device);
+        idle = idle && hipEventQuery(pb.swept) == hipSuccess;
+      }
+      ctx->det_idle = idle || ctx->det_mixed ? ctx->det_idle + 1 : 0;
+      if (ctx->det_idle >= 2) {
+        ctx->det_switch.store(true, std::memory_order_release);
+        if (g_det_timing)
+          std::fprintf(stderr, "[mfhip] det_run: host builds fell behind at superstep %lld: device builds from now on\n",
+                       static_cast<long long>(s));
+      }
+    }
     const int32_t iteration = static_cast<int32_t>(s / ctx->nb);  // :476
     const double eta = learning_rate(ctx->P.lr_method, ctx->P.learning_rate, iteration + 1, ctx->P.lambda,
                                      ctx->P.lr_arg);  // :383-386
@@ -1199,7 +1226,7 @@ void det_run(mf_ctx* ctx, int64_t count) {
       // staging copy on the copy stream, after the sweep that last read this buffer (s-3), so it
       // overlaps the sweeps still running on the compute stream
       MF_HIP(hipStreamWaitEvent(sh.copy_stream, db.swept, 0));
-      if (ctx->det_dev_build) {
+      if (db.dev_built) {
         // the slot table and the shuffle permutation go up; the entries are built on the device
         // (det_device_build), on the same stream
         const int64_t sm = (s - 1) % ctx->nb;
@@ -1490,10 +1517,17 @@ void prepare_det_sweep(mf_ctx* ctx) {
   ctx->det_split_blocks = cap / 2;
   ctx->det_alone = test_knob("det_alone") != "0";
   ctx->det_cu_period = device_cu_count(ctx->shards[0].device);
-  // MFHIP_TEST det_build=device: the sweep's input built on the device (measured slower, see
-  // profiles/r06_det_device_build_ab.txt: the build's traffic slows the running chain)
-  ctx->det_dev_build = test_knob("det_build") == "device";
-  if (ctx->det_dev_build) prepare_det_device_build(ctx);
+  // The sweep's input is built on the host while the device keeps up with it; the device build
+  // (4% slower on a free host: its traffic slows the running chain, profiles/r06_det_device_build_ab.txt)
+  // takes over when the host falls behind (det_run).  MFHIP_TEST det_build=device / host: always
+  // that one; mixed: the switch from the third superstep on (tests).
+  const std::string dbk = test_knob("det_build");
+  ctx->det_dev_build = dbk == "device";
+  ctx->det_dev_ready = dbk != "host";
+  ctx->det_mixed = dbk == "mixed";
+  ctx->det_switch = false;
+  ctx->det_idle = 0;
+  if (ctx->det_dev_ready) prepare_det_device_build(ctx);
 }
 
 void prepare(mf_ctx* ctx, const int32_t* u, const int32_t* i, const double* r, int64_t n) {

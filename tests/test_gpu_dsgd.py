@@ -546,7 +546,7 @@ def test_systolic_per_block_groups_equal_their_schedule(monkeypatch, k, nb, wave
     np.testing.assert_allclose(a_i, I, rtol=2e-4, atol=2e-5)
 
 
-@pytest.mark.parametrize("build", ["device", "host"])
+@pytest.mark.parametrize("build", ["device", "host", "mixed"])
 @pytest.mark.parametrize("split", ["1", "0"])
 @pytest.mark.parametrize("k,nb,shards", [(64, 4, 1), (128, 4, 2), (100, 3, 1), (256, 2, 2)])
 def test_deterministic_persistent_sweep_bit_exact_hot_items(monkeypatch, k, nb, shards, split, build):
@@ -555,7 +555,8 @@ def test_deterministic_persistent_sweep_bit_exact_hot_items(monkeypatch, k, nb, 
     same-item runs kept in registers) and heavy users (long ticket chains), on 1 or 2 shards.
     split=1 (default, k = 64/128/256): single-item chains run as a chain wave + a helper wave
     (k_det_sweep_split); split=0: one wave each (k_det_sweep2).  build: the superstep's entries
-    built on the device from the host's shuffle (det_device_build) or on the host (build_det_step)."""
+    built on the device from the host's shuffle (det_device_build), on the host (build_det_step), or
+    on the host and then, from the third superstep on, on the device (the auto mode's switch)."""
     set_knob(monkeypatch, "det_split", split)
     set_knob(monkeypatch, "det_build", build)
     d = hot_item_data(k)
