@@ -382,9 +382,10 @@ constexpr double kSysCellNs = 6000.0;     // per-cell start, drain, hand-off and
 // ML20M 4.65 -> 4.49 ms, NFLX 20.03 -> 19.97 ms at 5 us); k = 256 keeps 6 us (its 5-us schedule moves
 // YAHOO@0.05's RMSE past the 0.5% gate).
 // Round 6, with the record preload at k = 64 (profiles/r06_ML20M_cell_ab.txt): k = 64 re-swept to
-// 3.5 us per cell and 230 ns per run pair (ML20M 4.26 -> 4.13 ms); NFLX stays at 5 us / 186 ns
-// (210 / 230 / 170 / 155 ns: 20.45 / 21.17 / 20.23 / 21.20 ms against 19.87).
-constexpr double sys_cell_ns(int k) { return k <= 64 ? 3500.0 : k <= 128 ? 5000.0 : kSysCellNs; }
+// 3.5 us per cell and 230 ns per run pair (ML20M 4.26 -> 4.13 ms); NFLX keeps 186 ns (210 / 230 /
+// 170 / 155 ns: 20.45 / 21.17 / 20.23 / 21.20 ms against 19.87) and, with the CU isolation, 4.5 us
+// per cell (19.47 / 19.43 ms against 19.73 / 19.45 at 5 us; 5.5 / 4 us: 19.77 / 19.76, 19.76 / 19.71).
+constexpr double sys_cell_ns(int k) { return k <= 64 ? 3500.0 : k <= 128 ? 4500.0 : kSysCellNs; }
 constexpr double kSysPairNs = 300.0;      // mixed-cell pair step incl. no-op halves and group imbalance (tuned)
 constexpr double kSysRunPairNs = 186.0;   // single-item-run pair step (wave trace)
 constexpr double sys_run_pair_ns(int k) { return k <= 64 ? 230.0 : kSysRunPairNs; }
